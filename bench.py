@@ -1,0 +1,263 @@
+"""bench.py -- frames/sec of one training step (fwd + bwd + update) of the
+BASELINE stack Conv(40x11x3, 8x1, 128) -> Maxpool(1x1x4) -> FC(11616 -> 1024)
+on MI355X through libkcnn.so, plus the dominant hot-path kernel's roofline
+fraction (HIP events over the timed region) and the CPU oracle timed on the
+host beside it.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-gpu B]
+
+N > 1 runs under torch.distributed.run, one process per GPU: the minibatch is
+row-sharded (weak scaling, B frames per GPU), gradients are computed per
+component and all-reduced over RCCL (sum, fp32) while the lower layers
+backpropagate, then every replica applies the same update with
+lr / (B * N).  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kaldi-cnn_amd"))
+
+# BASELINE.json configs[1] (c2).
+H, W, C, KH, KW, G, PC, FC_OUT = 40, 11, 3, 8, 1, 128, 4, 1024
+OH, OW = H - KH + 1, W - KW + 1
+P = OH * OW
+POOL_OUT = P * G // PC
+PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 matrix (dense)
+
+# Algorithmic work per frame (SURVEY 8d / BASELINE.md 3).
+CONV_FLOP_PER_PASS = 2 * P * G * KH * KW * C          # 2,230,272
+CONV_BYTES_PER_PASS = 4 * (H * W * C + P * G)         # 191,136
+POOL_FWD_BYTES = 4 * (P * G + POOL_OUT)               # 232,320
+POOL_BWD_BYTES = 4 * (2 * P * G + 2 * POOL_OUT)       # 464,640
+FC_FLOP = 3 * 2 * POOL_OUT * FC_OUT                   # 71,368,704
+
+
+def stack_config():
+    return "\n".join([
+        f"ConvolutionComponent in-height={H} in-width={W} in-channel={C} "
+        f"kernel-height={KH} kernel-width={KW} stride=1 group={G} out-height={OH} "
+        f"out-width={OW} learning-rate=0.02 param-stddev=0.01 bias-stddev=0.5 "
+        f"weight-decay=0.0002 momentum=0.9",
+        f"MaxpoolComponent in-height={OH} in-width={OW} in-channel={G} "
+        f"pool-height-dim=1 pool-width-dim=1 pool-channel-dim={PC}",
+        f"FullyConnectedComponent input-dim={POOL_OUT} output-dim={FC_OUT} "
+        f"learning-rate=0.02 param-stddev=0.01 bias-stddev=1 weight-decay=0.0002 "
+        f"momentum=0.9",
+    ])
+
+
+def parse_profile(text):
+    out = {}
+    for line in text.strip().splitlines():
+        parts = line.split("\t")
+        if len(parts) >= 3:
+            out[parts[0]] = (float(parts[1].split()[0]), int(parts[2].split()[0]))
+    return out
+
+
+def cpu_baseline(frames_hint, budget_s=12.0):
+    """The CPU oracle (restated reference CPU path) on a bounded sample."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    O.set_threads(threads)
+    r = np.random.default_rng(1)
+
+    def one_step(n):
+        oc = O.Conv(H, W, C, KH, KW, G)
+        oc.W = (r.standard_normal((KH * KW * C, G)) * 0.01).astype(np.float32)
+        oc.b = (r.standard_normal(G) * 0.5).astype(np.float32)
+        op = O.Pool(OH, OW, G, 1, 1, PC)
+        of = O.FC(POOL_OUT, FC_OUT)
+        of.W = (r.standard_normal((FC_OUT, POOL_OUT)) * 0.01).astype(np.float32)
+        of.b = np.ones(FC_OUT, np.float32)
+        x = r.standard_normal((n, H * W * C)).astype(np.float32)
+        dy = (r.standard_normal((n, FC_OUT)) * 1e-2).astype(np.float32)
+        t0 = time.perf_counter()
+        y1 = oc.propagate(x)
+        y2 = op.propagate(y1)
+        of.propagate(y2)
+        d2 = of.backprop(y2, dy, update=True)
+        d1 = op.backprop(y1, y2, d2)
+        oc.backprop(x, d1, update=True)
+        return time.perf_counter() - t0
+
+    t_small = one_step(8)
+    n = int(max(8, min(frames_hint, 8 * budget_s / max(t_small, 1e-3))))
+    n = max(8, (n // 8) * 8)
+    t = one_step(n)
+    return {"value": round(n / t, 2), "unit": "frames/sec", "cores": threads,
+            "kind": "port",
+            "sample": f"{n} frames of the c2 stack, one fwd+bwd+update step, "
+                      f"C oracle (oracle/kcnn_oracle.c) with {threads} OpenMP threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--frames-per-gpu", type=int, default=4096)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--json-out", default=None)
+    args = ap.parse_args()
+
+    import torch
+    import kcnn
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    kcnn.init(local_rank)
+    kcnn.set_randn_seed(20261015)  # identical initial params on every replica
+
+    B = args.frames_per_gpu
+    net = kcnn.Nnet(stack_config())
+    conv, pool, fc = net.components
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(20261015 + rank)  # each rank its own shard of frames
+    x = torch.randn((B, H * W * C), generator=gen, device="cuda")
+    dy = torch.randn((B, FC_OUT), generator=gen, device="cuda") * 1e-2
+
+    grads = {i: torch.empty(c.NumGradientParams(), device="cuda")
+             for i, c in enumerate(net.components) if c.NumGradientParams() > 0}
+
+    def step():
+        net.Propagate(x)
+        if world == 1:
+            net.Backprop(dy)                     # reference semantics: update in Backprop
+            return
+        pending = []
+        for i in reversed(range(net.NumComponents())):
+            if i in grads:
+                net.BackpropComponent(i, dy, mode=1, grad=grads[i], skip_first_dx=False)
+                pending.append((i, dist.all_reduce(grads[i], async_op=True)))
+            else:
+                net.BackpropComponent(i, dy, mode=2, skip_first_dx=False)
+        for i, work in pending:
+            work.wait()
+            net.components[i].ApplyGradient(grads[i], B * world)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kcnn.set_profiling(True)
+    kcnn.profile_string()  # drain/reset
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kcnn.set_profiling(False)
+    prof = parse_profile(kcnn.profile_string())
+    if dist:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    frames = B * world * args.steps
+    value = frames / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # Per-kernel averages (HIP events around each launch, timed region).
+    def avg(key):
+        ms, n = prof.get(key, (0.0, 0))
+        # cumulative counts include warm-up-free timed steps only
+        return (ms / n) if n else None
+
+    k_fwd = avg("ConvolutionComponent::Propagate")
+    k_dgrad = avg("ConvolutionComponent::BackpropData")
+    k_wgrad = avg("ConvolutionComponent::ComputeGradient")
+    k_pool_f = avg("MaxpoolComponent::Propagate")
+    k_pool_b = avg("MaxpoolComponent::Backprop")
+    k_fc = prof.get("AddMatMat", (0.0, 0))
+    kernels = {}
+    for name, ms, flop, byts in (
+            ("conv_fwd", k_fwd, CONV_FLOP_PER_PASS * B, CONV_BYTES_PER_PASS * B),
+            ("conv_dgrad", k_dgrad, CONV_FLOP_PER_PASS * B, CONV_BYTES_PER_PASS * B),
+            ("conv_wgrad", k_wgrad, CONV_FLOP_PER_PASS * B, CONV_BYTES_PER_PASS * B),
+            ("maxpool_fwd", k_pool_f, 0, POOL_FWD_BYTES * B),
+            ("maxpool_bwd", k_pool_b, 0, POOL_BWD_BYTES * B)):
+        if ms:
+            kernels[name] = {"ms": round(ms, 4),
+                             "GB/s": round(byts / ms / 1e6, 1),
+                             "hbm_frac": round(byts / ms / 1e6 / PEAK_HBM_GBS, 4),
+                             "TFLOP/s": round(flop / ms / 1e9, 2) if flop else None,
+                             "mfma_frac": round(flop / ms / 1e9 / PEAK_FP32_MFMA_TFLOPS, 4) if flop else None}
+    if k_fc[1]:
+        kernels["fc_gemms_rocblas"] = {
+            "ms_per_step": round(k_fc[0] / args.steps, 4),
+            "TFLOP/s": round(FC_FLOP * B / (k_fc[0] / args.steps) / 1e9, 2)}
+
+    # Dominant hand-written hot-path kernel by time.
+    dom = max((k for k in kernels if not k.startswith("fc")),
+              key=lambda k: kernels[k]["ms"], default=None)
+    roofline = None
+    if dom:
+        dk = kernels[dom]
+        conv_like = dom.startswith("conv")
+        byts = (CONV_BYTES_PER_PASS if conv_like else
+                POOL_FWD_BYTES if dom == "maxpool_fwd" else POOL_BWD_BYTES) * B
+        achieved = byts / dk["ms"] / 1e6
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roofline = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
+                    "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                    "algorithmic_bytes_per_launch": byts}
+
+    if rank == 0:
+        result = {
+            "metric": "frames/sec fwd+bwd, Conv+Maxpool+FC stack, 4096-frame batch @1/2/4/8 GPU",
+            "value": round(value, 1), "unit": "frames/sec", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: N(0,1) fbank-shaped frames, N(0,1)*1e-2 output derivative",
+            "config": {"workload": "c2: Conv(40x11x3, 8x1, 128) -> Maxpool(1x1x4) -> "
+                                   "FC(11616->1024), fwd+bwd+update",
+                       "frames_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"dp{world}"},
+            "roofline": roofline,
+            "kernels": kernels,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            result["cpu_baseline"] = cpu_baseline(B)
+        line = json.dumps(result)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,173 @@
+/*
+ * include/kcnn.h -- extern "C" entry points of libkcnn.so above the kernel
+ * shim (include/cnsl-hip-kernels.h): the CuMatrixBase extension methods and
+ * the nnet2 components, callable with plain device pointers + MatrixDim.
+ *
+ * Each entry replaces one reference interface:
+ *   kcnn_mat_*        CuMatrixBase<float>::{Conv2D, AddMatRepVec, FlipMat,
+ *                     PaddingZero, TpBlock, TpInsideBlock, ModPermuteRow,
+ *                     Maxpool_prop, Maxpool_backprop}
+ *                     (reference src/cudamatrix/cu-matrix.h:451-480;
+ *                     bodies src/cnslmat/conv2D.cc:43-684)
+ *   kcnn_component_*  nnet2::Component / UpdatableComponent virtuals as the
+ *                     nnet0 components override them
+ *                     (reference src/nnet0/nnet-component-nnet0.h:23-232,
+ *                     src/nnet2/nnet-component.h:157-348) and the factory
+ *                     Component::NewFromString / ReadNew
+ *                     (src/nnet2/nnet-component.cc:38-136)
+ *   kcnn_nnet_*       the propagate/backprop loop of upstream nnet2's
+ *                     NnetUpdater (not vendored by the reference)
+ *                     over a stack of these components.
+ *
+ * Conventions: every pointer argument to matrix data is DEVICE memory on the
+ * active HIP device; functions return 0 on success and a nonzero code on
+ * failure (KALDI_ASSERT / KALDI_ERR / HIP errors), with the message in
+ * kcnn_last_error().  Output matrices are caller-allocated with the sizes the
+ * reference methods would Resize() them to.  All work is enqueued on the
+ * stream set by kcnn_set_stream (default: the legacy NULL stream).
+ */
+#ifndef KCNN_KCNN_H_
+#define KCNN_KCNN_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "cnsl-hip-kernels.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- runtime ------------------------------------------------------------ */
+const char *kcnn_last_error(void);
+const char *kcnn_version(void);
+/* CuDevice::SelectGpuId(use_gpu, device) (upstream cu-device.h). */
+int kcnn_init(int device);
+int kcnn_set_stream(kcnn_stream_t stream);
+int kcnn_synchronize(void);
+int kcnn_set_literal_path(int literal);  /* replay reference call sequences */
+int kcnn_set_profiling(int on);
+/* Writes the per-function hipEvent profile (CuDevice::PrintProfile). */
+int kcnn_profile_string(char *buf, size_t len);
+void kcnn_set_randn_seed(uint64_t seed);
+/* Host-side self test of the FastDiv helper; no GPU needed. */
+int kcnn_selftest_fastdiv(void);
+
+/* ---- CuMatrixBase methods (cu-matrix.h:451-480) ---------------------------- */
+int kcnn_mat_conv2d(const float *in, MatrixDim in_dim, const float *kernel,
+                    MatrixDim kernel_dim, int in_height, int in_width,
+                    int in_channel, int kernel_height, int kernel_width,
+                    int group, float *out, MatrixDim out_dim, int concat);
+int kcnn_mat_add_mat_rep_vec(float *m, MatrixDim dim, const float *vec,
+                             int vec_dim, int rep);
+int kcnn_mat_flip_mat(const float *m, MatrixDim dim, int kernel_height,
+                      int kernel_width, int in_channel, int group, float *flip,
+                      MatrixDim flip_dim);
+int kcnn_mat_padding_zero(const float *m, MatrixDim dim, int orig_height,
+                          int orig_width, int orig_channel, int kernel_height,
+                          int kernel_width, float *padmat, MatrixDim pad_dim);
+int kcnn_mat_tp_block(const float *m, MatrixDim dim, int in_channel,
+                      int block_size, float *out, MatrixDim out_dim);
+int kcnn_mat_tp_inside_block(const float *m, MatrixDim dim, int group,
+                             int block_size, float *out, MatrixDim out_dim);
+int kcnn_mat_mod_permute_row(const float *m, MatrixDim dim, int in_channel,
+                             int block_size, float *out, MatrixDim out_dim);
+int kcnn_mat_maxpool_prop(const float *in, MatrixDim in_dim, int in_height,
+                          int in_width, int pool_height_dim,
+                          int pool_width_dim, int pool_channel_dim,
+                          int overlap, int overlap2D, float *out,
+                          MatrixDim out_dim);
+int kcnn_mat_maxpool_backprop(const float *in_value, MatrixDim in_dim,
+                              const float *out_value, MatrixDim ov_dim,
+                              const float *out_deriv, MatrixDim od_dim,
+                              float *in_deriv, MatrixDim id_dim, int in_height,
+                              int in_width, int pool_height_dim,
+                              int pool_width_dim, int pool_channel_dim,
+                              int overlap, int overlap2D);
+
+/* ---- components ------------------------------------------------------------ */
+typedef struct kcnn_component kcnn_component;
+
+/* Component::NewFromString, e.g. "ConvolutionComponent in-height=40 ...". */
+kcnn_component *kcnn_component_new_from_string(const char *initializer_line);
+/* Component::ReadNew from a Kaldi stream file written by kcnn_component_write
+ * (binary files start with the "\0B" header). */
+kcnn_component *kcnn_component_read(const char *path);
+int kcnn_component_write(const kcnn_component *c, const char *path, int binary);
+kcnn_component *kcnn_component_copy(const kcnn_component *c);
+void kcnn_component_free(kcnn_component *c);
+int kcnn_component_type(const kcnn_component *c, char *buf, size_t len);
+int kcnn_component_info(const kcnn_component *c, char *buf, size_t len);
+int kcnn_component_input_dim(const kcnn_component *c);
+int kcnn_component_output_dim(const kcnn_component *c);
+int kcnn_component_backprop_needs_input(const kcnn_component *c);
+int kcnn_component_backprop_needs_output(const kcnn_component *c);
+/* Component::Propagate(ChunkInfo(in_dim.cols, num_chunks, 0, rows/num_chunks-1),
+ * ..., in, out). */
+int kcnn_component_propagate(const kcnn_component *c, const float *in,
+                             MatrixDim in_dim, float *out, MatrixDim out_dim,
+                             int num_chunks);
+/* Component::Backprop(..., to_update = update ? this : NULL, in_deriv);
+ * in_deriv may be NULL to skip the data gradient. */
+int kcnn_component_backprop(kcnn_component *c, const float *in_value,
+                            MatrixDim in_dim, const float *out_value,
+                            MatrixDim ov_dim, const float *out_deriv,
+                            MatrixDim od_dim, float *in_deriv,
+                            MatrixDim id_dim, int num_chunks, int update);
+/* Parameter access.  which: 0 = linear params, 1 = bias (as a 1 x N matrix),
+ * 2 = prev_grad_ (momentum buffer).  Sizes via kcnn_component_param_dim. */
+int kcnn_component_param_dim(const kcnn_component *c, int which, int *rows,
+                             int *cols);
+int kcnn_component_get_param(const kcnn_component *c, int which, float *dst,
+                             MatrixDim dst_dim);
+int kcnn_component_set_param(kcnn_component *c, int which, const float *src,
+                             MatrixDim src_dim);
+float kcnn_component_learning_rate(const kcnn_component *c);
+int kcnn_component_set_learning_rate(kcnn_component *c, float lr);
+/* UpdatableComponent::DotProduct / SetZero / Scale / Add / PerturbParams. */
+int kcnn_component_dot_product(const kcnn_component *a, const kcnn_component *b,
+                               float *out);
+int kcnn_component_set_zero(kcnn_component *c, int treat_as_gradient);
+int kcnn_component_scale(kcnn_component *c, float scale);
+int kcnn_component_add(kcnn_component *c, float alpha,
+                       const kcnn_component *other);
+int kcnn_component_perturb_params(kcnn_component *c, float stddev);
+/* Data-parallel split of Update: flat gradient [linear | bias] (floats). */
+int kcnn_component_num_gradient_params(const kcnn_component *c);
+int kcnn_component_compute_gradient(const kcnn_component *c,
+                                    const float *in_value, MatrixDim in_dim,
+                                    const float *out_deriv, MatrixDim od_dim,
+                                    float *grad);
+int kcnn_component_apply_gradient(kcnn_component *c, const float *grad,
+                                  int num_sample);
+/* ConvolutionComponent only: 1 if Backprop's reference branch is
+ * "flip kernel" (nnet-component-nnet0.cc:489-497). */
+int kcnn_component_conv_flip_branch(const kcnn_component *c);
+
+/* ---- component stack (NnetUpdater-style) -------------------------------- */
+typedef struct kcnn_nnet kcnn_nnet;
+/* One component initializer line per '\n'-separated line of `config`. */
+kcnn_nnet *kcnn_nnet_new(const char *config);
+void kcnn_nnet_free(kcnn_nnet *n);
+int kcnn_nnet_num_components(const kcnn_nnet *n);
+kcnn_component *kcnn_nnet_component(kcnn_nnet *n, int i);  /* borrowed */
+/* Forward over all components; keeps every layer's output for Backprop. */
+int kcnn_nnet_propagate(kcnn_nnet *n, const float *in, MatrixDim in_dim);
+/* Device pointer + dims of layer i's output (i = -1: the input copy). */
+int kcnn_nnet_output(const kcnn_nnet *n, int i, const float **data,
+                     MatrixDim *dim);
+/* Backprop of component i given d(output_i) = the buffer filled by the
+ * previous call (or `out_deriv` for the last component).  mode 0: reference
+ * (update in place); 1: write the gradient into grad (device, length
+ * kcnn_component_num_gradient_params) without updating; 2: data gradient
+ * only.  The data gradient of component 0 is skipped when skip_first_dx. */
+int kcnn_nnet_backprop_component(kcnn_nnet *n, int i, const float *out_deriv,
+                                 MatrixDim od_dim, int mode, float *grad,
+                                 int skip_first_dx);
+/* Full backward pass, last component to first, mode 0 (reference). */
+int kcnn_nnet_backprop(kcnn_nnet *n, const float *out_deriv, MatrixDim od_dim);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KCNN_KCNN_H_ */

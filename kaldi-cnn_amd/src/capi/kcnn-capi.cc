@@ -1,0 +1,510 @@
+// capi/kcnn-capi.cc -- extern "C" layer of libkcnn.so (include/kcnn.h).
+// Converts C++ exceptions (KALDI_ASSERT / KALDI_ERR / HIP errors) into error
+// codes + kcnn_last_error(), and wraps caller device buffers as CuSubMatrix /
+// borrowed CuMatrix views.
+#include "kcnn.h"
+
+#include <string.h>
+
+#include <fstream>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../cnslmat/hip-util.h"
+#include "../kaldi-lite/cu-device.h"
+#include "../kaldi-lite/cu-matrix.h"
+#include "../kaldi-lite/kaldi-io.h"
+#include "../nnet0/nnet-component-nnet0.h"
+#include "../nnet2/nnet-component.h"
+
+using namespace kaldi;
+using namespace kaldi::nnet2;
+
+struct kcnn_component {
+  Component *c;
+};
+
+struct kcnn_nnet {
+  std::vector<Component *> comps;
+  std::vector<kcnn_component> handles;
+  std::vector<CuMatrix<BaseFloat>> fwd;    // fwd[0] borrowed input, fwd[i+1] = out_i
+  std::vector<CuMatrix<BaseFloat>> deriv;  // deriv[i] = d input_i
+  int num_chunks = 0;
+  ~kcnn_nnet() { for (auto *c : comps) delete c; }
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(const char *what) {
+  g_err = what;
+  return -1;
+}
+
+template <typename F>
+int guard(F f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception &e) {
+    return fail(e.what());
+  } catch (...) {
+    return fail("unknown C++ exception");
+  }
+}
+
+CuSubMatrix<BaseFloat> view(const float *p, MatrixDim d) {
+  return CuSubMatrix<BaseFloat>(const_cast<float *>(p), d.rows, d.cols, d.stride);
+}
+
+void borrow(CuMatrix<BaseFloat> *m, const float *p, MatrixDim d) {
+  m->Borrow(const_cast<float *>(p), d.rows, d.cols, d.stride);
+}
+
+ChunkInfo chunk_info(int cols, int rows, int num_chunks) {
+  if (num_chunks <= 0) num_chunks = rows;
+  KALDI_ASSERT(rows > 0 && rows % num_chunks == 0);
+  return ChunkInfo(cols, num_chunks, 0, rows / num_chunks - 1);
+}
+
+void copy_out(std::string s, char *buf, size_t len) {
+  if (!buf || !len) return;
+  strncpy(buf, s.c_str(), len - 1);
+  buf[len - 1] = '\0';
+}
+
+UpdatableComponent *updatable(const kcnn_component *c) {
+  KALDI_ASSERT(c && c->c);
+  UpdatableComponent *u = dynamic_cast<UpdatableComponent *>(c->c);
+  if (!u) KALDI_ERR << c->c->Type() << " has no parameters";
+  return u;
+}
+
+// Parameter storage of a component: linear (0), bias (1), prev_grad (2).
+void param_ref(const kcnn_component *c, int which, float **data, MatrixDim *dim) {
+  using cnsl::nnet0::ConvolutionComponent;
+  using cnsl::nnet0::FullyConnectedComponent;
+  CuMatrixBase<BaseFloat> *m = nullptr;
+  CuVectorBase<BaseFloat> *v = nullptr;
+  if (auto *cc = dynamic_cast<ConvolutionComponent *>(c->c)) {
+    if (which == 0) m = &cc->LinearParamsMutable();
+    else if (which == 1) v = &cc->BiasParamsMutable();
+    else if (which == 2) m = &cc->PrevGradMutable();
+  } else if (auto *fc = dynamic_cast<FullyConnectedComponent *>(c->c)) {
+    if (which == 0) m = &fc->LinearParamsMutable();
+    else if (which == 1) v = &fc->BiasParamsMutable();
+    else if (which == 2) m = &fc->PrevGradMutable();
+  } else if (auto *af = dynamic_cast<AffineComponent *>(c->c)) {
+    if (which == 0) m = &af->LinearParamsMutable();
+    else if (which == 1) v = &af->BiasParamsMutable();
+  }
+  if (m) {
+    *data = m->Data();
+    *dim = m->Dim();
+  } else if (v) {
+    *data = v->Data();
+    dim->rows = 1; dim->cols = v->Dim(); dim->stride = v->Dim();
+  } else {
+    KALDI_ERR << c->c->Type() << " has no parameter #" << which;
+  }
+}
+
+void copy2d(float *dst, MatrixDim dd, const float *src, MatrixDim sd) {
+  KALDI_ASSERT(dd.rows == sd.rows && dd.cols == sd.cols);
+  if (dd.rows == 0 || dd.cols == 0) return;
+  CU_SAFE_CALL(hipMemcpy2DAsync(dst, sizeof(float) * dd.stride, src,
+                                sizeof(float) * sd.stride,
+                                sizeof(float) * dd.cols, dd.rows,
+                                hipMemcpyDeviceToDevice,
+                                CuDevice::Instantiate().Stream()));
+}
+}  // namespace
+
+extern "C" {
+
+const char *kcnn_last_error(void) { return g_err.c_str(); }
+const char *kcnn_version(void) { return "kcnn-mi355x 0.1 (gfx950)"; }
+
+int kcnn_init(int device) {
+  return guard([&] { CuDevice::Instantiate().SelectGpuId("yes", device); });
+}
+int kcnn_set_stream(kcnn_stream_t stream) {
+  return guard([&] {
+    CuDevice::Instantiate().SetStream(reinterpret_cast<hipStream_t>(stream));
+  });
+}
+int kcnn_synchronize(void) {
+  return guard([&] { CuDevice::Instantiate().Synchronize(); });
+}
+int kcnn_set_literal_path(int literal) {
+  cnsl::nnet0::SetLiteralPath(literal != 0);
+  return 0;
+}
+int kcnn_set_profiling(int on) {
+  CuDevice::Instantiate().SetProfiling(on != 0);
+  return 0;
+}
+int kcnn_profile_string(char *buf, size_t len) {
+  return guard([&] { copy_out(CuDevice::Instantiate().ProfileString(), buf, len); });
+}
+void kcnn_set_randn_seed(uint64_t seed) { SetRandnSeed(seed); }
+
+int kcnn_selftest_fastdiv(void) {
+  const uint32_t divs[] = {1, 2, 3, 5, 7, 8, 11, 24, 33, 40, 128, 363, 440,
+                           1320, 11616, 46464, 65535, 1000003, 0x7fffffffu};
+  uint64_t state = 12345;
+  for (uint32_t d : divs) {
+    kcnn::FastDiv f(d);
+    for (int t = 0; t < 20000; t++) {
+      state = state * 6364136223846793005ull + 1442695040888963407ull;
+      uint32_t n = (uint32_t)(state >> 33);  // < 2^31
+      if (t < 64) n = (uint32_t)t;
+      if (t >= 64 && t < 128) n = 0x7fffffffu - (uint32_t)(t - 64);
+      uint32_t q, r;
+      f.divmod(n, q, r);
+      if (q != n / d || r != n % d) {
+        std::ostringstream ss;
+        ss << "FastDiv(" << d << ") failed at n=" << n << ": " << q << "," << r;
+        return fail(ss.str().c_str());
+      }
+    }
+  }
+  return 0;
+}
+
+// ---- CuMatrixBase methods -----------------------------------------------------
+int kcnn_mat_conv2d(const float *in, MatrixDim in_dim, const float *kernel,
+                    MatrixDim kernel_dim, int in_height, int in_width,
+                    int in_channel, int kernel_height, int kernel_width,
+                    int group, float *out, MatrixDim out_dim, int concat) {
+  return guard([&] {
+    auto x = view(in, in_dim), k = view(kernel, kernel_dim), o = view(out, out_dim);
+    x.Conv2D(k, in_height, in_width, in_channel, kernel_height, kernel_width,
+             group, &o, concat != 0);
+  });
+}
+int kcnn_mat_add_mat_rep_vec(float *m, MatrixDim dim, const float *vec,
+                             int vec_dim, int rep) {
+  return guard([&] {
+    auto x = view(m, dim);
+    CuSubVector<BaseFloat> v(const_cast<float *>(vec), vec_dim);
+    x.AddMatRepVec(v, rep);
+  });
+}
+int kcnn_mat_flip_mat(const float *m, MatrixDim dim, int kernel_height,
+                      int kernel_width, int in_channel, int group, float *flip,
+                      MatrixDim flip_dim) {
+  return guard([&] {
+    auto x = view(m, dim);
+    CuMatrix<BaseFloat> f;
+    borrow(&f, flip, flip_dim);
+    x.FlipMat(kernel_height, kernel_width, in_channel, group, &f);
+  });
+}
+int kcnn_mat_padding_zero(const float *m, MatrixDim dim, int orig_height,
+                          int orig_width, int orig_channel, int kernel_height,
+                          int kernel_width, float *padmat, MatrixDim pad_dim) {
+  return guard([&] {
+    auto x = view(m, dim);
+    CuMatrix<BaseFloat> p;
+    borrow(&p, padmat, pad_dim);
+    x.PaddingZero(orig_height, orig_width, orig_channel, kernel_height,
+                  kernel_width, &p);
+  });
+}
+int kcnn_mat_tp_block(const float *m, MatrixDim dim, int in_channel,
+                      int block_size, float *out, MatrixDim out_dim) {
+  return guard([&] {
+    auto x = view(m, dim);
+    CuMatrix<BaseFloat> o;
+    borrow(&o, out, out_dim);
+    x.TpBlock(in_channel, block_size, &o);
+  });
+}
+int kcnn_mat_tp_inside_block(const float *m, MatrixDim dim, int group,
+                             int block_size, float *out, MatrixDim out_dim) {
+  return guard([&] {
+    auto x = view(m, dim);
+    CuMatrix<BaseFloat> o;
+    borrow(&o, out, out_dim);
+    x.TpInsideBlock(group, block_size, &o);
+  });
+}
+int kcnn_mat_mod_permute_row(const float *m, MatrixDim dim, int in_channel,
+                             int block_size, float *out, MatrixDim out_dim) {
+  return guard([&] {
+    auto x = view(m, dim);
+    CuMatrix<BaseFloat> o;
+    borrow(&o, out, out_dim);
+    x.ModPermuteRow(in_channel, block_size, &o);
+  });
+}
+int kcnn_mat_maxpool_prop(const float *in, MatrixDim in_dim, int in_height,
+                          int in_width, int pool_height_dim, int pool_width_dim,
+                          int pool_channel_dim, int overlap, int overlap2D,
+                          float *out, MatrixDim out_dim) {
+  return guard([&] {
+    auto x = view(in, in_dim), o = view(out, out_dim);
+    x.Maxpool_prop(in_height, in_width, pool_height_dim, pool_width_dim,
+                   pool_channel_dim, overlap != 0, overlap2D != 0, &o);
+  });
+}
+int kcnn_mat_maxpool_backprop(const float *in_value, MatrixDim in_dim,
+                              const float *out_value, MatrixDim ov_dim,
+                              const float *out_deriv, MatrixDim od_dim,
+                              float *in_deriv, MatrixDim id_dim, int in_height,
+                              int in_width, int pool_height_dim,
+                              int pool_width_dim, int pool_channel_dim,
+                              int overlap, int overlap2D) {
+  return guard([&] {
+    auto x = view(in_value, in_dim), y = view(out_value, ov_dim),
+         dy = view(out_deriv, od_dim);
+    CuMatrix<BaseFloat> dx;
+    borrow(&dx, in_deriv, id_dim);
+    x.Maxpool_backprop(y, dy, &dx, in_height, in_width, pool_height_dim,
+                       pool_width_dim, pool_channel_dim, overlap != 0,
+                       overlap2D != 0);
+  });
+}
+
+// ---- components ------------------------------------------------------------------
+kcnn_component *kcnn_component_new_from_string(const char *line) {
+  kcnn_component *h = nullptr;
+  guard([&] { h = new kcnn_component{Component::NewFromString(line)}; });
+  return h;
+}
+kcnn_component *kcnn_component_read(const char *path) {
+  kcnn_component *h = nullptr;
+  guard([&] {
+    std::ifstream is(path, std::ios::binary);
+    if (!is) KALDI_ERR << "cannot open " << path;
+    bool binary = false;
+    if (!InitKaldiInputStream(is, &binary)) KALDI_ERR << "bad Kaldi header in " << path;
+    h = new kcnn_component{Component::ReadNew(is, binary)};
+  });
+  return h;
+}
+int kcnn_component_write(const kcnn_component *c, const char *path, int binary) {
+  return guard([&] {
+    std::ofstream os(path, std::ios::binary);
+    if (!os) KALDI_ERR << "cannot open " << path << " for writing";
+    InitKaldiOutputStream(os, binary != 0);
+    c->c->Write(os, binary != 0);
+    if (!os) KALDI_ERR << "write failed: " << path;
+  });
+}
+kcnn_component *kcnn_component_copy(const kcnn_component *c) {
+  kcnn_component *h = nullptr;
+  guard([&] { h = new kcnn_component{c->c->Copy()}; });
+  return h;
+}
+void kcnn_component_free(kcnn_component *c) {
+  if (!c) return;
+  delete c->c;
+  delete c;
+}
+int kcnn_component_type(const kcnn_component *c, char *buf, size_t len) {
+  return guard([&] { copy_out(c->c->Type(), buf, len); });
+}
+int kcnn_component_info(const kcnn_component *c, char *buf, size_t len) {
+  return guard([&] { copy_out(c->c->Info(), buf, len); });
+}
+int kcnn_component_input_dim(const kcnn_component *c) { return c->c->InputDim(); }
+int kcnn_component_output_dim(const kcnn_component *c) { return c->c->OutputDim(); }
+int kcnn_component_backprop_needs_input(const kcnn_component *c) {
+  return c->c->BackpropNeedsInput();
+}
+int kcnn_component_backprop_needs_output(const kcnn_component *c) {
+  return c->c->BackpropNeedsOutput();
+}
+
+int kcnn_component_propagate(const kcnn_component *c, const float *in,
+                             MatrixDim in_dim, float *out, MatrixDim out_dim,
+                             int num_chunks) {
+  return guard([&] {
+    auto x = view(in, in_dim), y = view(out, out_dim);
+    ChunkInfo ii = chunk_info(in_dim.cols, in_dim.rows, num_chunks);
+    ChunkInfo oi = chunk_info(out_dim.cols, out_dim.rows, num_chunks);
+    c->c->Propagate(ii, oi, x, &y);
+  });
+}
+
+int kcnn_component_backprop(kcnn_component *c, const float *in_value,
+                            MatrixDim in_dim, const float *out_value,
+                            MatrixDim ov_dim, const float *out_deriv,
+                            MatrixDim od_dim, float *in_deriv,
+                            MatrixDim id_dim, int num_chunks, int update) {
+  return guard([&] {
+    auto x = view(in_value, in_dim), y = view(out_value, ov_dim),
+         dy = view(out_deriv, od_dim);
+    ChunkInfo ii = chunk_info(in_dim.cols, in_dim.rows, num_chunks);
+    ChunkInfo oi = chunk_info(od_dim.cols, od_dim.rows, num_chunks);
+    CuMatrix<BaseFloat> dx;
+    if (in_deriv) borrow(&dx, in_deriv, id_dim);
+    Component *to_update =
+        update && dynamic_cast<UpdatableComponent *>(c->c) ? c->c : nullptr;
+    c->c->Backprop(ii, oi, x, y, dy, to_update, in_deriv ? &dx : nullptr);
+  });
+}
+
+int kcnn_component_param_dim(const kcnn_component *c, int which, int *rows,
+                             int *cols) {
+  return guard([&] {
+    float *p;
+    MatrixDim d;
+    param_ref(c, which, &p, &d);
+    *rows = d.rows;
+    *cols = d.cols;
+  });
+}
+int kcnn_component_get_param(const kcnn_component *c, int which, float *dst,
+                             MatrixDim dst_dim) {
+  return guard([&] {
+    float *p;
+    MatrixDim d;
+    param_ref(c, which, &p, &d);
+    copy2d(dst, dst_dim, p, d);
+  });
+}
+int kcnn_component_set_param(kcnn_component *c, int which, const float *src,
+                             MatrixDim src_dim) {
+  return guard([&] {
+    float *p;
+    MatrixDim d;
+    param_ref(c, which, &p, &d);
+    copy2d(p, d, src, src_dim);
+  });
+}
+float kcnn_component_learning_rate(const kcnn_component *c) {
+  float lr = -1.0f;
+  guard([&] { lr = updatable(c)->LearningRate(); });
+  return lr;
+}
+int kcnn_component_set_learning_rate(kcnn_component *c, float lr) {
+  return guard([&] { updatable(c)->SetLearningRate(lr); });
+}
+int kcnn_component_dot_product(const kcnn_component *a, const kcnn_component *b,
+                               float *out) {
+  return guard([&] { *out = updatable(a)->DotProduct(*updatable(b)); });
+}
+int kcnn_component_set_zero(kcnn_component *c, int treat_as_gradient) {
+  return guard([&] { updatable(c)->SetZero(treat_as_gradient != 0); });
+}
+int kcnn_component_scale(kcnn_component *c, float scale) {
+  return guard([&] { updatable(c)->Scale(scale); });
+}
+int kcnn_component_add(kcnn_component *c, float alpha, const kcnn_component *other) {
+  return guard([&] { updatable(c)->Add(alpha, *updatable(other)); });
+}
+int kcnn_component_perturb_params(kcnn_component *c, float stddev) {
+  return guard([&] { updatable(c)->PerturbParams(stddev); });
+}
+int kcnn_component_num_gradient_params(const kcnn_component *c) {
+  auto *u = dynamic_cast<UpdatableComponent *>(c->c);
+  return u ? u->NumGradientParams() : 0;
+}
+int kcnn_component_compute_gradient(const kcnn_component *c,
+                                    const float *in_value, MatrixDim in_dim,
+                                    const float *out_deriv, MatrixDim od_dim,
+                                    float *grad) {
+  return guard([&] {
+    updatable(c)->ComputeGradient(view(in_value, in_dim), view(out_deriv, od_dim),
+                                  grad);
+  });
+}
+int kcnn_component_apply_gradient(kcnn_component *c, const float *grad,
+                                  int num_sample) {
+  return guard([&] { updatable(c)->ApplyGradient(grad, num_sample); });
+}
+int kcnn_component_conv_flip_branch(const kcnn_component *c) {
+  auto *cc = dynamic_cast<cnsl::nnet0::ConvolutionComponent *>(c->c);
+  if (!cc) return fail("not a ConvolutionComponent");
+  return cc->FlipKernelBranch() ? 1 : 0;
+}
+
+// ---- component stack ---------------------------------------------------------------
+kcnn_nnet *kcnn_nnet_new(const char *config) {
+  std::unique_ptr<kcnn_nnet> n(new kcnn_nnet());
+  int rc = guard([&] {
+    std::istringstream is(config);
+    std::string line;
+    while (std::getline(is, line)) {
+      const size_t b = line.find_first_not_of(" \t\r");
+      if (b == std::string::npos || line[b] == '#') continue;
+      n->comps.push_back(Component::NewFromString(line.substr(b)));
+    }
+    if (n->comps.empty()) KALDI_ERR << "empty nnet config";
+    for (size_t i = 0; i + 1 < n->comps.size(); i++)
+      if (n->comps[i]->OutputDim() != n->comps[i + 1]->InputDim())
+        KALDI_ERR << "dimension mismatch between component " << i << " ("
+                  << n->comps[i]->OutputDim() << ") and " << i + 1 << " ("
+                  << n->comps[i + 1]->InputDim() << ")";
+    for (auto *c : n->comps) n->handles.push_back(kcnn_component{c});
+    n->fwd.resize(n->comps.size() + 1);
+    n->deriv.resize(n->comps.size());
+  });
+  return rc ? nullptr : n.release();
+}
+void kcnn_nnet_free(kcnn_nnet *n) { delete n; }
+int kcnn_nnet_num_components(const kcnn_nnet *n) { return (int)n->comps.size(); }
+kcnn_component *kcnn_nnet_component(kcnn_nnet *n, int i) {
+  if (i < 0 || i >= (int)n->handles.size()) return nullptr;
+  return &n->handles[i];
+}
+
+int kcnn_nnet_propagate(kcnn_nnet *n, const float *in, MatrixDim in_dim) {
+  return guard([&] {
+    KALDI_ASSERT(in_dim.cols == n->comps[0]->InputDim());
+    borrow(&n->fwd[0], in, in_dim);
+    n->num_chunks = in_dim.rows;
+    for (size_t i = 0; i < n->comps.size(); i++) {
+      ChunkInfo ii(n->comps[i]->InputDim(), n->num_chunks, 0, 0);
+      ChunkInfo oi(n->comps[i]->OutputDim(), n->num_chunks, 0, 0);
+      n->comps[i]->Propagate(ii, oi, n->fwd[i], &n->fwd[i + 1]);
+    }
+  });
+}
+
+int kcnn_nnet_output(const kcnn_nnet *n, int i, const float **data,
+                     MatrixDim *dim) {
+  return guard([&] {
+    KALDI_ASSERT(i >= -1 && i < (int)n->comps.size());
+    const CuMatrix<BaseFloat> &m = n->fwd[i + 1];
+    *data = m.Data();
+    *dim = m.Dim();
+  });
+}
+
+int kcnn_nnet_backprop_component(kcnn_nnet *n, int i, const float *out_deriv,
+                                 MatrixDim od_dim, int mode, float *grad,
+                                 int skip_first_dx) {
+  return guard([&] {
+    const int nc = (int)n->comps.size();
+    KALDI_ASSERT(i >= 0 && i < nc);
+    Component *c = n->comps[i];
+    CuSubMatrix<BaseFloat> od = (i == nc - 1)
+        ? view(out_deriv, od_dim)
+        : CuSubMatrix<BaseFloat>(n->deriv[i + 1].Data(), n->deriv[i + 1].NumRows(),
+                                 n->deriv[i + 1].NumCols(), n->deriv[i + 1].Stride());
+    ChunkInfo ii(c->InputDim(), n->num_chunks, 0, 0);
+    ChunkInfo oi(c->OutputDim(), n->num_chunks, 0, 0);
+    auto *u = dynamic_cast<UpdatableComponent *>(c);
+    CuMatrix<BaseFloat> *dx = &n->deriv[i];
+    if (i == 0 && skip_first_dx && u) dx = nullptr;
+    Component *to_update = (mode == 0 && u) ? c : nullptr;
+    c->Backprop(ii, oi, n->fwd[i], n->fwd[i + 1], od, to_update, dx);
+    if (mode == 1 && u) u->ComputeGradient(n->fwd[i], od, grad);
+  });
+}
+
+int kcnn_nnet_backprop(kcnn_nnet *n, const float *out_deriv, MatrixDim od_dim) {
+  for (int i = (int)n->comps.size() - 1; i >= 0; i--) {
+    int rc = kcnn_nnet_backprop_component(n, i, out_deriv, od_dim, 0, nullptr, 0);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+}  // extern "C"

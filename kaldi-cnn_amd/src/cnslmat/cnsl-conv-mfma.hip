@@ -1,0 +1,536 @@
+// cnslmat/cnsl-conv-mfma.hip -- convolution on gfx950 matrix cores.
+//
+// CuMatrixBase::Conv2D (conv2D.cc:43-201) materialises an im2col matrix
+// ("spanThis", up to 0.5 GB per split), runs cuBLAS sgemm into a zero-filled
+// temporary, copies it into a second temporary and finally col2im's it into
+// `out` (four launches, ~10x the compulsory HBM traffic).  Here the same
+// contraction is one implicit GEMM:
+//
+//   D[g][m] = sum_k K[k][g] * B[k][m],     m = n*P + p   (sample-major),
+//   B[k][m] = X[n][c*H*W + (px+kx-pad_w)*H + (py+ky-pad_h)]  (0 outside),
+//   k = c*kh*kw + kx*kh + ky,  p = px*oh + py                
+//
+// on v_mfma_f32_32x32x2_f32 (exact fp32, fma-chain numerics): the B tile is
+// gathered straight from X (L1/L2-resident rows) into LDS, the kernel tile is
+// staged beside it, and the accumulator is stored directly in the reference's
+// output layout -- concat: out[n][g*P + p] with lanes along p (two 128-B
+// segments per store), or plain: out[p*R + n][g] -- with the bias add of
+// AddMatRepVec fused.  Virtual zero padding replaces PaddingZero.  Long
+// reductions split K across workgroups into a workspace and are reduced in a
+// fixed order (deterministic).
+//
+// Small output-channel counts (the data gradient of a 1- or 3-channel input
+// layer: G' = C) use a direct VALU kernel instead: an MFMA tile would be
+// >= 80 % padding there.
+//
+// The weight gradient of ConvolutionComponent::Update gets its own fused
+// kernel (TpBlock + TpInsideBlock + Conv2D + ModPermuteRow + AddRowSumMat,
+// nnet-component-nnet0.cc:745-775) reading X and dY once each.
+#include <hip/hip_runtime.h>
+
+#include "hip-util.h"
+
+using kcnn::FastDiv;
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct ConvGeom {
+  int R, H, W, C, pad_h, pad_w, kh, kw, G, oh, ow, P, Kdim, HW;
+  int64_t M;  // R * P
+  FastDiv div_P, div_oh, div_khkw, div_kh;
+};
+
+ConvGeom make_geom(int R, int H, int W, int C, int pad_h, int pad_w, int kh,
+                   int kw, int G) {
+  ConvGeom g;
+  g.R = R; g.H = H; g.W = W; g.C = C; g.pad_h = pad_h; g.pad_w = pad_w;
+  g.kh = kh; g.kw = kw; g.G = G;
+  g.oh = H + 2 * pad_h - kh + 1;
+  g.ow = W + 2 * pad_w - kw + 1;
+  g.P = g.oh * g.ow;
+  g.Kdim = kh * kw * C;
+  g.HW = H * W;
+  g.M = (int64_t)R * g.P;
+  g.div_P = FastDiv((uint32_t)(g.P > 0 ? g.P : 1));
+  g.div_oh = FastDiv((uint32_t)(g.oh > 0 ? g.oh : 1));
+  g.div_khkw = FastDiv((uint32_t)(kh * kw));
+  g.div_kh = FastDiv((uint32_t)kh);
+  return g;
+}
+
+// Input element of im2col row k for output position (px, py) of one sample.
+__device__ __forceinline__ float gather_x(const ConvGeom &g,
+                                          const float *__restrict__ xrow,
+                                          int k, int px, int py) {
+  uint32_t c, r, kx, ky;
+  g.div_khkw.divmod((uint32_t)k, c, r);
+  g.div_kh.divmod(r, kx, ky);
+  const int xx = px + (int)kx - g.pad_w, yy = py + (int)ky - g.pad_h;
+  if (xx < 0 || xx >= g.W || yy < 0 || yy >= g.H) return 0.0f;
+  return xrow[(int64_t)c * g.HW + (int64_t)xx * g.H + yy];
+}
+
+// ---------------------------------------------------------------------------
+// Implicit-GEMM kernel: block tile 64 (g) x 64 (m), K step 16, 4 waves each
+// owning one 32x32 MFMA accumulator.
+constexpr int IG_BG = 64, IG_BM = 64, IG_BK = 16;
+enum { ST_CONCAT = 0, ST_PLAIN = 1, ST_PARTIAL = 2 };
+
+template <int STORE>
+__global__ __launch_bounds__(256) void conv_igemm_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs,
+    const float *__restrict__ Kmat, int ks, const float *__restrict__ bias,
+    float *__restrict__ out, int os, float *__restrict__ ws, int k_per_split) {
+  __shared__ float As[IG_BK][IG_BG];
+  __shared__ float Bs[IG_BK][IG_BM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wg = wave & 1, wm = wave >> 1;
+  const int64_t m0 = (int64_t)blockIdx.x * IG_BM;
+  const int g0 = blockIdx.y * IG_BG;
+  const int kbeg = blockIdx.z * k_per_split;
+  const int kend = min(g.Kdim, kbeg + k_per_split);
+
+  // This thread's B column (fixed over the K loop).
+  const int bm = tid & 63, bk = tid >> 6;
+  const int64_t m = m0 + bm;
+  const bool mvalid = m < g.M;
+  uint32_t n = 0, p = 0, px = 0, py = 0;
+  if (mvalid) {
+    g.div_P.divmod((uint32_t)m, n, p);
+    g.div_oh.divmod(p, px, py);
+  }
+  const float *xrow = X + (int64_t)n * xs;
+  const int ak = tid >> 4, ag = (tid & 15) * 4;
+
+  floatx16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; i++) acc[i] = 0.0f;
+
+  for (int k0 = kbeg; k0 < kend; k0 += IG_BK) {
+    {
+      const int kk = k0 + ak;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int gg = g0 + ag + j;
+        As[ak][ag + j] =
+            (kk < kend && gg < g.G) ? Kmat[(int64_t)kk * ks + gg] : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int kk = k0 + bk + 4 * j;
+      Bs[bk + 4 * j][bm] = (mvalid && kk < kend)
+                               ? gather_x(g, xrow, kk, (int)px, (int)py)
+                               : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < IG_BK; kk += 2) {
+      const float a = As[kk + (lane >> 5)][wg * 32 + (lane & 31)];
+      const float b = Bs[kk + (lane >> 5)][wm * 32 + (lane & 31)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // Epilogue.  D[i][j]: j = lane & 31 (m), i = (r&3) + 8(r>>2) + 4(lane>>5) (g).
+  const int64_t mm = m0 + wm * 32 + (lane & 31);
+  if (mm >= g.M) return;
+  uint32_t on, op;
+  g.div_P.divmod((uint32_t)mm, on, op);
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const int gg = g0 + wg * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (gg >= g.G) continue;
+    float v = acc[r];
+    if (STORE == ST_CONCAT) {
+      if (bias) v = v + bias[gg];
+      out[(int64_t)on * os + (int64_t)gg * g.P + op] = v;
+    } else if (STORE == ST_PLAIN) {
+      out[((int64_t)op * g.R + on) * os + gg] = v;
+    } else {
+      ws[((int64_t)blockIdx.z * g.G + gg) * g.M + mm] = v;
+    }
+  }
+}
+
+// Fixed-order reduction of split-K partials [S][G][M] + the store epilogue.
+__global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(
+    ConvGeom g, const float *__restrict__ ws, int S,
+    const float *__restrict__ bias, float *__restrict__ out, int os,
+    int concat) {
+  const int64_t total = (int64_t)g.G * g.M;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int gg = (int)(e / g.M);
+    const int64_t mm = e - (int64_t)gg * g.M;
+    float outer = 0.0f;
+    for (int s0 = 0; s0 < S; s0 += 32) {  // two-level: error ~ sqrt(32)+sqrt(S/32)
+      float inner = 0.0f;
+      const int s1 = min(S, s0 + 32);
+      for (int s = s0; s < s1; s++) inner += ws[((int64_t)s * g.G + gg) * g.M + mm];
+      outer += inner;
+    }
+    uint32_t on, op;
+    g.div_P.divmod((uint32_t)mm, on, op);
+    if (concat) {
+      if (bias) outer = outer + bias[gg];
+      out[(int64_t)on * os + (int64_t)gg * g.P + op] = outer;
+    } else {
+      out[((int64_t)op * g.R + on) * os + gg] = outer;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Direct kernel for few output channels (G <= NG): thread per output
+// position, sequential k loop (same order as the reference GEMM's k), the
+// kernel row read through the scalar cache (k is wave-uniform).
+template <int NG>
+__global__ __launch_bounds__(256) void conv_direct_smallg_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs,
+    const float *__restrict__ Kmat, int ks, const float *__restrict__ bias,
+    float *__restrict__ out, int os) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= g.M) return;
+  uint32_t n, p, px, py;
+  g.div_P.divmod((uint32_t)m, n, p);
+  g.div_oh.divmod(p, px, py);
+  const float *xrow = X + (int64_t)n * xs;
+  float acc[NG];
+#pragma unroll
+  for (int j = 0; j < NG; j++) acc[j] = 0.0f;
+  int k = 0;
+  for (int c = 0; c < g.C; c++) {
+    const float *xc = xrow + (int64_t)c * g.HW;
+    for (int kx = 0; kx < g.kw; kx++) {
+      const int xx = (int)px + kx - g.pad_w;
+      const bool vx = xx >= 0 && xx < g.W;
+      const float *xcol = xc + (int64_t)xx * g.H;
+      for (int ky = 0; ky < g.kh; ky++, k++) {
+        const int yy = (int)py + ky - g.pad_h;
+        const float xv = (vx && yy >= 0 && yy < g.H) ? xcol[yy] : 0.0f;
+        const float *krow = Kmat + (int64_t)k * ks;
+#pragma unroll
+        for (int j = 0; j < NG; j++)
+          if (j < g.G) acc[j] += xv * krow[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NG; j++)
+    if (j < g.G) {
+      float v = acc[j];
+      if (bias) v = v + bias[j];
+      out[(int64_t)n * os + (int64_t)j * g.P + p] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fused weight gradient.  D[g][k] = sum_t dY[n][g*P + p] * B[t][k] over
+// t = n*P + p in this block's split; block tile 64 (g) x 64 (k), t step 32.
+constexpr int WG_BG = 64, WG_BK = 64, WG_BT = 32;
+
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs,
+    const float *__restrict__ dY, int dys, float *__restrict__ ws_w,
+    float *__restrict__ ws_b, int64_t t_per_split) {
+  __shared__ float As[WG_BT][WG_BG + 1];  // dY tile, [t][g]
+  __shared__ float Bs[WG_BT][WG_BK];      // im2col tile, [t][k]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wg = wave & 1, wk = wave >> 1;
+  const int split = blockIdx.x;
+  const int g0 = blockIdx.y * WG_BG, k0 = blockIdx.z * WG_BK;
+  const int64_t T = g.M;
+  const int64_t tbeg = (int64_t)split * t_per_split;
+  const int64_t tend = min(T, tbeg + t_per_split);
+
+  // B: this thread's conv-k column.
+  const int bk = tid & 63, bt = tid >> 6;
+  const int kk = k0 + bk;
+  const bool kvalid = kk < g.Kdim;
+  int koff = 0, kx = 0, ky = 0;
+  if (kvalid) {
+    uint32_t c, r, qx, qy;
+    g.div_khkw.divmod((uint32_t)kk, c, r);
+    g.div_kh.divmod(r, qx, qy);
+    kx = (int)qx; ky = (int)qy;
+    koff = (int)c * g.HW;
+  }
+  // A: this thread's g row and 8 consecutive t.
+  const int ag = tid >> 2, at = (tid & 3) * 8;
+  const int agg = g0 + ag;
+
+  floatx16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; i++) acc[i] = 0.0f;
+  float bsum = 0.0f;
+
+  for (int64_t t0 = tbeg; t0 < tend; t0 += WG_BT) {
+    {
+      int64_t t = t0 + at;
+      uint32_t n = 0, p = 0;
+      if (t < tend) g.div_P.divmod((uint32_t)t, n, p);
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        float v = 0.0f;
+        if (t + i < tend && agg < g.G)
+          v = dY[(int64_t)n * dys + (int64_t)agg * g.P + p];
+        As[at + i][ag] = v;
+        if (++p == (uint32_t)g.P) { p = 0; ++n; }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int64_t t = t0 + bt + 4 * j;
+      float v = 0.0f;
+      if (kvalid && t < tend) {
+        uint32_t n, p, px, py;
+        g.div_P.divmod((uint32_t)t, n, p);
+        g.div_oh.divmod(p, px, py);
+        const int xx = (int)px + kx - g.pad_w, yy = (int)py + ky - g.pad_h;
+        if (xx >= 0 && xx < g.W && yy >= 0 && yy < g.H)
+          v = X[(int64_t)n * xs + koff + (int64_t)xx * g.H + yy];
+      }
+      Bs[bt + 4 * j][bk] = v;
+    }
+    __syncthreads();
+    if (blockIdx.z == 0 && tid < 64) {
+#pragma unroll 8
+      for (int i = 0; i < WG_BT; i++) bsum += As[i][tid];
+    }
+#pragma unroll
+    for (int i = 0; i < WG_BT; i += 2) {
+      const float a = As[i + (lane >> 5)][wg * 32 + (lane & 31)];
+      const float b = Bs[i + (lane >> 5)][wk * 32 + (lane & 31)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  const int kl = k0 + wk * 32 + (lane & 31);
+  if (kl < g.Kdim) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int gl = g0 + wg * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (gl < g.G) ws_w[((int64_t)split * g.G + gl) * g.Kdim + kl] = acc[r];
+    }
+  }
+  if (blockIdx.z == 0 && tid < 64 && g0 + tid < g.G)
+    ws_b[(int64_t)split * g.G + g0 + tid] = bsum;
+}
+
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(
+    ConvGeom g, const float *__restrict__ ws_w, const float *__restrict__ ws_b,
+    int S, float *__restrict__ gW, int gws, float *__restrict__ gb) {
+  const int total = g.G * g.Kdim;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total + g.G;
+       e += gridDim.x * blockDim.x) {
+    float outer = 0.0f;
+    if (e < total) {
+      const int gg = e / g.Kdim, k = e - gg * g.Kdim;
+      for (int s0 = 0; s0 < S; s0 += 32) {
+        float inner = 0.0f;
+        const int s1 = min(S, s0 + 32);
+        for (int s = s0; s < s1; s++)
+          inner += ws_w[((int64_t)s * g.G + gg) * g.Kdim + k];
+        outer += inner;
+      }
+      gW[(int64_t)k * gws + gg] = outer;
+    } else if (gb) {
+      const int gg = e - total;
+      for (int s0 = 0; s0 < S; s0 += 32) {
+        float inner = 0.0f;
+        const int s1 = min(S, s0 + 32);
+        for (int s = s0; s < s1; s++) inner += ws_b[(int64_t)s * g.G + gg];
+        outer += inner;
+      }
+      gb[gg] = outer;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side planning.
+struct IgemmPlan {
+  int S, k_per_split;
+  size_t ws_bytes;
+};
+
+IgemmPlan plan_igemm(const ConvGeom &g) {
+  IgemmPlan pl;
+  const int64_t tiles = ((g.M + IG_BM - 1) / IG_BM) * ((g.G + IG_BG - 1) / IG_BG);
+  int S = 1;
+  if (tiles < 1024 && g.Kdim > 8 * IG_BK) {
+    int64_t want = (2048 + tiles - 1) / tiles;
+    int64_t maxs = (g.Kdim + 4 * IG_BK - 1) / (4 * IG_BK);
+    S = (int)(want < maxs ? want : maxs);
+    if (S < 1) S = 1;
+  }
+  int kps = (g.Kdim + S - 1) / S;
+  kps = (kps + IG_BK - 1) / IG_BK * IG_BK;
+  S = (g.Kdim + kps - 1) / kps;
+  pl.S = S;
+  pl.k_per_split = kps;
+  pl.ws_bytes = S > 1 ? (size_t)S * g.G * g.M * sizeof(float) : 0;
+  return pl;
+}
+
+bool use_direct(const ConvGeom &g, int concat) { return concat && g.G <= 8; }
+
+struct WgradPlan {
+  int S;
+  int64_t t_per_split;
+  size_t ws_bytes;
+};
+
+WgradPlan plan_wgrad(const ConvGeom &g) {
+  WgradPlan pl;
+  const int64_t T = g.M;
+  const int gk_tiles = ((g.G + WG_BG - 1) / WG_BG) * ((g.Kdim + WG_BK - 1) / WG_BK);
+  int64_t tps = 1024;  // 32 t-steps per block: fp32 chain error ~ sqrt(1024) eps
+  int64_t S = (T + tps - 1) / tps;
+  const int64_t max_blocks = 16384;
+  if (S * gk_tiles > max_blocks) {
+    S = max_blocks / gk_tiles;
+    if (S < 1) S = 1;
+    tps = (T + S - 1) / S;
+    tps = (tps + WG_BT - 1) / WG_BT * WG_BT;
+    S = (T + tps - 1) / tps;
+  }
+  if (S < 1) S = 1;
+  pl.S = (int)S;
+  pl.t_per_split = tps;
+  pl.ws_bytes = ((size_t)S * g.G * g.Kdim + (size_t)S * g.G) * sizeof(float);
+  return pl;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t hipF_conv2d_workspace_bytes(MatrixDim in_dim, int in_height,
+                                   int in_width, int in_channel, int pad_h,
+                                   int pad_w, int kernel_height,
+                                   int kernel_width, int group) {
+  ConvGeom g = make_geom(in_dim.rows, in_height, in_width, in_channel, pad_h,
+                         pad_w, kernel_height, kernel_width, group);
+  if (g.oh <= 0 || g.ow <= 0) return 0;
+  if (use_direct(g, 1)) return 0;  // caller decides concat; direct needs none
+  return plan_igemm(g).ws_bytes;
+}
+
+int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
+                int in_channel, int pad_h, int pad_w, const float *kernel,
+                MatrixDim kernel_dim, int kernel_height, int kernel_width,
+                int group, const float *bias, float *out, MatrixDim out_dim,
+                int concat, void *workspace, size_t workspace_bytes,
+                kcnn_stream_t stream) {
+  hipStream_t st = kcnn::as_stream(stream);
+  ConvGeom g = make_geom(in_dim.rows, in_height, in_width, in_channel, pad_h,
+                         pad_w, kernel_height, kernel_width, group);
+  if (g.oh <= 0 || g.ow <= 0 || in_dim.cols != g.HW * in_channel ||
+      kernel_dim.rows != g.Kdim || kernel_dim.cols != group)
+    return (int)hipErrorInvalidValue;
+  if (concat ? (out_dim.rows != g.R || out_dim.cols != g.P * group)
+             : (out_dim.rows != g.M || out_dim.cols != group))
+    return (int)hipErrorInvalidValue;
+  if (g.M == 0) return 0;
+  if (g.M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  if (!concat) bias = nullptr;
+
+  if (use_direct(g, concat)) {
+    const unsigned blocks = (unsigned)((g.M + 255) / 256);
+#define KCNN_DIRECT(NG)                                                        \
+  hipLaunchKernelGGL(conv_direct_smallg_kernel<NG>, dim3(blocks), dim3(256), 0, \
+                     st, g, in, in_dim.stride, kernel, kernel_dim.stride, bias, \
+                     out, out_dim.stride)
+    if (g.G <= 1) KCNN_DIRECT(1);
+    else if (g.G <= 2) KCNN_DIRECT(2);
+    else if (g.G <= 4) KCNN_DIRECT(4);
+    else KCNN_DIRECT(8);
+#undef KCNN_DIRECT
+    return kcnn::launch_status();
+  }
+
+  IgemmPlan pl = plan_igemm(g);
+  if (pl.S > 1 && (workspace == nullptr || workspace_bytes < pl.ws_bytes)) {
+    pl.S = 1;
+    pl.k_per_split = (g.Kdim + IG_BK - 1) / IG_BK * IG_BK;
+  }
+  dim3 grid((unsigned)((g.M + IG_BM - 1) / IG_BM),
+            (unsigned)((g.G + IG_BG - 1) / IG_BG), (unsigned)pl.S);
+  if (pl.S > 1) {
+    float *ws = static_cast<float *>(workspace);
+    hipLaunchKernelGGL(conv_igemm_kernel<ST_PARTIAL>, grid, dim3(256), 0, st, g,
+                       in, in_dim.stride, kernel, kernel_dim.stride, nullptr,
+                       nullptr, 0, ws, pl.k_per_split);
+    int rc = kcnn::launch_status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(conv_splitk_reduce_kernel,
+                       dim3(kcnn::grid_for((int64_t)g.G * g.M)), dim3(256), 0,
+                       st, g, ws, pl.S, bias, out, out_dim.stride, concat);
+  } else if (concat) {
+    hipLaunchKernelGGL(conv_igemm_kernel<ST_CONCAT>, grid, dim3(256), 0, st, g,
+                       in, in_dim.stride, kernel, kernel_dim.stride, bias, out,
+                       out_dim.stride, nullptr, pl.k_per_split);
+  } else {
+    hipLaunchKernelGGL(conv_igemm_kernel<ST_PLAIN>, grid, dim3(256), 0, st, g,
+                       in, in_dim.stride, kernel, kernel_dim.stride, nullptr,
+                       out, out_dim.stride, nullptr, pl.k_per_split);
+  }
+  return kcnn::launch_status();
+}
+
+size_t hipF_conv2d_wgrad_workspace_bytes(MatrixDim in_dim, int in_height,
+                                         int in_width, int in_channel,
+                                         int pad_h, int pad_w,
+                                         int kernel_height, int kernel_width,
+                                         int group) {
+  ConvGeom g = make_geom(in_dim.rows, in_height, in_width, in_channel, pad_h,
+                         pad_w, kernel_height, kernel_width, group);
+  if (g.oh <= 0 || g.ow <= 0) return 0;
+  return plan_wgrad(g).ws_bytes;
+}
+
+int hipF_conv2d_wgrad(const float *in, MatrixDim in_dim, int in_height,
+                      int in_width, int in_channel, int pad_h, int pad_w,
+                      const float *out_deriv, MatrixDim out_deriv_dim,
+                      int kernel_height, int kernel_width, int group,
+                      float *grad_W, MatrixDim grad_W_dim, float *grad_b,
+                      void *workspace, size_t workspace_bytes,
+                      kcnn_stream_t stream) {
+  hipStream_t st = kcnn::as_stream(stream);
+  ConvGeom g = make_geom(in_dim.rows, in_height, in_width, in_channel, pad_h,
+                         pad_w, kernel_height, kernel_width, group);
+  if (g.oh <= 0 || g.ow <= 0 || in_dim.cols != g.HW * in_channel ||
+      out_deriv_dim.rows != g.R || out_deriv_dim.cols != g.P * group ||
+      grad_W_dim.rows != g.Kdim || grad_W_dim.cols != group)
+    return (int)hipErrorInvalidValue;
+  if (g.M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  WgradPlan pl = plan_wgrad(g);
+  if (workspace == nullptr || workspace_bytes < pl.ws_bytes)
+    return (int)hipErrorInvalidValue;
+  float *ws_w = static_cast<float *>(workspace);
+  float *ws_b = ws_w + (size_t)pl.S * g.G * g.Kdim;
+  if (g.M == 0) {
+    if (hipMemsetAsync(ws_w, 0, pl.ws_bytes, st) != hipSuccess)
+      return (int)hipErrorInvalidValue;
+  } else {
+    dim3 grid((unsigned)pl.S, (unsigned)((g.G + WG_BG - 1) / WG_BG),
+              (unsigned)((g.Kdim + WG_BK - 1) / WG_BK));
+    hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, st, g, in,
+                       in_dim.stride, out_deriv, out_deriv_dim.stride, ws_w,
+                       ws_b, pl.t_per_split);
+  }
+  int rc = kcnn::launch_status();
+  if (rc) return rc;
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel,
+                     dim3(kcnn::grid_for((int64_t)g.G * g.Kdim + g.G)),
+                     dim3(256), 0, st, g, ws_w, ws_b, pl.S, grad_W,
+                     grad_W_dim.stride, grad_b);
+  return kcnn::launch_status();
+}
+
+}  // extern "C"

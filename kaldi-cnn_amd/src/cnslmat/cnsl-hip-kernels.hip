@@ -1,0 +1,463 @@
+// cnslmat/cnsl-hip-kernels.hip -- gfx950 bandwidth kernels of the CNN hot
+// path: the reshape helpers behind CuMatrixBase::{FlipMat, PaddingZero,
+// TpBlock, TpInsideBlock, ModPermuteRow, AddMatRepVec} (conv2D.cc:213-463),
+// 3-D max pooling forward/backward (conv2D.cc:465-684) and the momentum
+// update (nnet-component-nnet0.cc:769-775, :1137-1142).
+//
+// The reference launches every op as one thread per output element on 16x16
+// blocks with int32 offsets (cnsl-cu-kernels.cu:10-529).  Here an op is a
+// grid-stride loop over a flattened index with one FastDiv per element, 256
+// threads (4 wave64s) per block, 64-bit element offsets, and -- for pooling,
+// the only one of these on the training step -- wave-contiguous output
+// columns so every wave reads and writes whole 256-B row segments.
+#include <hip/hip_runtime.h>
+
+#include "hip-util.h"
+
+using kcnn::FastDiv;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Elementwise over a [rows x cols] output.  Rows are processed in slabs so
+// the flattened index stays below 2^31 (FastDiv domain).
+template <typename F>
+__global__ __launch_bounds__(256) void elem2d_kernel(int64_t r0, uint32_t n,
+                                                     FastDiv divc, F f) {
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += gridDim.x * blockDim.x) {
+    uint32_t i, j;
+    divc.divmod(e, i, j);
+    f(r0 + (int64_t)i, (int)j);
+  }
+}
+
+template <typename F>
+int launch_elem2d(int64_t rows, int cols, F f, hipStream_t st) {
+  if (rows <= 0 || cols <= 0) return 0;
+  const int64_t max_rows = ((int64_t)1 << 31) / 2 / cols;  // keep e < 2^30
+  FastDiv divc((uint32_t)cols);
+  for (int64_t r0 = 0; r0 < rows; r0 += max_rows) {
+    const int64_t nr = rows - r0 < max_rows ? rows - r0 : max_rows;
+    const uint32_t n = (uint32_t)(nr * cols);
+    hipLaunchKernelGGL(elem2d_kernel<F>, dim3(kcnn::grid_for(n)), dim3(256), 0,
+                       st, r0, n, divc, f);
+  }
+  return kcnn::launch_status();
+}
+
+// ---- functors (one per reference kernel) -----------------------------------
+
+// conv2D.cc:120-133 / cnsl-cu-kernels.cu:10-38 (im2col).
+struct SpanRowToConvmat {
+  const float *in; MatrixDim in_dim; float *span; MatrixDim span_dim;
+  int in_height, in_width, kernel_height; int64_t row_offset;
+  FastDiv div_ks, div_kh, div_rows, div_q;
+  __device__ void operator()(int64_t i, int j) const {
+    uint32_t J, Jr, I, Ir, a, b, kx, ky;
+    div_ks.divmod((uint32_t)j, J, Jr);
+    div_rows.divmod((uint32_t)(i + row_offset), I, Ir);
+    div_q.divmod(I, b, a);                    // Q = I % q + I / q * H
+    div_kh.divmod(Jr, kx, ky);                // P = Jr % kh + Jr / kh * H
+    const int64_t col = (int64_t)a + (int64_t)b * in_height + ky +
+                        (int64_t)kx * in_height +
+                        (int64_t)J * in_height * in_width;
+    span[i * span_dim.stride + j] = in[(int64_t)Ir * in_dim.stride + col];
+  }
+};
+
+// conv2D.cc:190-196 / cnsl-cu-kernels.cu:42-59 (col2im).
+struct ConvmatToOut {
+  const float *conv; MatrixDim conv_dim; float *out; MatrixDim out_dim;
+  int64_t plane; FastDiv div_ns;
+  __device__ void operator()(int64_t i, int j) const {
+    uint32_t I, Ir;
+    div_ns.divmod((uint32_t)i, I, Ir);
+    out[(int64_t)Ir * out_dim.stride + I + j * plane] =
+        conv[i * conv_dim.stride + j];
+  }
+};
+
+// conv2D.cc:232-239 / cnsl-cu-kernels.cu:61-75.
+struct AddMatRepVec {
+  const float *vec; float *out; MatrixDim out_dim; FastDiv div_rep;
+  __device__ void operator()(int64_t i, int j) const {
+    out[i * out_dim.stride + j] += vec[div_rep.div((uint32_t)j)];
+  }
+};
+
+// conv2D.cc:270-281 / cnsl-cu-kernels.cu:78-97.
+struct FlipMat {
+  const float *orig; MatrixDim orig_dim; float *flip; MatrixDim flip_dim;
+  int ksize; FastDiv div_ks;
+  __device__ void operator()(int64_t i, int j) const {
+    const int gi = (int)div_ks.div((uint32_t)i);
+    const int p = (gi + 1) * ksize - 1 - (int)i;
+    const int64_t m = p + (int64_t)j * ksize;
+    flip[i * flip_dim.stride + j] = orig[m * orig_dim.stride + gi];
+  }
+};
+
+// conv2D.cc:318-339 / cnsl-cu-kernels.cu:100-134.
+struct PadZero {
+  const float *orig; MatrixDim orig_dim; float *pad; MatrixDim pad_dim;
+  int oh, ow, kh, kw; FastDiv div_psize, div_ph;
+  __device__ void operator()(int64_t i, int j) const {
+    uint32_t chan, p, J, I;
+    div_psize.divmod((uint32_t)j, chan, p);
+    div_ph.divmod(p, J, I);
+    float v = 0.0f;
+    if ((int)I >= kh - 1 && (int)I < kh + oh - 1 && (int)J >= kw - 1 &&
+        (int)J < kw + ow - 1) {
+      const int m = (int)I - kh + 1, n = (int)J - kw + 1;
+      v = orig[i * orig_dim.stride + (int64_t)n * oh + m +
+               (int64_t)chan * oh * ow];
+    }
+    pad[i * pad_dim.stride + j] = v;
+  }
+};
+
+// conv2D.cc:376-383 / cnsl-cu-kernels.cu:138-161.
+struct TpBlock {
+  const float *in; MatrixDim in_dim; float *out; MatrixDim out_dim;
+  int bs; FastDiv div_bs;
+  __device__ void operator()(int64_t i, int j) const {
+    uint32_t row, r;
+    div_bs.divmod((uint32_t)j, row, r);
+    out[i * out_dim.stride + j] =
+        in[(int64_t)row * in_dim.stride + i * bs + r];
+  }
+};
+
+// conv2D.cc:416-423 / cnsl-cu-kernels.cu:165-185.
+struct TpInsideBlock {
+  const float *in; MatrixDim in_dim; float *out; MatrixDim out_dim;
+  int bs; FastDiv div_bs;
+  __device__ void operator()(int64_t i, int j) const {
+    uint32_t row, r;
+    div_bs.divmod((uint32_t)i, row, r);
+    out[i * out_dim.stride + j] =
+        in[(int64_t)row * in_dim.stride + (int64_t)j * bs + r];
+  }
+};
+
+// conv2D.cc:453-460 / cnsl-cu-kernels.cu:189-210.
+struct ModPermuteRow {
+  const float *in; MatrixDim in_dim; float *out; MatrixDim out_dim;
+  int bs; FastDiv div_c;
+  __device__ void operator()(int64_t i, int j) const {
+    uint32_t pos, chan;
+    div_c.divmod((uint32_t)i, pos, chan);
+    out[((int64_t)chan * bs + pos) * out_dim.stride + j] =
+        in[i * in_dim.stride + j];
+  }
+};
+
+// cnsl-cu-kernels.cu:214-228.
+struct CopyRowsAt {
+  const float *src; MatrixDim src_dim; float *dst; MatrixDim dst_dim;
+  int64_t off;
+  __device__ void operator()(int64_t i, int j) const {
+    dst[(i + off) * dst_dim.stride + j] = src[i * src_dim.stride + j];
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Max pooling.  Window of output column j (same enumeration order as the
+// reference: channel, width, height; cnsl-cu-kernels.cu:253-263).
+struct PoolGeom {
+  int in_h, in_w, ph, pw, pc, mode;
+  int64_t plane;           // in_h * in_w
+  FastDiv div_outplane;    // oh' * ow'   (mode 0/1) | in_h*in_w (mode 2)
+  FastDiv div_outh;        // oh'
+  int out_2d, in_2d;       // mode 2
+  FastDiv div_out2d;
+};
+
+__device__ __forceinline__ int64_t pool_start(const PoolGeom &g, int j) {
+  uint32_t oc, pos;
+  g.div_outplane.divmod((uint32_t)j, oc, pos);
+  if (g.mode == 2) return (int64_t)pos;  // channel part added per element
+  uint32_t wi, hi;
+  g.div_outh.divmod(pos, wi, hi);
+  const int64_t cbase =
+      g.mode == 1 ? (int64_t)oc * g.plane : (int64_t)oc * g.pc * g.plane;
+  return cbase + (int64_t)wi * g.pw * g.in_h + (int64_t)hi * g.ph;
+}
+
+struct MaxpoolProp {
+  const float *src; MatrixDim src_dim; float *pool; MatrixDim pool_dim;
+  PoolGeom g;
+  __device__ void operator()(int64_t i, int j) const {
+    const float *row = src + i * src_dim.stride;
+    float val = -1e20f;
+    if (g.mode == 2) {  // cnsl-cu-kernels.cu:434-446
+      const int64_t pos = pool_start(g, j);
+      uint32_t oc = g.div_outplane.div((uint32_t)j), x, y;
+      g.div_out2d.divmod(oc, x, y);
+      for (int cx = 0; cx < g.pc; cx++)
+        for (int cy = 0; cy < g.pc; cy++) {
+          const int64_t ic = (int64_t)(x + cx) * g.in_2d + (y + cy);
+          const float v = row[ic * g.plane + pos];
+          if (val < v) val = v;
+        }
+    } else {            // cnsl-cu-kernels.cu:253-263 / :340-350
+      const int64_t start = pool_start(g, j);
+      for (int c = 0; c < g.pc; c++)
+        for (int w = 0; w < g.pw; w++)
+          for (int h = 0; h < g.ph; h++) {
+            const float v = row[start + h + (int64_t)w * g.in_h + c * g.plane];
+            if (val < v) val = v;
+          }
+    }
+    pool[i * pool_dim.stride + j] = val;
+  }
+};
+
+// Non-overlap backprop, scatter form: each output element owns its window
+// (disjoint windows), one writer per in_deriv element.
+struct MaxpoolBackpropDisjoint {
+  const float *in_val; MatrixDim in_dim; const float *out_val; MatrixDim ov_dim;
+  const float *out_der; MatrixDim od_dim; float *dest; MatrixDim dest_dim;
+  PoolGeom g; int write_all;
+  __device__ void operator()(int64_t i, int j) const {
+    const float o = out_val[i * ov_dim.stride + j];
+    const float e = out_der[i * od_dim.stride + j];  // own stride
+    const float *x = in_val + i * in_dim.stride;
+    float *d = dest + i * dest_dim.stride;
+    const int64_t start = pool_start(g, j);
+    for (int c = 0; c < g.pc; c++)
+      for (int w = 0; w < g.pw; w++)
+        for (int h = 0; h < g.ph; h++) {
+          const int64_t idx = start + h + (int64_t)w * g.in_h + c * g.plane;
+          const bool hit = x[idx] == o;
+          if (write_all) d[idx] = hit ? e : 0.0f;
+          else if (hit) d[idx] = e;
+        }
+  }
+};
+
+// Overlapping modes, gather form: thread per in_deriv element; sums the
+// derivatives of every output whose window contains it, in increasing output
+// column order (the order of the CPU loop conv2D.cc:645-681), from 0.
+struct MaxpoolBackpropGather {
+  const float *in_val; MatrixDim in_dim; const float *out_val; MatrixDim ov_dim;
+  const float *out_der; MatrixDim od_dim; float *dest; MatrixDim dest_dim;
+  PoolGeom g; int out_channels; int write_all; FastDiv div_plane, div_in2d;
+  __device__ void operator()(int64_t i, int col) const {
+    uint32_t ic, pos;
+    div_plane.divmod((uint32_t)col, ic, pos);
+    const float x = in_val[i * in_dim.stride + col];
+    const float *ov = out_val + i * ov_dim.stride;
+    const float *od = out_der + i * od_dim.stride;
+    float acc = 0.0f;
+    bool any = false;
+    if (g.mode == 1) {  // out channel oc covers input channels oc..oc+pc-1
+      int lo = (int)ic - g.pc + 1;
+      if (lo < 0) lo = 0;
+      int hi = (int)ic < out_channels - 1 ? (int)ic : out_channels - 1;
+      for (int oc = lo; oc <= hi; oc++) {
+        const int64_t j = (int64_t)oc * g.plane + pos;
+        if (x == ov[j]) { acc += od[j]; any = true; }
+      }
+    } else {            // overlap2D: (X,Y) in in_2d map, outputs (x,y) on out_2d
+      uint32_t X, Y;
+      div_in2d.divmod(ic, X, Y);
+      for (int xo = (int)X - g.pc + 1; xo <= (int)X; xo++) {
+        if (xo < 0 || xo >= g.out_2d) continue;
+        for (int yo = (int)Y - g.pc + 1; yo <= (int)Y; yo++) {
+          if (yo < 0 || yo >= g.out_2d) continue;
+          const int64_t j = ((int64_t)xo * g.out_2d + yo) * g.plane + pos;
+          if (x == ov[j]) { acc += od[j]; any = true; }
+        }
+      }
+    }
+    float *d = dest + i * dest_dim.stride + col;
+    if (write_all) *d = acc;
+    else if (any) *d += acc;
+  }
+};
+
+struct MomentumUpdate {
+  float *W; MatrixDim wd; float *prev; MatrixDim pd; const float *grad;
+  MatrixDim gd; float momentum, a_wd, a_g;
+  __device__ void operator()(int64_t i, int j) const {
+    float p = prev[i * pd.stride + j] * momentum;   // Scale(momentum_)
+    const float w = W[i * wd.stride + j];
+    p = a_wd * w + p;                               // AddMat(-lr*wd, W)
+    p = a_g * grad[i * gd.stride + j] + p;          // AddMat(lr, grad)
+    prev[i * pd.stride + j] = p;
+    W[i * wd.stride + j] = 1.0f * p + w;            // AddMat(1.0, prev)
+  }
+};
+
+struct BiasUpdate {
+  float *b; const float *gb; float a_g;
+  __device__ void operator()(int64_t, int j) const { b[j] = a_g * gb[j] + b[j]; }
+};
+
+PoolGeom make_pool_geom(int in_h, int in_w, int ph, int pw, int pc, int mode,
+                        int out_cols) {
+  PoolGeom g;
+  g.in_h = in_h; g.in_w = in_w; g.ph = ph; g.pw = pw; g.pc = pc; g.mode = mode;
+  g.plane = (int64_t)in_h * in_w;
+  const int oh = in_h / ph, ow = in_w / pw;
+  g.div_outplane = FastDiv((uint32_t)(mode == 2 ? in_h * in_w : oh * ow));
+  g.div_outh = FastDiv((uint32_t)oh);
+  g.out_2d = g.in_2d = 1;
+  g.div_out2d = FastDiv(1);
+  if (mode == 2) {
+    const int out_channel = out_cols / (in_h * in_w);
+    int o2 = 0;
+    while ((o2 + 1) * (o2 + 1) <= out_channel) o2++;  // (int)sqrt
+    g.out_2d = o2 > 0 ? o2 : 1;
+    g.in_2d = g.out_2d + pc - 1;
+    g.div_out2d = FastDiv((uint32_t)g.out_2d);
+  }
+  return g;
+}
+
+}  // namespace
+
+// ===========================================================================
+// extern "C" shim (include/cnsl-hip-kernels.h)
+// ===========================================================================
+extern "C" {
+
+int hipF_span_row_to_convmat(const float *in, MatrixDim in_dim, float *span,
+                             MatrixDim span_dim, int in_height, int in_width,
+                             int in_channel, int kernel_height,
+                             int kernel_width, int64_t row_offset,
+                             kcnn_stream_t stream) {
+  (void)in_channel;
+  SpanRowToConvmat f{in, in_dim, span, span_dim, in_height, in_width,
+                     kernel_height, row_offset,
+                     FastDiv((uint32_t)(kernel_height * kernel_width)),
+                     FastDiv((uint32_t)kernel_height),
+                     FastDiv((uint32_t)in_dim.rows),
+                     FastDiv((uint32_t)(in_height - kernel_height + 1))};
+  return launch_elem2d(span_dim.rows, span_dim.cols, f, kcnn::as_stream(stream));
+}
+
+int hipF_convmat_to_out(const float *conv_mat, MatrixDim conv_dim, float *out,
+                        MatrixDim out_dim, int out_height, int out_width,
+                        int num_sample, kcnn_stream_t stream) {
+  ConvmatToOut f{conv_mat, conv_dim, out, out_dim,
+                 (int64_t)out_height * out_width,
+                 FastDiv((uint32_t)num_sample)};
+  return launch_elem2d(conv_dim.rows, conv_dim.cols, f, kcnn::as_stream(stream));
+}
+
+int hipF_add_mat_rep_vec(const float *vec, int rep, float *out,
+                         MatrixDim out_dim, kcnn_stream_t stream) {
+  AddMatRepVec f{vec, out, out_dim, FastDiv((uint32_t)rep)};
+  return launch_elem2d(out_dim.rows, out_dim.cols, f, kcnn::as_stream(stream));
+}
+
+int hipF_flip_mat(const float *orig, MatrixDim orig_dim, int kernel_height,
+                  int kernel_width, int group, float *flip, MatrixDim flip_dim,
+                  kcnn_stream_t stream) {
+  (void)group;
+  const int ks = kernel_height * kernel_width;
+  FlipMat f{orig, orig_dim, flip, flip_dim, ks, FastDiv((uint32_t)ks)};
+  return launch_elem2d(flip_dim.rows, flip_dim.cols, f, kcnn::as_stream(stream));
+}
+
+int hipF_pad_zero(const float *orig, MatrixDim orig_dim, int orig_height,
+                  int orig_width, int kernel_height, int kernel_width,
+                  float *padmat, MatrixDim padmat_dim, kcnn_stream_t stream) {
+  const int ph = orig_height + 2 * (kernel_height - 1);
+  const int pw = orig_width + 2 * (kernel_width - 1);
+  PadZero f{orig, orig_dim, padmat, padmat_dim, orig_height, orig_width,
+            kernel_height, kernel_width, FastDiv((uint32_t)(ph * pw)),
+            FastDiv((uint32_t)ph)};
+  return launch_elem2d(padmat_dim.rows, padmat_dim.cols, f,
+                       kcnn::as_stream(stream));
+}
+
+int hipF_tp_block(const float *in, MatrixDim in_dim, float *out,
+                  MatrixDim out_dim, int block_size, kcnn_stream_t stream) {
+  TpBlock f{in, in_dim, out, out_dim, block_size,
+            FastDiv((uint32_t)block_size)};
+  return launch_elem2d(out_dim.rows, out_dim.cols, f, kcnn::as_stream(stream));
+}
+
+int hipF_tp_inside_block(const float *in, MatrixDim in_dim, float *out,
+                         MatrixDim out_dim, int block_size,
+                         kcnn_stream_t stream) {
+  TpInsideBlock f{in, in_dim, out, out_dim, block_size,
+                  FastDiv((uint32_t)block_size)};
+  return launch_elem2d(out_dim.rows, out_dim.cols, f, kcnn::as_stream(stream));
+}
+
+int hipF_mod_permute_row(const float *in, MatrixDim in_dim, float *out,
+                         MatrixDim out_dim, int block_size, int in_channel,
+                         kcnn_stream_t stream) {
+  ModPermuteRow f{in, in_dim, out, out_dim, block_size,
+                  FastDiv((uint32_t)in_channel)};
+  return launch_elem2d(in_dim.rows, in_dim.cols, f, kcnn::as_stream(stream));
+}
+
+int hipF_copy_rows_at(const float *src, MatrixDim src_dim, float *dest,
+                      MatrixDim dest_dim, int64_t row_offset,
+                      kcnn_stream_t stream) {
+  CopyRowsAt f{src, src_dim, dest, dest_dim, row_offset};
+  return launch_elem2d(src_dim.rows, src_dim.cols, f, kcnn::as_stream(stream));
+}
+
+int hipF_maxpool_prop(const float *src, MatrixDim src_dim, float *pool,
+                      MatrixDim pool_dim, int in_height, int in_width,
+                      int pool_height_dim, int pool_width_dim,
+                      int pool_channel_dim, int mode, kcnn_stream_t stream) {
+  if (mode != 0) pool_height_dim = pool_width_dim = 1;  // cnsl-cu-kernels.cu:316
+  PoolGeom g = make_pool_geom(in_height, in_width, pool_height_dim,
+                              pool_width_dim, pool_channel_dim, mode,
+                              pool_dim.cols);
+  MaxpoolProp f{src, src_dim, pool, pool_dim, g};
+  return launch_elem2d(pool_dim.rows, pool_dim.cols, f, kcnn::as_stream(stream));
+}
+
+int hipF_maxpool_backprop(const float *in_val, MatrixDim in_val_dim,
+                          const float *out_val, MatrixDim out_val_dim,
+                          const float *out_deriv, MatrixDim out_deriv_dim,
+                          float *dest, MatrixDim dest_dim, int in_height,
+                          int in_width, int pool_height_dim,
+                          int pool_width_dim, int pool_channel_dim, int mode,
+                          int write_all, kcnn_stream_t stream) {
+  hipStream_t st = kcnn::as_stream(stream);
+  if (mode == 0) {
+    PoolGeom g = make_pool_geom(in_height, in_width, pool_height_dim,
+                                pool_width_dim, pool_channel_dim, 0,
+                                out_val_dim.cols);
+    MaxpoolBackpropDisjoint f{in_val, in_val_dim, out_val, out_val_dim,
+                              out_deriv, out_deriv_dim, dest, dest_dim, g,
+                              write_all};
+    return launch_elem2d(out_val_dim.rows, out_val_dim.cols, f, st);
+  }
+  PoolGeom g = make_pool_geom(in_height, in_width, 1, 1, pool_channel_dim,
+                              mode, out_val_dim.cols);
+  const int plane = in_height * in_width;
+  MaxpoolBackpropGather f{in_val, in_val_dim, out_val, out_val_dim, out_deriv,
+                          out_deriv_dim, dest, dest_dim, g,
+                          out_val_dim.cols / plane, write_all,
+                          FastDiv((uint32_t)plane),
+                          FastDiv((uint32_t)g.in_2d)};
+  return launch_elem2d(in_val_dim.rows, in_val_dim.cols, f, st);
+}
+
+int hipF_momentum_update(float *W, MatrixDim W_dim, float *prev,
+                         MatrixDim prev_dim, const float *grad,
+                         MatrixDim grad_dim, float momentum, float a_wd,
+                         float a_g, float *b, const float *grad_b, int b_dim,
+                         kcnn_stream_t stream) {
+  hipStream_t st = kcnn::as_stream(stream);
+  MomentumUpdate f{W, W_dim, prev, prev_dim, grad, grad_dim, momentum, a_wd, a_g};
+  int rc = launch_elem2d(W_dim.rows, W_dim.cols, f, st);
+  if (rc == 0 && b != nullptr && grad_b != nullptr && b_dim > 0) {
+    BiasUpdate fb{b, grad_b, a_g};
+    rc = launch_elem2d(1, b_dim, fb, st);
+  }
+  return rc;
+}
+
+}  // extern "C"

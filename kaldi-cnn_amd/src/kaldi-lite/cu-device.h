@@ -1,0 +1,113 @@
+// kaldi-lite/cu-device.h -- device singleton of the MI355X build.
+//
+// Upstream Kaldi's CuDevice (cudamatrix/cu-device.h) selects the GPU, owns
+// the cuBLAS handle and a caching allocator and accumulates per-function
+// profile times (AccuProfile, used around every launch in conv2D.cc:110 ff.).
+// This one does the same for HIP/ROCm, with three MI355X-first changes:
+//   - one explicit hipStream_t that every kernel of the library is launched
+//     on (settable, so a host framework can hand its own stream in);
+//   - a caching allocator whose blocks are reused in stream order (no
+//     hipMalloc / hipFree in steady state, which would serialise the device);
+//   - profiling through hipEvents around the launches (the reference's Timer
+//     measured launch latency only).
+// There is no CPU mode: Enabled() is always true once a device is selected,
+// and selecting "no" throws -- the product path has no CPU fallback.
+#ifndef KCNN_KALDI_LITE_CU_DEVICE_H_
+#define KCNN_KALDI_LITE_CU_DEVICE_H_
+
+#include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "kaldi-common.h"
+
+namespace kaldi {
+
+#define CU_SAFE_CALL(expr)                                               \
+  do {                                                                   \
+    hipError_t e__ = (expr);                                             \
+    if (e__ != hipSuccess)                                               \
+      KALDI_ERR << "HIP error " << (int)e__ << " (" << hipGetErrorString(e__) \
+                << ") in " << #expr;                                     \
+  } while (0)
+
+#define CNSL_SAFE_CALL(expr)                                            \
+  do {                                                                  \
+    int e__ = (expr);                                                   \
+    if (e__ != 0)                                                       \
+      KALDI_ERR << "kernel launch failed: " << #expr << " -> HIP error " \
+                << e__ << " (" << hipGetErrorString((hipError_t)e__) << ")"; \
+  } while (0)
+
+class CuDevice {
+ public:
+  static CuDevice &Instantiate();
+
+  // "yes"/"optional"/"wait": use device `device_id` (or the current one if
+  // < 0); "no": throws (no CPU path in this build).
+  void SelectGpuId(const std::string &use_gpu, int device_id = -1);
+  bool Enabled() const { return active_device_ >= 0; }
+  int ActiveDevice() const { return active_device_; }
+
+  hipStream_t Stream() { EnsureInit(); return stream_; }
+  void SetStream(hipStream_t s);
+  rocblas_handle GetBlasHandle() { EnsureInit(); return blas_; }
+
+  // Caching allocator (stream-ordered reuse on Stream()).
+  void *Malloc(size_t bytes);
+  void Free(void *ptr);
+  void ReleaseCache();
+  size_t BytesInUse() const { return bytes_in_use_; }
+  size_t BytesCached() const { return bytes_cached_; }
+
+  // Stream-ordered scratch for kernels (split-K partials etc.).  Valid until
+  // the next call with a larger size; callers on Stream() only.
+  void *Workspace(size_t bytes);
+
+  // Profiling: per-function accumulated kernel milliseconds, measured with
+  // hipEvents when enabled (KCNN_PROFILE=1 or SetProfiling(true)).
+  void SetProfiling(bool on) { profiling_ = on; }
+  bool Profiling() const { return profiling_; }
+  void AccuProfile(const std::string &key, double ms);
+  std::string ProfileString() const;
+  void ResetProfile() { profile_.clear(); }
+
+  void Synchronize();
+
+ private:
+  CuDevice();
+  ~CuDevice();
+  void EnsureInit();
+
+  int active_device_ = -1;
+  hipStream_t stream_ = nullptr;
+  rocblas_handle blas_ = nullptr;
+  bool profiling_ = false;
+  std::map<std::string, std::pair<double, long>> profile_;
+
+  std::mutex mu_;
+  std::multimap<size_t, void *> free_blocks_;
+  std::map<void *, size_t> live_blocks_;
+  size_t bytes_in_use_ = 0, bytes_cached_ = 0;
+  void *ws_ = nullptr;
+  size_t ws_bytes_ = 0;
+};
+
+// Times a scope with hipEvents on the device stream when profiling is on.
+class CuProfileScope {
+ public:
+  explicit CuProfileScope(const char *key);
+  ~CuProfileScope();
+
+ private:
+  const char *key_;
+  hipEvent_t beg_ = nullptr, end_ = nullptr;
+};
+
+}  // namespace kaldi
+
+#endif  // KCNN_KALDI_LITE_CU_DEVICE_H_

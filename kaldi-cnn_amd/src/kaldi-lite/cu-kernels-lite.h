@@ -1,0 +1,28 @@
+// kaldi-lite/cu-kernels-lite.h -- internal launchers for the generic
+// CuMatrix/CuVector ops (not part of the public boundary).
+#ifndef KCNN_KALDI_LITE_CU_KERNELS_LITE_H_
+#define KCNN_KALDI_LITE_CU_KERNELS_LITE_H_
+
+#include <stddef.h>
+
+#include "cnsl-hip-kernels.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+int kl_set(float *d, MatrixDim dim, float v, kcnn_stream_t st);
+int kl_scale(float *d, MatrixDim dim, float a, kcnn_stream_t st);
+int kl_add(float *d, MatrixDim dim, float a, kcnn_stream_t st);
+int kl_add_mat(float alpha, const float *A, MatrixDim ad, int transA,
+               float beta, float *D, MatrixDim dd, kcnn_stream_t st);
+int kl_copy_rows_from_vec(const float *v, float *D, MatrixDim dd,
+                          kcnn_stream_t st);
+size_t kl_col_sum_workspace_bytes(MatrixDim md);
+int kl_col_sum(const float *M, MatrixDim md, float alpha, float beta, float *v,
+               void *ws, kcnn_stream_t st);
+int kl_dot(const float *A, MatrixDim ad, const float *B, MatrixDim bd,
+           int transB, double *out_dev, kcnn_stream_t st);
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,342 @@
+"""ctypes binding of the CPU oracle (oracle/libkcnn_oracle.so).
+
+TEST INFRASTRUCTURE ONLY -- imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg as the *checker*; the product (libkcnn.so) never
+touches it.  PARITY UNPINNED: see kcnn_oracle.h.
+
+Matrices are numpy float32 arrays, 2-D, row-contiguous (a row stride larger
+than the column count is allowed, mirroring Kaldi's pitched CuMatrix).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libkcnn_oracle.so")
+
+
+class OrcMat(ctypes.Structure):
+    _fields_ = [("data", ctypes.POINTER(ctypes.c_float)),
+                ("rows", ctypes.c_int32), ("cols", ctypes.c_int32),
+                ("stride", ctypes.c_int32)]
+
+
+class OrcConv(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "in_height", "in_width", "in_channel", "in_pad_height", "in_pad_width",
+        "kernel_height", "kernel_width", "stride", "group", "out_height",
+        "out_width")] + [
+        ("learning_rate", ctypes.c_float), ("weight_decay", ctypes.c_float),
+        ("momentum", ctypes.c_float), ("W", OrcMat),
+        ("b", ctypes.POINTER(ctypes.c_float)), ("prev", OrcMat)]
+
+
+class OrcPool(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "in_height", "in_width", "in_channel", "pool_height_dim",
+        "pool_width_dim", "pool_channel_dim", "overlap", "overlap2D")]
+
+
+class OrcFC(ctypes.Structure):
+    _fields_ = [("input_dim", ctypes.c_int32), ("output_dim", ctypes.c_int32),
+                ("learning_rate", ctypes.c_float),
+                ("weight_decay", ctypes.c_float), ("momentum", ctypes.c_float),
+                ("W", OrcMat), ("b", ctypes.POINTER(ctypes.c_float)),
+                ("prev", OrcMat)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            raise RuntimeError(f"oracle not built: {_LIB_PATH} (run make -C oracle)")
+        _lib = ctypes.CDLL(_LIB_PATH)
+        _lib.orc_last_error.restype = ctypes.c_char_p
+    return _lib
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+def _chk(rc):
+    if rc != 0:
+        raise OracleError(lib().orc_last_error().decode())
+
+
+def mat(a: np.ndarray) -> OrcMat:
+    assert a.dtype == np.float32 and a.ndim == 2, (a.dtype, a.ndim)
+    assert a.strides[1] == 4, "rows must be contiguous"
+    rows, cols = a.shape
+    stride = a.strides[0] // 4 if rows > 1 else max(cols, 1)
+    return OrcMat(a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), rows, cols,
+                  stride)
+
+
+def fptr(v: np.ndarray):
+    assert v.dtype == np.float32 and v.flags.c_contiguous
+    return v.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+class accum:
+    """Context manager selecting the oracle's reduction precision.
+
+    0 = float sequential (reference BLAS stand-in), 1 = double accumulation
+    (fp64 truth), 2 = sum of |a*b| (error-bound scale)."""
+
+    def __init__(self, mode: int):
+        self.mode = mode
+
+    def __enter__(self):
+        self.prev = lib().orc_get_accum_mode()
+        lib().orc_set_accum_mode(self.mode)
+
+    def __exit__(self, *a):
+        lib().orc_set_accum_mode(self.prev)
+
+
+def set_threads(n: int):
+    lib().orc_set_num_threads(int(n))
+
+
+# --- CuMatrixBase extensions ------------------------------------------------
+
+def conv2d(x, k, H, W, C, kh, kw, G, concat=True, out=None):
+    oh, ow = H - kh + 1, W - kw + 1
+    if out is None:
+        shape = (x.shape[0], oh * ow * G) if concat else (oh * ow * x.shape[0], G)
+        out = np.zeros(shape, np.float32)
+    _chk(lib().orc_conv2d(ctypes.byref(mat(x)), ctypes.byref(mat(k)), H, W, C,
+                          kh, kw, G, ctypes.byref(mat(out)), int(concat)))
+    return out
+
+
+def add_mat_rep_vec(m, vec, rep):
+    _chk(lib().orc_add_mat_rep_vec(ctypes.byref(mat(m)), fptr(vec), vec.shape[0], rep))
+    return m
+
+
+def flip_mat(m, kh, kw, C, G):
+    flip = np.zeros((kh * kw * G, C), np.float32)
+    _chk(lib().orc_flip_mat(ctypes.byref(mat(m)), kh, kw, C, G, ctypes.byref(mat(flip))))
+    return flip
+
+
+def padding_zero(m, H, W, C, kh, kw):
+    ph, pw = H + 2 * (kh - 1), W + 2 * (kw - 1)
+    out = np.zeros((m.shape[0], ph * pw * C), np.float32)
+    _chk(lib().orc_padding_zero(ctypes.byref(mat(m)), H, W, C, kh, kw,
+                                ctypes.byref(mat(out))))
+    return out
+
+
+def tp_block(m, C, bs):
+    out = np.zeros((C, m.shape[0] * bs), np.float32)
+    _chk(lib().orc_tp_block(ctypes.byref(mat(m)), C, bs, ctypes.byref(mat(out))))
+    return out
+
+
+def tp_inside_block(m, G, bs):
+    out = np.zeros((bs * m.shape[0], G), np.float32)
+    _chk(lib().orc_tp_inside_block(ctypes.byref(mat(m)), G, bs, ctypes.byref(mat(out))))
+    return out
+
+
+def mod_permute_row(m, C, bs):
+    out = np.zeros_like(m)
+    _chk(lib().orc_mod_permute_row(ctypes.byref(mat(m)), C, bs, ctypes.byref(mat(out))))
+    return out
+
+
+def maxpool_prop(x, H, W, ph, pw, pc, out_dim, overlap=False, overlap2D=False):
+    out = np.zeros((x.shape[0], out_dim), np.float32)
+    _chk(lib().orc_maxpool_prop(ctypes.byref(mat(x)), H, W, ph, pw, pc,
+                                int(overlap), int(overlap2D), ctypes.byref(mat(out))))
+    return out
+
+
+def maxpool_backprop(x, y, dy, H, W, ph, pw, pc, overlap=False, overlap2D=False):
+    dx = np.zeros_like(x)
+    _chk(lib().orc_maxpool_backprop(ctypes.byref(mat(x)), ctypes.byref(mat(y)),
+                                    ctypes.byref(mat(dy)), ctypes.byref(mat(dx)),
+                                    H, W, ph, pw, pc, int(overlap), int(overlap2D)))
+    return dx
+
+
+def gemm(alpha, A, tA, B, tB, beta, C):
+    _chk(lib().orc_gemm(ctypes.c_float(alpha), ctypes.byref(mat(A)), int(tA),
+                        ctypes.byref(mat(B)), int(tB), ctypes.c_float(beta),
+                        ctypes.byref(mat(C))))
+    return C
+
+
+# --- components -----------------------------------------------------------------
+
+@dataclass
+class Conv:
+    """ConvolutionComponent state (nnet-component-nnet0.h:123-145)."""
+    in_height: int
+    in_width: int
+    in_channel: int
+    kernel_height: int
+    kernel_width: int
+    group: int
+    in_pad_height: int = 0
+    in_pad_width: int = 0
+    learning_rate: float = 0.02
+    weight_decay: float = 0.0002
+    momentum: float = 0.9
+    W: np.ndarray = None
+    b: np.ndarray = None
+    prev: np.ndarray = None
+    _keep: list = field(default_factory=list, repr=False)
+
+    @property
+    def out_height(self):
+        return self.in_height + 2 * self.in_pad_height - self.kernel_height + 1
+
+    @property
+    def out_width(self):
+        return self.in_width + 2 * self.in_pad_width - self.kernel_width + 1
+
+    @property
+    def input_dim(self):
+        return self.in_height * self.in_width * self.in_channel
+
+    @property
+    def output_dim(self):
+        return self.out_height * self.out_width * self.group
+
+    def _c(self) -> OrcConv:
+        kd = self.kernel_height * self.kernel_width * self.in_channel
+        if self.W is None:
+            self.W = np.zeros((kd, self.group), np.float32)
+        if self.b is None:
+            self.b = np.zeros(self.group, np.float32)
+        if self.prev is None:
+            self.prev = np.zeros_like(self.W)
+        s = OrcConv(self.in_height, self.in_width, self.in_channel,
+                    self.in_pad_height, self.in_pad_width, self.kernel_height,
+                    self.kernel_width, 1, self.group, self.out_height,
+                    self.out_width, self.learning_rate, self.weight_decay,
+                    self.momentum, mat(self.W), fptr(self.b), mat(self.prev))
+        return s
+
+    def flip_branch(self) -> bool:
+        return bool(lib().orc_conv_flip_branch(ctypes.byref(self._c())))
+
+    def propagate(self, x):
+        out = np.zeros((x.shape[0], self.output_dim), np.float32)
+        _chk(lib().orc_conv_propagate(ctypes.byref(self._c()), ctypes.byref(mat(x)),
+                                      ctypes.byref(mat(out))))
+        return out
+
+    def backprop(self, x, dy, update=True):
+        dx = np.zeros((dy.shape[0], self.input_dim), np.float32)
+        _chk(lib().orc_conv_backprop(ctypes.byref(self._c()), ctypes.byref(mat(x)),
+                                     ctypes.byref(mat(dy)), ctypes.byref(mat(dx)),
+                                     int(update)))
+        return dx
+
+    def gradient(self, x, dy):
+        kd = self.kernel_height * self.kernel_width * self.in_channel
+        gW = np.zeros((kd, self.group), np.float32)
+        gb = np.zeros(self.group, np.float32)
+        _chk(lib().orc_conv_gradient(ctypes.byref(self._c()), ctypes.byref(mat(x)),
+                                     ctypes.byref(mat(dy)), ctypes.byref(mat(gW)),
+                                     fptr(gb)))
+        return gW, gb
+
+    def apply(self, gW, gb, num_sample):
+        _chk(lib().orc_conv_apply(ctypes.byref(self._c()), ctypes.byref(mat(gW)),
+                                  fptr(gb), int(num_sample)))
+
+
+@dataclass
+class Pool:
+    in_height: int
+    in_width: int
+    in_channel: int
+    pool_height_dim: int = 1
+    pool_width_dim: int = 1
+    pool_channel_dim: int = 1
+    overlap: bool = False
+    overlap2D: bool = False
+
+    def _c(self):
+        return OrcPool(self.in_height, self.in_width, self.in_channel,
+                       self.pool_height_dim, self.pool_width_dim,
+                       self.pool_channel_dim, int(self.overlap), int(self.overlap2D))
+
+    @property
+    def input_dim(self):
+        return self.in_height * self.in_width * self.in_channel
+
+    @property
+    def output_dim(self):
+        return lib().orc_pool_output_dim(ctypes.byref(self._c()))
+
+    def propagate(self, x):
+        return maxpool_prop(x, self.in_height, self.in_width, self.pool_height_dim,
+                            self.pool_width_dim, self.pool_channel_dim,
+                            self.output_dim, self.overlap, self.overlap2D)
+
+    def backprop(self, x, y, dy):
+        return maxpool_backprop(x, y, dy, self.in_height, self.in_width,
+                                self.pool_height_dim, self.pool_width_dim,
+                                self.pool_channel_dim, self.overlap, self.overlap2D)
+
+
+@dataclass
+class FC:
+    input_dim: int
+    output_dim: int
+    learning_rate: float = 0.02
+    weight_decay: float = 0.0002
+    momentum: float = 0.9
+    W: np.ndarray = None
+    b: np.ndarray = None
+    prev: np.ndarray = None
+
+    def _c(self):
+        if self.W is None:
+            self.W = np.zeros((self.output_dim, self.input_dim), np.float32)
+        if self.b is None:
+            self.b = np.zeros(self.output_dim, np.float32)
+        if self.prev is None:
+            self.prev = np.zeros_like(self.W)
+        return OrcFC(self.input_dim, self.output_dim, self.learning_rate,
+                     self.weight_decay, self.momentum, mat(self.W), fptr(self.b),
+                     mat(self.prev))
+
+    def propagate(self, x):
+        out = np.zeros((x.shape[0], self.output_dim), np.float32)
+        _chk(lib().orc_fc_propagate(ctypes.byref(self._c()), ctypes.byref(mat(x)),
+                                    ctypes.byref(mat(out))))
+        return out
+
+    def backprop(self, x, dy, update=True):
+        dx = np.zeros((dy.shape[0], self.input_dim), np.float32)
+        _chk(lib().orc_fc_backprop(ctypes.byref(self._c()), ctypes.byref(mat(x)),
+                                   ctypes.byref(mat(dy)), ctypes.byref(mat(dx)),
+                                   int(update)))
+        return dx
+
+    def gradient(self, x, dy):
+        gW = np.zeros((self.output_dim, self.input_dim), np.float32)
+        gb = np.zeros(self.output_dim, np.float32)
+        _chk(lib().orc_fc_gradient(ctypes.byref(self._c()), ctypes.byref(mat(x)),
+                                   ctypes.byref(mat(dy)), ctypes.byref(mat(gW)),
+                                   fptr(gb)))
+        return gW, gb
+
+    def apply(self, gW, gb, num_sample):
+        _chk(lib().orc_fc_apply(ctypes.byref(self._c()), ctypes.byref(mat(gW)),
+                                fptr(gb), int(num_sample)))

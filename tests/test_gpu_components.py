@@ -1,0 +1,244 @@
+"""GPU parity of the nnet0 components (reference nnet0/nnet-component-nnet0.cc)
+against the CPU oracle: Propagate, Backprop (data gradient, both of the
+reference's branches), Update (weight/bias gradient + momentum/decay step),
+the FC layer, Read/Write round trips and a finite-difference gradient check
+(the reference's own test pattern, nnet0/nnet-conv-test.cc:60-210).
+
+Both execution paths of the product are checked: the fused MI355X kernels
+(default) and the literal replay of the reference's CuMatrixBase call
+sequence (kcnn.set_literal_path(True)).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from _util import assert_bound, assert_same, dev, host, randn, rng, triple, with_ties
+
+pytestmark = pytest.mark.gpu
+
+CONVS = {
+    # name: (H, W, C, kh, kw, G, pad_h, pad_w)
+    "c2": (40, 11, 3, 8, 1, 128, 0, 0),                 # BASELINE c2 (flip branch)
+    "nnet_cfg_l1": (40, 21, 1, 40, 4, 128, 0, 0),       # nnet.config:2 (pad-kernel branch)
+    "nnet_cfg_l2": (1, 18, 128, 1, 3, 128, 0, 0),       # nnet.config:4
+    "c5_C3_pad": (8, 9, 256, 3, 3, 32, 1, 1),           # padded (c5 C3, fewer groups)
+    "c5_C4": (4, 9, 64, 4, 3, 256, 0, 0),               # pad-kernel branch
+    "small_pad": (5, 6, 2, 3, 3, 5, 1, 2),
+    "tiny": (3, 4, 1, 2, 2, 3, 0, 0),
+}
+
+
+def conv_line(H, W, C, kh, kw, G, ph, pw, lr=0.02):
+    oh, ow = H + 2 * ph - kh + 1, W + 2 * pw - kw + 1
+    return (f"ConvolutionComponent in-height={H} in-width={W} in-channel={C} "
+            f"in-pad-height={ph} in-pad-width={pw} kernel-height={kh} "
+            f"kernel-width={kw} stride=1 group={G} out-height={oh} out-width={ow} "
+            f"learning-rate={lr} param-stddev=0.1 bias-stddev=0.5")
+
+
+def make_pair(kc, cfg, seed):
+    H, W, C, kh, kw, G, ph, pw = cfg
+    comp = kc.Component.NewFromString(conv_line(*cfg))
+    r = rng(seed)
+    oc = O.Conv(H, W, C, kh, kw, G, in_pad_height=ph, in_pad_width=pw)
+    oc.W = randn(r, (kh * kw * C, G), 0.1)
+    oc.b = randn(r, (G,), 0.5)
+    oc.prev = randn(r, (kh * kw * C, G), 0.01)  # nonzero momentum state
+    comp.SetParam(kc.PARAM_LINEAR, dev(oc.W))
+    comp.SetParam(kc.PARAM_BIAS, dev(oc.b))
+    comp.SetParam(kc.PARAM_PREV_GRAD, dev(oc.prev))
+    return comp, oc
+
+
+@pytest.fixture(params=["fused", "literal"])
+def path(request, kc):
+    kc.set_literal_path(request.param == "literal")
+    yield request.param
+    kc.set_literal_path(False)
+
+
+@pytest.mark.parametrize("name", list(CONVS))
+def test_conv_component(kc, path, name):
+    cfg = CONVS[name]
+    H, W, C, kh, kw, G, ph, pw = cfg
+    comp, oc = make_pair(kc, cfg, seed=len(name))
+    assert comp.FlipKernelBranch() == oc.flip_branch()
+    N = 9
+    r = rng(100 + len(name))
+    x = randn(r, (N, H * W * C))
+    # Propagate (:423-446)
+    f32, y_t, y_s = triple(lambda: oc.propagate(x))
+    y = comp.Propagate(dev(x))
+    assert_bound(host(y), y_t, y_s, what=f"{name} Propagate")
+    # Backprop data gradient (:461-540), no update
+    dy = randn(r, y_t.shape)
+    _, dx_t, dx_s = triple(lambda: oc.backprop(x, dy, update=False))
+    dx = comp.Backprop(dev(x), None, dev(dy), update=False)
+    assert_bound(host(dx), dx_t, dx_s, what=f"{name} Backprop dX")
+    # Update (:738-777): compare the gradient, then the updated parameters
+    _, (gW_t, gb_t), (gW_s, gb_s) = triple(lambda: oc.gradient(x, dy))
+    g = host(comp.ComputeGradient(dev(x), dev(dy)))
+    kd = kh * kw * C
+    assert_bound(g[:kd * G].reshape(kd, G), gW_t, gW_s, what=f"{name} gW")
+    assert_bound(g[kd * G:], gb_t, gb_s, what=f"{name} gb")
+    W0, b0, p0 = oc.W.copy(), oc.b.copy(), oc.prev.copy()
+    with O.accum(1):
+        oc.backprop(x, dy, update=True)
+    comp.Backprop(dev(x), None, dev(dy), update=True)
+    lr = 0.02 / N
+    # bound: the update is W + m*prev - lr*wd*W + lr*gW; its rounding error
+    # is a few ulps of each term plus lr * (gradient error <= 1e-5 * S).
+    scale_W = np.abs(W0) + np.abs(p0) + lr * gW_s + 1e-30
+    assert_bound(host(comp.LinearParams()), oc.W, scale_W, what=f"{name} W'")
+    assert_bound(host(comp.PrevGrad()), oc.prev, np.abs(p0) + lr * gW_s + 1e-6 * np.abs(W0),
+                 what=f"{name} prev'")
+    assert_bound(host(comp.BiasParams()), oc.b, np.abs(b0) + lr * gb_s, what=f"{name} b'")
+
+
+def test_conv_update_divides_by_local_rows(kc):
+    # B10: Update divides the learning rate by in_value.NumRows() (:767).
+    cfg = CONVS["tiny"]
+    comp, oc = make_pair(kc, cfg, 3)
+    r = rng(3)
+    x = randn(r, (4, 12))
+    dy = randn(r, (4, 2 * 3 * 3))
+    gW, gb = oc.gradient(x, dy)
+    comp.Backprop(dev(x), None, dev(dy), update=True)
+    oc.apply(gW, gb, 4)
+    assert_bound(host(comp.LinearParams()), oc.W, np.abs(oc.W) + 1e-3, what="W")
+
+
+@pytest.mark.parametrize("cfg", [
+    (33, 11, 128, 1, 1, 4, False, False),
+    (8, 9, 256, 2, 1, 4, False, False),
+    (4, 3, 6, 1, 1, 3, True, False),
+    (2, 3, 16, 1, 1, 2, False, True),
+])
+def test_maxpool_component(kc, path, cfg):
+    H, W, C, ph, pw, pc, ov, ov2 = cfg
+    line = (f"MaxpoolComponent in-height={H} in-width={W} in-channel={C} "
+            f"pool-height-dim={ph} pool-width-dim={pw} pool-channel-dim={pc} "
+            f"overlap={'true' if ov else 'false'} overlap2D={'true' if ov2 else 'false'}")
+    comp = kc.Component.NewFromString(line)
+    op = O.Pool(H, W, C, ph, pw, pc, ov, ov2)
+    assert comp.OutputDim() == op.output_dim
+    r = rng(sum(cfg[:6]))
+    x = with_ties(r, (7, H * W * C))
+    y = op.propagate(x)
+    yg = comp.Propagate(dev(x))
+    assert_same(host(yg), y, "Maxpool Propagate")
+    dy = randn(r, y.shape)
+    dx = op.backprop(x, y, dy)
+    dxg = comp.Backprop(dev(x), dev(y), dev(dy))
+    assert_same(host(dxg), dx, "Maxpool Backprop")
+
+
+def test_fc_component(kc, path):
+    I, Od, N = 300, 70, 33
+    comp = kc.Component.NewFromString(
+        f"FullyConnectedComponent input-dim={I} output-dim={Od} learning-rate=0.02 "
+        f"param-stddev=0.01 bias-stddev=1 weight-decay=0.0002 momentum=0.9")
+    r = rng(5)
+    of = O.FC(I, Od)
+    of.W = randn(r, (Od, I), 0.05)
+    of.b = randn(r, (Od,), 0.5)
+    of.prev = randn(r, (Od, I), 0.01)
+    for which, v in ((0, of.W), (1, of.b), (2, of.prev)):
+        comp.SetParam(which, dev(v))
+    x = randn(r, (N, I))
+    _, y_t, y_s = triple(lambda: of.propagate(x))
+    assert_bound(host(comp.Propagate(dev(x))), y_t, y_s, what="FC Propagate")
+    dy = randn(r, (N, Od))
+    _, dx_t, dx_s = triple(lambda: of.backprop(x, dy, update=False))
+    _, (gW_t, gb_t), (gW_s, gb_s) = triple(lambda: of.gradient(x, dy))
+    W0, p0, b0 = of.W.copy(), of.prev.copy(), of.b.copy()
+    with O.accum(1):
+        of.backprop(x, dy, update=True)
+    dx = comp.Backprop(dev(x), None, dev(dy), update=True)
+    assert_bound(host(dx), dx_t, dx_s, what="FC dX")
+    lr = 0.02 / N
+    assert_bound(host(comp.LinearParams()), of.W,
+                 np.abs(W0) + np.abs(p0) + lr * gW_s, what="FC W'")
+    assert_bound(host(comp.BiasParams()), of.b, np.abs(b0) + lr * gb_s, what="FC b'")
+
+
+@pytest.mark.parametrize("binary", [True, False])
+def test_read_write_roundtrip(kc, tmp_path, binary):
+    comps = [
+        kc.Component.NewFromString(conv_line(*CONVS["small_pad"])),
+        kc.Component.NewFromString(
+            "MaxpoolComponent in-height=6 in-width=4 in-channel=8 pool-height-dim=2 "
+            "pool-width-dim=2 pool-channel-dim=2"),
+        kc.Component.NewFromString(
+            "FullyConnectedComponent input-dim=20 output-dim=7 learning-rate=0.01 "
+            "weight-decay=0.0005 momentum=0.5"),
+    ]
+    for c in comps:
+        p = tmp_path / f"{c.Type()}.{'bin' if binary else 'txt'}"
+        c.Write(p, binary)
+        c2 = kc.Component.ReadNew(p)
+        assert c2.Type() == c.Type() and c2.Info() == c.Info()
+        if c.Type() != "MaxpoolComponent":
+            for which in (0, 1, 2):
+                assert_same(host(c2.GetParam(which)), host(c.GetParam(which)),
+                            f"{c.Type()} param {which}")
+            assert c2.LearningRate() == c.LearningRate()
+
+
+def test_fd_gradient_check(kc):
+    """nnet-conv-test.cc:60-210 pattern: objective = sum(out * objf_vec);
+    predicted change tr(delta^T dX) vs observed change under a small input
+    perturbation; the same for a parameter perturbation via DotProduct."""
+    cfg = (6, 5, 2, 3, 2, 4, 0, 0)
+    comp, _ = make_pair(kc, cfg, 11)
+    import torch
+    r = rng(12)
+    x = dev(randn(r, (4, 60)).astype(np.float64).astype(np.float32))
+    y = comp.Propagate(x)
+    w = dev(randn(r, tuple(y.shape)))
+    dx = comp.Backprop(x, None, w, update=False)
+    obj = lambda xx: float((comp.Propagate(xx).double() * w.double()).sum())
+    base = obj(x)
+    for _ in range(3):
+        delta = dev(randn(r, tuple(x.shape), 1e-3))
+        pred = float((delta.double() * dx.double()).sum())
+        obs = obj(x + delta) - base
+        assert abs(pred - obs) <= 0.15 * abs(pred + obs) / 2 + 1e-4, (pred, obs)
+    # parameter gradient: grad component via SetZero(true) + Update on it
+    grad_comp = comp.Copy()
+    grad_comp.SetZero(True)
+    g = comp.ComputeGradient(x, w)
+    kd = 3 * 2 * 2
+    Wd = dev(randn(r, (kd, 4), 1e-3))
+    perturbed = comp.Copy()
+    perturbed.SetParam(kc.PARAM_LINEAR, comp.LinearParams() + Wd)
+    pred = float((Wd.double().flatten() * g[:kd * 4].double()).sum())
+    obs = float((perturbed.Propagate(x).double() * w.double()).sum()) - base
+    assert abs(pred - obs) <= 0.05 * abs(pred + obs) / 2 + 1e-4, (pred, obs)
+
+
+def test_init_from_string_quirks(kc):
+    # B5: learning-rate is effectively mandatory
+    with pytest.raises(kc.KcnnError):
+        kc.Component.NewFromString(
+            "ConvolutionComponent in-height=4 in-width=4 in-channel=1 kernel-height=2 "
+            "kernel-width=2 stride=1 group=2 out-height=3 out-width=3")
+    # B6: stride != 1 rejected
+    with pytest.raises(kc.KcnnError):
+        kc.Component.NewFromString(conv_line(4, 4, 1, 2, 2, 2, 0, 0).replace("stride=1", "stride=2"))
+    # B4: weight-decay/momentum from the config are ignored (0.0002 / 0.9)
+    c = kc.Component.NewFromString(conv_line(4, 4, 1, 2, 2, 2, 0, 0) +
+                                   " weight-decay=0.5 momentum=0.1")
+    assert "weight-decay=0.0002" in c.Info() and "momentum=0.9" in c.Info()
+    # unknown option
+    with pytest.raises(kc.KcnnError):
+        kc.Component.NewFromString(conv_line(4, 4, 1, 2, 2, 2, 0, 0) + " foo=1")
+    # bad geometry
+    with pytest.raises(kc.KcnnError):
+        kc.Component.NewFromString(conv_line(4, 4, 1, 2, 2, 2, 0, 0).replace("out-height=3", "out-height=4"))
+    # Maxpool: window must tile the map
+    with pytest.raises(kc.KcnnError):
+        kc.Component.NewFromString("MaxpoolComponent in-height=5 in-width=4 in-channel=2 "
+                                   "pool-height-dim=2 pool-width-dim=1 pool-channel-dim=1")

@@ -145,6 +145,25 @@ int hipF_conv2d_wgrad(const float *in, MatrixDim in_dim, int in_height,
                       void *workspace, size_t workspace_bytes,
                       kcnn_stream_t stream);
 
+/* Data gradient of ConvolutionComponent::Backprop (nnet-component-nnet0.cc:
+ * 461-540): in_deriv [R x H*W*C] from out_deriv [R x oh*ow*G] and the
+ * (unflipped) kernel [kh*kw*C x G] of a convolution whose input was padded
+ * by (pad_h, pad_w).  Replaces either reference branch -- PaddingZero(dY) +
+ * FlipMat(W) + Conv2D, or TpInsideBlock + FlipMat + AddMat(kTrans) + TpBlock
+ * + PaddingZero + Conv2D + TpBlock -- with no materialised intermediate
+ * (both compute the same sum).  Needs pad <= kernel - 1 (reference :533). */
+size_t hipF_conv2d_dgrad_workspace_bytes(MatrixDim out_deriv_dim,
+                                         int in_height, int in_width,
+                                         int in_channel, int pad_h, int pad_w,
+                                         int kernel_height, int kernel_width,
+                                         int group);
+int hipF_conv2d_dgrad(const float *out_deriv, MatrixDim out_deriv_dim,
+                      int in_height, int in_width, int in_channel, int pad_h,
+                      int pad_w, const float *kernel, MatrixDim kernel_dim,
+                      int kernel_height, int kernel_width, int group,
+                      float *in_deriv, MatrixDim in_deriv_dim, void *workspace,
+                      size_t workspace_bytes, kcnn_stream_t stream);
+
 /* Momentum / weight-decay step of ConvolutionComponent::Update
  * (nnet-component-nnet0.cc:769-775) and FullyConnectedComponent::UpdateSimple
  * (:1137-1142), one pass:  prev = momentum*prev + a_wd*W + a_g*grad;

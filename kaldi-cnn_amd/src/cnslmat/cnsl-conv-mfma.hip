@@ -28,37 +28,14 @@
 // nnet-component-nnet0.cc:745-775) reading X and dY once each.
 #include <hip/hip_runtime.h>
 
-#include "hip-util.h"
+#include "conv-geom.h"
 
 using kcnn::FastDiv;
+using kcnn::ConvGeom;
+using kcnn::floatx16;
+using kcnn::make_geom;
 
 namespace {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-struct ConvGeom {
-  int R, H, W, C, pad_h, pad_w, kh, kw, G, oh, ow, P, Kdim, HW;
-  int64_t M;  // R * P
-  FastDiv div_P, div_oh, div_khkw, div_kh;
-};
-
-ConvGeom make_geom(int R, int H, int W, int C, int pad_h, int pad_w, int kh,
-                   int kw, int G) {
-  ConvGeom g;
-  g.R = R; g.H = H; g.W = W; g.C = C; g.pad_h = pad_h; g.pad_w = pad_w;
-  g.kh = kh; g.kw = kw; g.G = G;
-  g.oh = H + 2 * pad_h - kh + 1;
-  g.ow = W + 2 * pad_w - kw + 1;
-  g.P = g.oh * g.ow;
-  g.Kdim = kh * kw * C;
-  g.HW = H * W;
-  g.M = (int64_t)R * g.P;
-  g.div_P = FastDiv((uint32_t)(g.P > 0 ? g.P : 1));
-  g.div_oh = FastDiv((uint32_t)(g.oh > 0 ? g.oh : 1));
-  g.div_khkw = FastDiv((uint32_t)(kh * kw));
-  g.div_kh = FastDiv((uint32_t)kh);
-  return g;
-}
 
 // Input element of im2col row k for output position (px, py) of one sample.
 __device__ __forceinline__ float gather_x(const ConvGeom &g,
@@ -309,46 +286,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(
     }
     __syncthreads();
   }
+  // partial row of this split: [G*Kdim (e = g*Kdim + k) | G (bias)]
+  const int64_t E = (int64_t)g.G * g.Kdim + g.G;
   const int kl = k0 + wk * 32 + (lane & 31);
   if (kl < g.Kdim) {
 #pragma unroll
     for (int r = 0; r < 16; r++) {
       const int gl = g0 + wg * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (gl < g.G) ws_w[((int64_t)split * g.G + gl) * g.Kdim + kl] = acc[r];
+      if (gl < g.G) ws_w[split * E + (int64_t)gl * g.Kdim + kl] = acc[r];
     }
   }
   if (blockIdx.z == 0 && tid < 64 && g0 + tid < g.G)
-    ws_b[(int64_t)split * g.G + g0 + tid] = bsum;
-}
-
-__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(
-    ConvGeom g, const float *__restrict__ ws_w, const float *__restrict__ ws_b,
-    int S, float *__restrict__ gW, int gws, float *__restrict__ gb) {
-  const int total = g.G * g.Kdim;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total + g.G;
-       e += gridDim.x * blockDim.x) {
-    float outer = 0.0f;
-    if (e < total) {
-      const int gg = e / g.Kdim, k = e - gg * g.Kdim;
-      for (int s0 = 0; s0 < S; s0 += 32) {
-        float inner = 0.0f;
-        const int s1 = min(S, s0 + 32);
-        for (int s = s0; s < s1; s++)
-          inner += ws_w[((int64_t)s * g.G + gg) * g.Kdim + k];
-        outer += inner;
-      }
-      gW[(int64_t)k * gws + gg] = outer;
-    } else if (gb) {
-      const int gg = e - total;
-      for (int s0 = 0; s0 < S; s0 += 32) {
-        float inner = 0.0f;
-        const int s1 = min(S, s0 + 32);
-        for (int s = s0; s < s1; s++) inner += ws_b[(int64_t)s * g.G + gg];
-        outer += inner;
-      }
-      gb[gg] = outer;
-    }
-  }
+    ws_b[split * E + g0 + tid] = bsum;
 }
 
 // ---------------------------------------------------------------------------
@@ -373,7 +322,9 @@ IgemmPlan plan_igemm(const ConvGeom &g) {
   S = (g.Kdim + kps - 1) / kps;
   pl.S = S;
   pl.k_per_split = kps;
-  pl.ws_bytes = S > 1 ? (size_t)S * g.G * g.M * sizeof(float) : 0;
+  pl.ws_bytes = S > 1 ? (size_t)S * g.G * g.M * sizeof(float) +
+                            kcnn_reduce_splits_ws(S, (int)(g.G * g.M))
+                      : 0;
   return pl;
 }
 
@@ -402,8 +353,15 @@ WgradPlan plan_wgrad(const ConvGeom &g) {
   if (S < 1) S = 1;
   pl.S = (int)S;
   pl.t_per_split = tps;
-  pl.ws_bytes = ((size_t)S * g.G * g.Kdim + (size_t)S * g.G) * sizeof(float);
+  const size_t E = (size_t)g.G * g.Kdim + g.G;
+  pl.ws_bytes = (size_t)S * E * sizeof(float) + kcnn_reduce_splits_ws((int)S, (int)E);
   return pl;
+}
+
+// Frame-resident kernels apply when the kernel volume is small (input layers).
+size_t wgrad_ws_bytes(const ConvGeom &g) {
+  const size_t f = kcnn_conv_wgrad_frame_ws(g);
+  return f ? f : plan_wgrad(g).ws_bytes;
 }
 
 }  // namespace
@@ -440,6 +398,10 @@ int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
   if (g.M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   if (!concat) bias = nullptr;
 
+  if (concat && kcnn_conv_fwd_frame(g, in, in_dim.stride, kernel,
+                                    kernel_dim.stride, bias, out,
+                                    out_dim.stride, st) == 0)
+    return 0;
   if (use_direct(g, concat)) {
     const unsigned blocks = (unsigned)((g.M + 255) / 256);
 #define KCNN_DIRECT(NG)                                                        \
@@ -468,9 +430,15 @@ int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
                        nullptr, 0, ws, pl.k_per_split);
     int rc = kcnn::launch_status();
     if (rc) return rc;
+    // pass 1 (groups of 32 splits) into tmp, pass 2 = reduce + store epilogue
+    const int E = (int)(g.G * g.M);
+    const int Q = (pl.S + 31) / 32;
+    float *tmp = ws + (size_t)pl.S * E;
+    rc =kcnn_reduce_splits_pass1(ws, pl.S, E, tmp, st);
+    if (rc) return rc;
     hipLaunchKernelGGL(conv_splitk_reduce_kernel,
                        dim3(kcnn::grid_for((int64_t)g.G * g.M)), dim3(256), 0,
-                       st, g, ws, pl.S, bias, out, out_dim.stride, concat);
+                       st, g, tmp, Q, bias, out, out_dim.stride, concat);
   } else if (concat) {
     hipLaunchKernelGGL(conv_igemm_kernel<ST_CONCAT>, grid, dim3(256), 0, st, g,
                        in, in_dim.stride, kernel, kernel_dim.stride, bias, out,
@@ -491,7 +459,8 @@ size_t hipF_conv2d_wgrad_workspace_bytes(MatrixDim in_dim, int in_height,
   ConvGeom g = make_geom(in_dim.rows, in_height, in_width, in_channel, pad_h,
                          pad_w, kernel_height, kernel_width, group);
   if (g.oh <= 0 || g.ow <= 0) return 0;
-  return plan_wgrad(g).ws_bytes;
+  const size_t a = kcnn_conv_wgrad_frame_ws(g), b = plan_wgrad(g).ws_bytes;
+  return a > b ? a : b;
 }
 
 int hipF_conv2d_wgrad(const float *in, MatrixDim in_dim, int in_height,
@@ -509,13 +478,20 @@ int hipF_conv2d_wgrad(const float *in, MatrixDim in_dim, int in_height,
       grad_W_dim.rows != g.Kdim || grad_W_dim.cols != group)
     return (int)hipErrorInvalidValue;
   if (g.M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  if (g.M > 0 && kcnn_conv_wgrad_frame(g, in, in_dim.stride, out_deriv,
+                                       out_deriv_dim.stride, grad_W,
+                                       grad_W_dim.stride, grad_b, workspace,
+                                       workspace_bytes, st) == 0)
+    return 0;
   WgradPlan pl = plan_wgrad(g);
   if (workspace == nullptr || workspace_bytes < pl.ws_bytes)
     return (int)hipErrorInvalidValue;
+  const int E = g.G * g.Kdim + g.G;
   float *ws_w = static_cast<float *>(workspace);
-  float *ws_b = ws_w + (size_t)pl.S * g.G * g.Kdim;
+  float *ws_b = ws_w + (size_t)g.G * g.Kdim;
+  float *tmp = ws_w + (size_t)pl.S * E;
   if (g.M == 0) {
-    if (hipMemsetAsync(ws_w, 0, pl.ws_bytes, st) != hipSuccess)
+    if (hipMemsetAsync(ws_w, 0, (size_t)pl.S * E * sizeof(float), st) != hipSuccess)
       return (int)hipErrorInvalidValue;
   } else {
     dim3 grid((unsigned)pl.S, (unsigned)((g.G + WG_BG - 1) / WG_BG),
@@ -526,11 +502,72 @@ int hipF_conv2d_wgrad(const float *in, MatrixDim in_dim, int in_height,
   }
   int rc = kcnn::launch_status();
   if (rc) return rc;
-  hipLaunchKernelGGL(conv_wgrad_reduce_kernel,
-                     dim3(kcnn::grid_for((int64_t)g.G * g.Kdim + g.G)),
-                     dim3(256), 0, st, g, ws_w, ws_b, pl.S, grad_W,
-                     grad_W_dim.stride, grad_b);
-  return kcnn::launch_status();
+  return kcnn_reduce_splits_wgrad(ws_w, pl.S, E, tmp, g.G * g.Kdim, g.Kdim,
+                                  grad_W, grad_W_dim.stride, grad_b, st);
+}
+
+size_t hipF_conv2d_dgrad_workspace_bytes(MatrixDim out_deriv_dim, int in_height,
+                                         int in_width, int in_channel,
+                                         int pad_h, int pad_w,
+                                         int kernel_height, int kernel_width,
+                                         int group) {
+  ConvGeom g = make_geom(out_deriv_dim.rows, in_height, in_width, in_channel,
+                         pad_h, pad_w, kernel_height, kernel_width, group);
+  if (g.oh <= 0 || g.ow <= 0) return 0;
+  // fallback: flipped kernel + implicit GEMM over the virtually padded dY
+  ConvGeom gt = make_geom(out_deriv_dim.rows, g.oh, g.ow, group,
+                          kernel_height - 1 - pad_h, kernel_width - 1 - pad_w,
+                          kernel_height, kernel_width, in_channel);
+  const size_t flip_bytes = (size_t)kernel_height * kernel_width * group *
+                            in_channel * sizeof(float);
+  const size_t flip_pad = (flip_bytes + 255) & ~(size_t)255;
+  return flip_pad + (use_direct(gt, 1) ? 0 : plan_igemm(gt).ws_bytes);
+}
+
+int hipF_conv2d_dgrad(const float *out_deriv, MatrixDim out_deriv_dim,
+                      int in_height, int in_width, int in_channel, int pad_h,
+                      int pad_w, const float *kernel, MatrixDim kernel_dim,
+                      int kernel_height, int kernel_width, int group,
+                      float *in_deriv, MatrixDim in_deriv_dim, void *workspace,
+                      size_t workspace_bytes, kcnn_stream_t stream) {
+  hipStream_t st = kcnn::as_stream(stream);
+  ConvGeom g = make_geom(out_deriv_dim.rows, in_height, in_width, in_channel,
+                         pad_h, pad_w, kernel_height, kernel_width, group);
+  if (g.oh <= 0 || g.ow <= 0 || out_deriv_dim.cols != g.P * group ||
+      kernel_dim.rows != g.Kdim || kernel_dim.cols != group ||
+      in_deriv_dim.rows != g.R || in_deriv_dim.cols != g.HW * in_channel ||
+      pad_h > kernel_height - 1 || pad_w > kernel_width - 1)
+    return (int)hipErrorInvalidValue;
+  if (g.R == 0) return 0;
+  if (g.M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  if (kcnn_conv_dgrad_frame(g, out_deriv, out_deriv_dim.stride, kernel,
+                            kernel_dim.stride, in_deriv, in_deriv_dim.stride,
+                            st) == 0)
+    return 0;
+  // General shapes: dX = Conv2D(virtually padded dY, FlipMat(W)) -- the
+  // reference's flip branch (nnet-component-nnet0.cc:529-540) in gather form.
+  const size_t flip_bytes = (size_t)kernel_height * kernel_width * group *
+                            in_channel * sizeof(float);
+  const size_t flip_pad = (flip_bytes + 255) & ~(size_t)255;
+  const size_t need = hipF_conv2d_dgrad_workspace_bytes(
+      out_deriv_dim, in_height, in_width, in_channel, pad_h, pad_w,
+      kernel_height, kernel_width, group);
+  if (workspace == nullptr || workspace_bytes < need)
+    return (int)hipErrorInvalidValue;
+  float *flip = static_cast<float *>(workspace);
+  MatrixDim fd;
+  fd.rows = kernel_height * kernel_width * group;
+  fd.cols = in_channel;
+  fd.stride = in_channel;
+  int rc = hipF_flip_mat(kernel, kernel_dim, kernel_height, kernel_width, group,
+                         flip, fd, stream);
+  if (rc) return rc;
+  return hipF_conv2d(out_deriv, out_deriv_dim, g.oh, g.ow, group,
+                     kernel_height - 1 - pad_h, kernel_width - 1 - pad_w, flip,
+                     fd, kernel_height, kernel_width, in_channel, nullptr,
+                     in_deriv, in_deriv_dim, 1,
+                     static_cast<char *>(workspace) + flip_pad,
+                     workspace_bytes - flip_pad, stream);
 }
 
 }  // extern "C"

@@ -1,0 +1,74 @@
+// cnslmat/conv-geom.h -- geometry shared by the convolution kernels.
+#ifndef KCNN_CNSLMAT_CONV_GEOM_H_
+#define KCNN_CNSLMAT_CONV_GEOM_H_
+
+#include "hip-util.h"
+
+namespace kcnn {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// One convolution instance: R rows (frames) of H x W x C maps (column
+// h + w*H + c*H*W), virtual zero padding (pad_h, pad_w), kernel kh x kw,
+// G output maps of oh x ow (p = px*oh + py).
+struct ConvGeom {
+  int R, H, W, C, pad_h, pad_w, kh, kw, G, oh, ow, P, Kdim, HW;
+  int64_t M;  // R * P
+  FastDiv div_P, div_oh, div_khkw, div_kh, div_H, div_HW;
+};
+
+inline ConvGeom make_geom(int R, int H, int W, int C, int pad_h, int pad_w,
+                          int kh, int kw, int G) {
+  ConvGeom g;
+  g.R = R; g.H = H; g.W = W; g.C = C; g.pad_h = pad_h; g.pad_w = pad_w;
+  g.kh = kh; g.kw = kw; g.G = G;
+  g.oh = H + 2 * pad_h - kh + 1;
+  g.ow = W + 2 * pad_w - kw + 1;
+  g.P = g.oh * g.ow;
+  g.Kdim = kh * kw * C;
+  g.HW = H * W;
+  g.M = (int64_t)R * g.P;
+  g.div_P = FastDiv((uint32_t)(g.P > 0 ? g.P : 1));
+  g.div_oh = FastDiv((uint32_t)(g.oh > 0 ? g.oh : 1));
+  g.div_khkw = FastDiv((uint32_t)(kh * kw > 0 ? kh * kw : 1));
+  g.div_kh = FastDiv((uint32_t)(kh > 0 ? kh : 1));
+  g.div_H = FastDiv((uint32_t)(H > 0 ? H : 1));
+  g.div_HW = FastDiv((uint32_t)(g.HW > 0 ? g.HW : 1));
+  return g;
+}
+
+// MFMA 32x32 accumulator register r of lane l holds row
+// (r & 3) + 8 (r >> 2) + 4 (l >> 5), column l & 31.
+__device__ __forceinline__ int mfma32_row(int r, int lane) {
+  return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+}
+
+}  // namespace kcnn
+
+// Frame-resident kernels (cnsl-conv-frame.hip).  Each returns -1 when the
+// shape is not eligible (caller falls back to the implicit-GEMM path).
+int kcnn_conv_fwd_frame(const kcnn::ConvGeom &g, const float *X, int xs,
+                        const float *K, int ks, const float *bias, float *out,
+                        int os, hipStream_t st);
+int kcnn_conv_dgrad_frame(const kcnn::ConvGeom &g, const float *dY, int dys,
+                          const float *K, int ks, float *dX, int dxs,
+                          hipStream_t st);
+size_t kcnn_conv_wgrad_frame_ws(const kcnn::ConvGeom &g);
+int kcnn_conv_wgrad_frame(const kcnn::ConvGeom &g, const float *X, int xs,
+                          const float *dY, int dys, float *gW, int gws,
+                          float *gb, void *ws, size_t ws_bytes, hipStream_t st);
+// Deterministic column sums of a [S x E] fp32 slab, out[e] = sum_s in[s][e]
+// in a fixed order: pass 1 sums groups of 32 rows into tmp [ceil(S/32) x E],
+// pass 2 sums the groups (cnsl-conv-frame.hip).
+size_t kcnn_reduce_splits_ws(int S, int E);
+int kcnn_reduce_splits(const float *in, int S, int E, float *tmp, float *out,
+                       hipStream_t st);
+int kcnn_reduce_splits_pass1(const float *in, int S, int E, float *tmp,
+                             hipStream_t st);
+// pass 2 into the implicit-GEMM wgrad layout: e = g*inner + k (e < nw) ->
+// gW[k][g]; e >= nw -> gb[e - nw].
+int kcnn_reduce_splits_wgrad(const float *in, int S, int E, float *tmp, int nw,
+                             int inner, float *gW, int gws, float *gb,
+                             hipStream_t st);
+
+#endif  // KCNN_CNSLMAT_CONV_GEOM_H_

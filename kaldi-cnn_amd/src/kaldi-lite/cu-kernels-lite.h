@@ -17,6 +17,8 @@ int kl_add_mat(float alpha, const float *A, MatrixDim ad, int transA,
                float beta, float *D, MatrixDim dd, kcnn_stream_t st);
 int kl_copy_rows_from_vec(const float *v, float *D, MatrixDim dd,
                           kcnn_stream_t st);
+int kl_sum_partials(const float *parts, int S, int m, int n, float beta,
+                    float *C, MatrixDim cd, kcnn_stream_t st);
 size_t kl_col_sum_workspace_bytes(MatrixDim md);
 int kl_col_sum(const float *M, MatrixDim md, float alpha, float beta, float *v,
                void *ws, kcnn_stream_t st);

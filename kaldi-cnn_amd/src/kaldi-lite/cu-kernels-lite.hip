@@ -86,6 +86,18 @@ __global__ __launch_bounds__(256) void kl_colsum_final(
   v[j] = beta == 0.0f ? alpha * s : beta * v[j] + alpha * s;
 }
 
+// C = sum_s P_s + beta C  (split-K partials [S][m][n], fixed order).
+struct SumPartialsF {
+  const float *p; int64_t pstride; int n; float *c; int cs; float beta; int S;
+  __device__ void operator()(int64_t i, int j) const {
+    const float *q = p + i * n + j;
+    float acc = q[0];
+    for (int s = 1; s < S; s++) acc += q[(int64_t)s * pstride];
+    float *y = c + i * cs + j;
+    *y = beta == 0.0f ? acc : acc + beta * *y;
+  }
+};
+
 // sum_{i,j} A[i][j] * op(B)[i][j] in double, one block, fixed order.
 __global__ __launch_bounds__(256) void kl_dot_kernel(
     const float *__restrict__ A, MatrixDim ad, const float *__restrict__ B,
@@ -130,6 +142,12 @@ int kl_add_mat(float alpha, const float *A, MatrixDim ad, int transA,
 int kl_copy_rows_from_vec(const float *v, float *D, MatrixDim dd,
                           kcnn_stream_t st) {
   return kl_launch(dd.rows, dd.cols, CopyRowsFromVecF{v, D, dd.stride},
+                   kcnn::as_stream(st));
+}
+int kl_sum_partials(const float *parts, int S, int m, int n, float beta,
+                    float *C, MatrixDim cd, kcnn_stream_t st) {
+  return kl_launch(m, n,
+                   SumPartialsF{parts, (int64_t)m * n, n, C, cd.stride, beta, S},
                    kcnn::as_stream(st));
 }
 size_t kl_col_sum_workspace_bytes(MatrixDim md) {

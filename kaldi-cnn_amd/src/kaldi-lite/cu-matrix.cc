@@ -2,6 +2,7 @@
 #include "cu-matrix.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <limits>
@@ -269,6 +270,42 @@ void CuMatrixBase<Real>::AddMatMat(Real alpha, const CuMatrixBase<Real> &A,
       transB == kTrans ? rocblas_operation_transpose : rocblas_operation_none;
   const rocblas_operation opA =
       transA == kTrans ? rocblas_operation_transpose : rocblas_operation_none;
+  // A thin output with a long K (the FC forward: 4096 x 1024, K = 11616)
+  // gives too few output tiles to fill 256 CUs: split K over a strided
+  // batch, then sum the partials in a fixed order.
+  int nsplit = 1;
+  {
+    const int64_t tiles = (int64_t)((m + 255) / 256) * ((n + 255) / 256);
+    if (tiles < 128 && k >= 4096) {
+      for (int s : {4, 2})
+        if (k % s == 0 && k / s >= 1024 && tiles * s <= 512) { nsplit = s; break; }
+    }
+    static const char *env = getenv("KCNN_GEMM_SPLITK");
+    if (env) {
+      const int e = atoi(env);
+      if (e >= 1 && k % e == 0) nsplit = e;
+    }
+  }
+  if (nsplit > 1) {
+    CuDevice &dev = CuDevice::Instantiate();
+    const int S_ = nsplit;
+    const int kc = k / S_;
+    const rocblas_stride sA = transA == kNoTrans ? kc : (rocblas_stride)kc * A.Stride();
+    const rocblas_stride sB = transB == kNoTrans ? (rocblas_stride)kc * B.Stride() : kc;
+    float *part = static_cast<float *>(dev.Malloc(sizeof(float) * (size_t)S_ * m * n));
+    const float zero = 0.0f;
+    rocblas_status st = rocblas_sgemm_strided_batched(
+        dev.GetBlasHandle(), opB, opA, n, m, kc, &alpha, B.Data(), B.Stride(),
+        sB, A.Data(), A.Stride(), sA, &zero, part, n, (rocblas_stride)m * n, S_);
+    int rc = st == rocblas_status_success
+                 ? kl_sum_partials(part, S_, m, n, beta, data_, Dim(), S())
+                 : -1;
+    dev.Free(part);
+    if (st != rocblas_status_success)
+      KALDI_ERR << "rocblas_sgemm_strided_batched failed with status " << (int)st;
+    CNSL_SAFE_CALL(rc);
+    return;
+  }
   rocblas_status st = rocblas_sgemm(
       CuDevice::Instantiate().GetBlasHandle(), opB, opA, n, m, k, &alpha,
       B.Data(), B.Stride(), A.Data(), A.Stride(), &beta, data_, stride_);

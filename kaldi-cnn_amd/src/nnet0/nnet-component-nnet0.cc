@@ -285,25 +285,20 @@ void ConvolutionComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
     if (LiteralPath()) {
       BackpropDataLiteral(out_deriv, in_deriv);
     } else {
-      const int32 ph = kernel_height_ - 1 - in_pad_height_,
-                  pw = kernel_width_ - 1 - in_pad_width_;
-      KALDI_ASSERT(ph >= 0 && pw >= 0 && "kernel must exceed the padding");
-      CuMatrix<BaseFloat> flip_kernel(kernel_height_ * kernel_width_ * group_,
-                                      in_channel_, kUndefined);
-      linear_params_.FlipMat(kernel_height_, kernel_width_, in_channel_, group_,
-                             &flip_kernel);                         // :536
+      KALDI_ASSERT(kernel_height_ - 1 - in_pad_height_ >= 0 &&
+                   kernel_width_ - 1 - in_pad_width_ >= 0 &&
+                   "kernel must exceed the padding");               // :533
       CuDevice &dev = CuDevice::Instantiate();
-      const size_t ws_bytes = hipF_conv2d_workspace_bytes(
-          out_deriv.Dim(), out_height_, out_width_, group_, ph, pw,
-          kernel_height_, kernel_width_, in_channel_);
+      const size_t ws_bytes = hipF_conv2d_dgrad_workspace_bytes(
+          out_deriv.Dim(), in_height_, in_width_, in_channel_, in_pad_height_,
+          in_pad_width_, kernel_height_, kernel_width_, group_);
       void *ws = ws_bytes ? dev.Workspace(ws_bytes) : nullptr;
       CuProfileScope prof("ConvolutionComponent::BackpropData");
-      CNSL_SAFE_CALL(hipF_conv2d(out_deriv.Data(), out_deriv.Dim(), out_height_,
-                                 out_width_, group_, ph, pw, flip_kernel.Data(),
-                                 flip_kernel.Dim(), kernel_height_,
-                                 kernel_width_, in_channel_, nullptr,
-                                 in_deriv->Data(), in_deriv->Dim(), 1, ws,
-                                 ws_bytes, S()));
+      CNSL_SAFE_CALL(hipF_conv2d_dgrad(
+          out_deriv.Data(), out_deriv.Dim(), in_height_, in_width_, in_channel_,
+          in_pad_height_, in_pad_width_, linear_params_.Data(),
+          linear_params_.Dim(), kernel_height_, kernel_width_, group_,
+          in_deriv->Data(), in_deriv->Dim(), ws, ws_bytes, S()));
     }
   }
   if (to_update != NULL) to_update->Update(in_value, out_deriv);    // :541

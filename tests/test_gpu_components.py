@@ -135,8 +135,8 @@ def test_maxpool_component(kc, path, cfg):
     assert_same(host(dxg), dx, "Maxpool Backprop")
 
 
-def test_fc_component(kc, path):
-    I, Od, N = 300, 70, 33
+@pytest.mark.parametrize("I,Od,N", [(300, 70, 33), (8192, 64, 40)])  # 2nd: split-K GEMM
+def test_fc_component(kc, path, I, Od, N):
     comp = kc.Component.NewFromString(
         f"FullyConnectedComponent input-dim={I} output-dim={Od} learning-rate=0.02 "
         f"param-stddev=0.01 bias-stddev=1 weight-decay=0.0002 momentum=0.9")

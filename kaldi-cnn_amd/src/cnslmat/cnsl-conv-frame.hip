@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(
     Ws[e] = (k < g.Kdim && gg < g.G) ? K[(int64_t)k * ks + gg] : 0.0f;
   }
   for (int k = tid; k < Kpad; k += 256) {
-    int2 v = make_int2(0, 0);
+    int2 v = make_int2(0, 0x7fff << 16);  // padded tap: never in bounds
     if (k < g.Kdim) {
       uint32_t c, r, kx, ky;
       g.div_khkw.divmod((uint32_t)k, c, r);
@@ -80,28 +80,26 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(
       const bool pv = p < g.P;
       uint32_t px = 0, py = 0;
       if (pv) g.div_oh.divmod((uint32_t)p, px, py);
-      for (int gs = 0; gs < Gp; gs += 32 * NGB) {
+      for (int gs = 0; gs < Gp; gs += 32 * NGB) {  // Gp: multiple of 32*NGB
         floatx16 acc[NGB];
 #pragma unroll
         for (int b = 0; b < NGB; b++) acc[b] = zero16();
         for (int s = 0; s < ksteps; s++) {
           const int k = 2 * s + (lane >> 5);
-          float bv = 0.0f;
-          if (pv && k < g.Kdim) {
-            const int2 ko = koff[k];
-            const int xx = (int)px + (ko.y >> 16) - g.pad_w;
-            const int yy = (int)py + (ko.y & 0xffff) - g.pad_h;
-            if ((unsigned)xx < (unsigned)g.W && (unsigned)yy < (unsigned)g.H)
-              bv = Xs[ko.x + xx * g.H + yy];
-          }
+          // branch-free gather: padded taps (k >= Kdim) carry zero weights,
+          // invalid positions / padding read a clamped address and are
+          // zeroed by a select (no exec-masked regions around the MFMAs).
+          const int2 ko = koff[k];
+          const int xx = (int)px + (ko.y >> 16) - g.pad_w;
+          const int yy = (int)py + (ko.y & 0xffff) - g.pad_h;
+          const bool ok = pv && (unsigned)xx < (unsigned)g.W &&
+                          (unsigned)yy < (unsigned)g.H;
+          const float xv = Xs[ok ? ko.x + xx * g.H + yy : 0];
+          const float bv = ok ? xv : 0.0f;
           const float *wrow = Ws + k * Gp + gs + (lane & 31);
 #pragma unroll
-          for (int b = 0; b < NGB; b++) {
-            if (gs + b * 32 < Gp) {
-              const float av = wrow[b * 32];
-              acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[b], 0, 0, 0);
-            }
-          }
+          for (int b = 0; b < NGB; b++)
+            acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(wrow[b * 32], bv, acc[b], 0, 0, 0);
         }
         if (pv) {
           float *orow = out + (int64_t)n * os + p;
@@ -124,42 +122,46 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// NK = G/2 k-steps, fully unrolled: every A load of a 32-position tile is
+// issued before the MFMA chain consumes it (64 x 256 B in flight per wave at
+// G = 128), which is what hides HBM latency here.  Lanes past the last
+// position read a clamped address; their Z rows are never stored.
+template <int NK>
 __global__ __launch_bounds__(256) void conv_dgrad_frame_kernel(
     ConvGeom g, const float *__restrict__ dY, int dys,
     const float *__restrict__ K, int ks, float *__restrict__ dX, int dxs,
-    int Gpe) {
+    int ZZ) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float *Wt = reinterpret_cast<float *>(smem);   // [Gpe][ZS]: Wt[g][k] = W[k][g]
-  float *Zs = Wt + Gpe * ZS;                     // [P][ZS]
+  float *Wt = reinterpret_cast<float *>(smem);   // [2*NK][32]: Wt[g][k] = W[k][g]
+  float *Zs = Wt + 2 * NK * 32;                  // [P][ZZ]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int e = tid; e < Gpe * 32; e += 256) {
+  for (int e = tid; e < 2 * NK * 32; e += 256) {
     const int gg = e >> 5, k = e & 31;
-    Wt[gg * ZS + k] = (gg < g.G && k < g.Kdim) ? K[(int64_t)k * ks + gg] : 0.0f;
+    Wt[e] = (gg < g.G && k < g.Kdim) ? K[(int64_t)k * ks + gg] : 0.0f;
   }
   const int ntile = (g.P + 31) >> 5;
-  const int gsteps = Gpe >> 1;
   const int CHW = g.C * g.HW;
   const int khkw = g.kh * g.kw;
+  const float *wcol = Wt + (lane >> 5) * 32 + (lane & 31);
 
   for (int n = blockIdx.x; n < g.R; n += gridDim.x) {
     __syncthreads();  // Wt ready / previous col2im done with Zs
     const float *dyr = dY + (int64_t)n * dys;
     for (int pt = wave; pt < ntile; pt += 4) {
       const int p = pt * 32 + (lane & 31);
-      const bool pv = p < g.P;
-      const float *col = dyr + p;
+      const int pc = p < g.P ? p : g.P - 1;
+      const float *col = dyr + pc + (int64_t)(lane >> 5) * g.P;
+      float a[NK];
+#pragma unroll
+      for (int s = 0; s < NK; s++) a[s] = col[(int64_t)(2 * s) * g.P];
       floatx16 acc = zero16();
-#pragma unroll 8
-      for (int s = 0; s < gsteps; s++) {
-        const int gg = 2 * s + (lane >> 5);
-        const float av = (pv && gg < g.G) ? col[(int64_t)gg * g.P] : 0.0f;
-        const float bv = Wt[gg * ZS + (lane & 31)];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
-      }
+#pragma unroll
+      for (int s = 0; s < NK; s++)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], wcol[s * 64], acc, 0, 0, 0);
 #pragma unroll
       for (int r = 0; r < 16; r++) {
         const int pl = pt * 32 + mfma32_row(r, lane);
-        if (pl < g.P) Zs[pl * ZS + (lane & 31)] = acc[r];
+        if (pl < g.P && (lane & 31) < g.Kdim) Zs[pl * ZZ + (lane & 31)] = acc[r];
       }
     }
     __syncthreads();
@@ -172,10 +174,10 @@ __global__ __launch_bounds__(256) void conv_dgrad_frame_kernel(
       for (int kx = 0; kx < g.kw; kx++) {
         const int px = (int)wi + g.pad_w - kx;
         if ((unsigned)px >= (unsigned)g.ow) continue;
-        const float *zr = Zs + (int64_t)(px * g.oh) * ZS + (int)c * khkw + kx * g.kh;
+        const float *zr = Zs + (int64_t)(px * g.oh) * ZZ + (int)c * khkw + kx * g.kh;
         for (int ky = 0; ky < g.kh; ky++) {
           const int py = (int)hi + g.pad_h - ky;
-          if ((unsigned)py < (unsigned)g.oh) sum += zr[py * ZS + ky];
+          if ((unsigned)py < (unsigned)g.oh) sum += zr[py * ZZ + ky];
         }
       }
       dxr[e] = sum;
@@ -222,35 +224,43 @@ __global__ __launch_bounds__(256) void conv_wgrad_frame_kernel(
     for (int su = 0; su < NSUP; su++) {
       const int g0 = (su * 4 + wave) * 32;
       if (g0 >= g.G) continue;  // wave-uniform
-      for (int pc = 0; pc < g.P; pc += 32) {
-        // stage dY[g0 .. g0+31][pc .. pc+31] (coalesced along p) -> myD[g][p]
+      // dY tile rows g0 + 2i + (lane >> 5), column pc + (lane & 31); rows past
+      // G or columns past P read a clamped address and are zeroed.
+      const int gl0 = lane >> 5, pl0 = lane & 31;
+      float nxt[16];
+      auto load_tile = [&](int pc) {
+        const bool pv = pc + pl0 < g.P;
+        const int pcl = pv ? pc + pl0 : g.P - 1;
 #pragma unroll
         for (int i = 0; i < 16; i++) {
-          const int gl = 2 * i + (lane >> 5), pl = lane & 31;
-          float v = 0.0f;
-          if (g0 + gl < g.G && pc + pl < g.P)
-            v = dyr[(int64_t)(g0 + gl) * g.P + pc + pl];
-          myD[gl * ZS + pl] = v;
+          const int gg = g0 + 2 * i + gl0;
+          const bool v = pv && gg < g.G;
+          const float x = dyr[(int64_t)(v ? gg : 0) * g.P + pcl];
+          nxt[i] = v ? x : 0.0f;
         }
+      };
+      load_tile(0);
+      for (int pc = 0; pc < g.P; pc += 32) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) myD[(2 * i + gl0) * ZS + pl0] = nxt[i];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (pc + 32 < g.P) load_tile(pc + 32);  // in flight during the MFMAs
+        // im2col operand for p = pc + 2s + (lane >> 5), walked incrementally
+        uint32_t px, py;
+        g.div_oh.divmod((uint32_t)(pc + gl0), px, py);
+        int ipx = (int)px, ipy = (int)py;
 #pragma unroll 4
         for (int s = 0; s < 16; s++) {
-          const int pl = 2 * s + (lane >> 5);
-          const int p = pc + pl;
-          float av = 0.0f;
-          if (p < g.P) {
-            if (j < g.Kdim) {
-              uint32_t px, py;
-              g.div_oh.divmod((uint32_t)p, px, py);
-              const int xx = (int)px + kx - g.pad_w, yy = (int)py + ky - g.pad_h;
-              if ((unsigned)xx < (unsigned)g.W && (unsigned)yy < (unsigned)g.H)
-                av = Xs[koff + xx * g.H + yy];
-            } else if (is_ones) {
-              av = 1.0f;
-            }
-          }
-          const float bv = myD[(lane & 31) * ZS + pl];
+          const int p = pc + 2 * s + gl0;
+          const int xx = ipx + kx - g.pad_w, yy = ipy + ky - g.pad_h;
+          const bool ok = j < g.Kdim && p < g.P && (unsigned)xx < (unsigned)g.W &&
+                          (unsigned)yy < (unsigned)g.H;
+          const float xv = Xs[ok ? koff + xx * g.H + yy : 0];
+          const float av = ok ? xv : ((is_ones && p < g.P) ? 1.0f : 0.0f);
+          const float bv = myD[(lane & 31) * ZS + 2 * s + gl0];
           acc[su] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[su], 0, 0, 0);
+          ipy += 2;
+          while (ipy >= g.oh) { ipy -= g.oh; ipx++; }
         }
       }
     }
@@ -321,14 +331,15 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
                         int os, hipStream_t st) {
   if (g.Kdim > 64 || g.P < 16) return -1;
   const int Kpad = (g.Kdim + 1) & ~1;
-  const int Gp = (g.G + 31) / 32 * 32;
+  const int ngb = g.G > 64 ? 4 : (g.G > 32 ? 2 : 1);
+  const int Gp = (g.G + 32 * ngb - 1) / (32 * ngb) * (32 * ngb);
   const size_t lds = fwd_lds(g, Kpad, Gp);
   if (lds > (size_t)kFrameLdsMax) return -1;
   const unsigned grid = frame_grid(g, 4);
-  if (Gp >= 128) {
+  if (ngb == 4) {
     hipLaunchKernelGGL(conv_fwd_frame_kernel<4>, dim3(grid), dim3(256), lds, st,
                        g, X, xs, K, ks, bias, out, os, Kpad, Gp);
-  } else if (Gp >= 64) {
+  } else if (ngb == 2) {
     hipLaunchKernelGGL(conv_fwd_frame_kernel<2>, dim3(grid), dim3(256), lds, st,
                        g, X, xs, K, ks, bias, out, os, Kpad, Gp);
   } else {
@@ -342,11 +353,16 @@ int kcnn_conv_dgrad_frame(const ConvGeom &g, const float *dY, int dys,
                           const float *K, int ks, float *dX, int dxs,
                           hipStream_t st) {
   if (g.Kdim > 32) return -1;
-  const int Gpe = (g.G + 1) & ~1;
-  const size_t lds = (size_t)(Gpe + g.P) * ZS * 4;
+  if (g.G != 64 && g.G != 128) return -1;  // NK = G/2, fully unrolled
+  const int ZZ = g.Kdim | 1;               // odd row stride: conflict-free col2im
+  const size_t lds = ((size_t)g.G * 32 + (size_t)g.P * ZZ) * 4;
   if (lds > (size_t)kFrameLdsMax) return -1;
-  hipLaunchKernelGGL(conv_dgrad_frame_kernel, dim3(frame_grid(g, 2)), dim3(256),
-                     lds, st, g, dY, dys, K, ks, dX, dxs, Gpe);
+  if (g.G == 128)
+    hipLaunchKernelGGL(conv_dgrad_frame_kernel<64>, dim3(frame_grid(g, 3)),
+                       dim3(256), lds, st, g, dY, dys, K, ks, dX, dxs, ZZ);
+  else
+    hipLaunchKernelGGL(conv_dgrad_frame_kernel<32>, dim3(frame_grid(g, 3)),
+                       dim3(256), lds, st, g, dY, dys, K, ks, dX, dxs, ZZ);
   return (int)hipGetLastError();
 }
 

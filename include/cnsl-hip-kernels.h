@@ -164,6 +164,26 @@ int hipF_conv2d_dgrad(const float *out_deriv, MatrixDim out_deriv_dim,
                       float *in_deriv, MatrixDim in_deriv_dim, void *workspace,
                       size_t workspace_bytes, kcnn_stream_t stream);
 
+/* Whole backward of ConvolutionComponent (Backprop with an update,
+ * nnet-component-nnet0.cc:461-540 + Update :738-775): in_deriv (nullable)
+ * AND grad_W / grad_b from one pass over out_deriv.  Equal to
+ * hipF_conv2d_dgrad + hipF_conv2d_wgrad (same sums; to which it falls back
+ * for shapes outside the fused kernel's range: kh*kw*C <= 31, group a
+ * multiple of 32 up to 128, oh*ow <= 384). */
+size_t hipF_conv2d_backward_workspace_bytes(MatrixDim in_dim, int in_height,
+                                            int in_width, int in_channel,
+                                            int pad_h, int pad_w,
+                                            int kernel_height, int kernel_width,
+                                            int group);
+int hipF_conv2d_backward(const float *in, MatrixDim in_dim, int in_height,
+                         int in_width, int in_channel, int pad_h, int pad_w,
+                         const float *out_deriv, MatrixDim out_deriv_dim,
+                         const float *kernel, MatrixDim kernel_dim,
+                         int kernel_height, int kernel_width, int group,
+                         float *in_deriv, MatrixDim in_deriv_dim, float *grad_W,
+                         MatrixDim grad_W_dim, float *grad_b, void *workspace,
+                         size_t workspace_bytes, kcnn_stream_t stream);
+
 /* Momentum / weight-decay step of ConvolutionComponent::Update
  * (nnet-component-nnet0.cc:769-775) and FullyConnectedComponent::UpdateSimple
  * (:1137-1142), one pass:  prev = momentum*prev + a_wd*W + a_g*grad;

@@ -140,6 +140,15 @@ int kcnn_component_compute_gradient(const kcnn_component *c,
                                     float *grad);
 int kcnn_component_apply_gradient(kcnn_component *c, const float *grad,
                                   int num_sample);
+/* Backprop without update (in_deriv nullable: no data gradient) AND
+ * ComputeGradient in one call; ConvolutionComponent runs both from a single
+ * pass over out_deriv (hipF_conv2d_backward).  in_deriv must be preallocated
+ * [rows x InputDim]. */
+int kcnn_component_backprop_gradient(const kcnn_component *c,
+                                     const float *in_value, MatrixDim in_dim,
+                                     const float *out_deriv, MatrixDim od_dim,
+                                     float *in_deriv, MatrixDim id_dim,
+                                     float *grad);
 /* ConvolutionComponent only: 1 if Backprop's reference branch is
  * "flip kernel" (nnet-component-nnet0.cc:489-497). */
 int kcnn_component_conv_flip_branch(const kcnn_component *c);

@@ -414,6 +414,23 @@ class Component:
             dim(out_deriv), ptr(grad)))
         return grad
 
+    def BackpropGradient(self, in_value, out_deriv, in_deriv=None, grad=None,
+                         want_in_deriv=True):
+        """Backprop (no update) + ComputeGradient in one call; returns
+        (in_deriv or None, grad)."""
+        import torch
+        if grad is None:
+            grad = torch.empty(self.NumGradientParams(), dtype=torch.float32,
+                               device="cuda")
+        if in_deriv is None and want_in_deriv:
+            in_deriv = empty(in_value.shape[0], self.InputDim())
+        check(lib().kcnn_component_backprop_gradient(
+            self._h, ptr(in_value), dim(in_value), ptr(out_deriv),
+            dim(out_deriv), ptr(in_deriv) if in_deriv is not None else None,
+            dim(in_deriv) if in_deriv is not None else MatrixDim(0, 0, 0),
+            ptr(grad)))
+        return in_deriv, grad
+
     def ApplyGradient(self, grad, num_sample: int):
         check(lib().kcnn_component_apply_gradient(self._h, ptr(grad), int(num_sample)))
 

@@ -418,6 +418,22 @@ int kcnn_component_apply_gradient(kcnn_component *c, const float *grad,
                                   int num_sample) {
   return guard([&] { updatable(c)->ApplyGradient(grad, num_sample); });
 }
+int kcnn_component_backprop_gradient(const kcnn_component *c,
+                                     const float *in_value, MatrixDim in_dim,
+                                     const float *out_deriv, MatrixDim od_dim,
+                                     float *in_deriv, MatrixDim id_dim,
+                                     float *grad) {
+  return guard([&] {
+    const UpdatableComponent *u = updatable(c);
+    ChunkInfo ii = chunk_info(in_dim.cols, in_dim.rows, 0);
+    ChunkInfo oi = chunk_info(od_dim.cols, od_dim.rows, 0);
+    auto x = view(in_value, in_dim);
+    CuMatrix<BaseFloat> dx;
+    if (in_deriv) borrow(&dx, in_deriv, id_dim);
+    u->BackpropGradient(ii, oi, x, x, view(out_deriv, od_dim),
+                        in_deriv ? &dx : nullptr, grad);
+  });
+}
 int kcnn_component_conv_flip_branch(const kcnn_component *c) {
   auto *cc = dynamic_cast<cnsl::nnet0::ConvolutionComponent *>(c->c);
   if (!cc) return fail("not a ConvolutionComponent");
@@ -493,9 +509,12 @@ int kcnn_nnet_backprop_component(kcnn_nnet *n, int i, const float *out_deriv,
     auto *u = dynamic_cast<UpdatableComponent *>(c);
     CuMatrix<BaseFloat> *dx = &n->deriv[i];
     if (i == 0 && skip_first_dx && u) dx = nullptr;
+    if (mode == 1 && u) {
+      u->BackpropGradient(ii, oi, n->fwd[i], n->fwd[i + 1], od, dx, grad);
+      return;
+    }
     Component *to_update = (mode == 0 && u) ? c : nullptr;
     c->Backprop(ii, oi, n->fwd[i], n->fwd[i + 1], od, to_update, dx);
-    if (mode == 1 && u) u->ComputeGradient(n->fwd[i], od, grad);
   });
 }
 

@@ -21,6 +21,8 @@
 //            falls out of the same MFMAs.  Per-workgroup partials are reduced
 //            in a fixed order (deterministic).
 #include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
 
 #include "conv-geom.h"
 
@@ -120,6 +122,319 @@ __global__ __launch_bounds__(256) void conv_fwd_frame_kernel(
     }
   }
 }
+
+// ---------------------------------------------------------------------------
+// Forward, slab-streamed: the workgroup computes one 32-map slab of a frame's
+// output (32 x P, a contiguous run of Y) into LDS, then streams it to HBM as
+// linear 16-byte-per-lane stores of whole lines.
+__global__ __launch_bounds__(256) void conv_fwd_slab_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs,
+    const float *__restrict__ K, int ks, const float *__restrict__ bias,
+    float *__restrict__ out, int os, int Kpad, int Gp, int vec_ok) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int2 *koff = reinterpret_cast<int2 *>(smem);
+  float *T = reinterpret_cast<float *>(smem + align16(Kpad * 8));   // [32][P]
+  float *Ws = T + ((32 * g.P + 3) & ~3);                             // [Kpad][Gp]
+  float *Xs = Ws + Kpad * Gp;                                        // [C*HW]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int e = tid; e < Kpad * Gp; e += 256) {
+    const int k = e / Gp, gg = e - k * Gp;
+    Ws[e] = (k < g.Kdim && gg < g.G) ? K[(int64_t)k * ks + gg] : 0.0f;
+  }
+  for (int k = tid; k < Kpad; k += 256) {
+    int2 v = make_int2(0, 0x7fff << 16);
+    if (k < g.Kdim) {
+      uint32_t c, r, kx, ky;
+      g.div_khkw.divmod((uint32_t)k, c, r);
+      g.div_kh.divmod(r, kx, ky);
+      v = make_int2((int)c * g.HW, (int)((kx << 16) | ky));
+    }
+    koff[k] = v;
+  }
+  const int CHW = g.C * g.HW;
+  const int ntile = (g.P + 31) >> 5;
+  const int ksteps = Kpad >> 1;
+  for (int n = blockIdx.x; n < g.R; n += gridDim.x) {
+    __syncthreads();
+    const float *xr = X + (int64_t)n * xs;
+    for (int e = tid; e < CHW; e += 256) Xs[e] = xr[e];
+    __syncthreads();
+    for (int gb = 0; gb < Gp; gb += 32) {
+      for (int pt = wave; pt < ntile; pt += 4) {
+        const int p = pt * 32 + (lane & 31);
+        const bool pv = p < g.P;
+        uint32_t px = 0, py = 0;
+        if (pv) g.div_oh.divmod((uint32_t)p, px, py);
+        floatx16 acc = zero16();
+        const float *wcol = Ws + gb + (lane & 31);
+        for (int s = 0; s < ksteps; s++) {
+          const int k = 2 * s + (lane >> 5);
+          const int2 ko = koff[k];
+          const int xx = (int)px + (ko.y >> 16) - g.pad_w;
+          const int yy = (int)py + (ko.y & 0xffff) - g.pad_h;
+          const bool ok = pv && (unsigned)xx < (unsigned)g.W &&
+                          (unsigned)yy < (unsigned)g.H;
+          const float xv = Xs[ok ? ko.x + xx * g.H + yy : 0];
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wcol[k * Gp], ok ? xv : 0.0f,
+                                                     acc, 0, 0, 0);
+        }
+        if (pv) {
+#pragma unroll
+          for (int r = 0; r < 16; r++) {
+            const int gl = mfma32_row(r, lane);
+            const int gg = gb + gl;
+            T[gl * g.P + p] = acc[r] + (bias && gg < g.G ? bias[gg] : 0.0f);
+          }
+        }
+      }
+      __syncthreads();
+      const int rows = g.G - gb < 32 ? g.G - gb : 32;
+      const int cnt = rows * g.P;
+      float *dst = out + (int64_t)n * os + (int64_t)gb * g.P;
+      if (vec_ok) {
+        const float4 *src4 = reinterpret_cast<const float4 *>(T);
+        float4 *dst4 = reinterpret_cast<float4 *>(dst);
+        for (int e = tid; e < (cnt >> 2); e += 256) dst4[e] = src4[e];
+        for (int e = (cnt & ~3) + tid; e < cnt; e += 256) dst[e] = T[e];
+      } else {
+        for (int e = tid; e < cnt; e += 256) dst[e] = T[e];
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused backward: data AND weight gradient from a single pass over dY.
+// dY of one frame is streamed in 32-map slabs (32 x P floats, contiguous and
+// 16-B aligned in HBM): linear dwordx4 loads, prefetched into registers one
+// slab ahead, committed to LDS.  From the LDS slab
+//   dgrad: Z[p][k] += sum_{g in slab} dY[g][p] W[k][g]   (lanes along p)
+//   wgrad: gW[k][g] += sum_p X[k-tap](p) dY[g][p]         (lanes along g;
+//          row K of the A operand = 1 gives the bias gradient)
+// Each wave owns position tiles {wave, wave+4, wave+8} for both products, so
+// no cross-wave reduction is needed; Z is col2im'ed from LDS per frame and
+// the weight-gradient partials are reduced across workgroups in fixed order.
+constexpr int BWD_THREADS = 512;  // 8 waves, one workgroup per CU
+constexpr int BWD_WAVES = BWD_THREADS / 64;
+constexpr int BWD_MAXT = 2;   // position tiles per wave (P <= 512)
+constexpr int BWD_MAXV = 8;   // float4 prefetch registers per thread
+
+// slab buffer: a 32 x SP slab, later Z [P][ZZ] and the wave-partial sums
+__host__ __device__ inline int bwd_sd_floats(int SP) {
+  const int slab = (32 * SP + 3) & ~3;
+  return slab > BWD_WAVES * 1024 ? slab : BWD_WAVES * 1024;
+}
+
+template <int NCH, bool DX>
+__global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_frame_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs,
+    const float *__restrict__ dY, int dys, const float *__restrict__ K, int ks,
+    float *__restrict__ dX, int dxs, float *__restrict__ ws_part, int ZZ,
+    int SP, FastDiv div_hp, FastDiv div_hpwp) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float *Wt = reinterpret_cast<float *>(smem);         // [NCH*32][32]
+  float *Sd = Wt + NCH * 32 * 32;                      // [32][SP]  (16-B aligned)
+  float *Xs = Sd + bwd_sd_floats(SP) + 32;             // [C][Wp][Hp] + {1}
+  int *qtab = reinterpret_cast<int *>(Xs + ((g.C * (g.H + 2 * g.pad_h) *
+                                              (g.W + 2 * g.pad_w) + 4) & ~3));
+  float *Zs = Sd;                                       // [P][ZZ] after the slabs
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l = lane & 31, h = lane >> 5;
+  for (int e = tid; e < NCH * 32 * 32; e += BWD_THREADS) {
+    const int gg = e >> 5, k = e & 31;
+    Wt[e] = (gg < g.G && k < g.Kdim) ? K[(int64_t)k * ks + gg] : 0.0f;
+  }
+  // wgrad A operand of this lane = row l of the [Kdim+1 x P] im2col tile,
+  // read as Xs[min(abase + qmul * qtab[p], CHWp)] (byte offsets):
+  //   conv row l < Kdim: abase = its tap offset in the zero-padded frame
+  //     map, qtab[p] = px*Hp + py (no bounds tests);
+  //   row Kdim and above: the constant slot Xs[CHWp] = 1 (row Kdim is the
+  //     bias gradient, rows above are never stored);
+  //   p >= P: qtab = huge, clamps to the constant slot, and B is masked to
+  //     +0, so padded positions add exact zeros (finite * +0).
+  const int Hp = g.H + 2 * g.pad_h, Wp = g.W + 2 * g.pad_w;
+  const int CHWp = g.C * Hp * Wp;
+  int abase = CHWp * 4, qmul = 0;
+  if (l < g.Kdim) {
+    uint32_t c, r, qx, qy;
+    g.div_khkw.divmod((uint32_t)l, c, r);
+    g.div_kh.divmod(r, qx, qy);
+    abase = ((int)c * Hp * Wp + (int)qx * Hp + (int)qy) * 4;
+    qmul = 1;
+  }
+  if (tid == 0) Xs[CHWp] = 1.0f;
+  for (int p = tid; p < ((g.P + 31) & ~31); p += BWD_THREADS) {
+    uint32_t px, py;
+    g.div_oh.divmod((uint32_t)p, px, py);
+    qtab[p] = p < g.P ? ((int)px * Hp + (int)py) * 4 : 0x3fffffff;
+  }
+  const uint32_t amax = (uint32_t)CHWp * 4;
+  const char *Xb = reinterpret_cast<const char *>(Xs);
+  const bool unpadded = g.pad_h == 0 && g.pad_w == 0;
+  const int CHW = g.C * g.HW;
+  const int ntile = (g.P + 31) >> 5;
+  const int nv4 = 8 * g.P;  // float4 per slab (32 * P / 4)
+
+  floatx16 wacc[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; c++) wacc[c] = zero16();
+  // one slab in flight per thread: BWD_MAXV float4 registers (scalars, so
+  // they stay in VGPRs), 16-B aligned linear loads of the 32 x P slab
+  float4 p0, p1, p2, p3, p4, p5, p6, p7;
+#define KCNN_SLAB_REGS(X) X(0, p0) X(1, p1) X(2, p2) X(3, p3) X(4, p4) X(5, p5) \
+  X(6, p6) X(7, p7)
+#define KCNN_SLAB_LOAD(i, r) \
+  if (tid + BWD_THREADS * (i) < nv4) r = src4[tid + BWD_THREADS * (i)];
+#define KCNN_SLAB_STORE(i, r) \
+  if (tid + BWD_THREADS * (i) < nv4) dst4[tid + BWD_THREADS * (i)] = r;
+  float4 *dst4 = reinterpret_cast<float4 *>(Sd);
+  if (blockIdx.x < (unsigned)g.R) {
+    const float4 *src4 = reinterpret_cast<const float4 *>(dY + (int64_t)blockIdx.x * dys);
+    KCNN_SLAB_REGS(KCNN_SLAB_LOAD)
+  }
+  for (int n = blockIdx.x; n < g.R; n += gridDim.x) {
+    __syncthreads();  // previous frame's Zs / Xs reads are done
+    const float *xr = X + (int64_t)n * xs;
+    if (unpadded) {
+      for (int e = tid; e < CHW; e += BWD_THREADS) Xs[e] = xr[e];
+    } else {
+      for (int e = tid; e < CHWp; e += BWD_THREADS) {
+        uint32_t c, r, wp, hp;
+        div_hpwp.divmod((uint32_t)e, c, r);
+        div_hp.divmod(r, wp, hp);
+        const int wi = (int)wp - g.pad_w, hi = (int)hp - g.pad_h;
+        Xs[e] = ((unsigned)wi < (unsigned)g.W && (unsigned)hi < (unsigned)g.H)
+                    ? xr[(int)c * g.HW + wi * g.H + hi] : 0.0f;
+      }
+    }
+    floatx16 zacc[BWD_MAXT];
+#pragma unroll
+    for (int t = 0; t < BWD_MAXT; t++) zacc[t] = zero16();
+    // wgrad A operands of this frame (im2col values of the wave's tiles):
+    // identical for every slab, so gathered once per frame into registers
+    float ain[BWD_MAXT][16];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++) {
+      KCNN_SLAB_REGS(KCNN_SLAB_STORE)
+      __syncthreads();
+      {
+        const int nn = ch + 1 < NCH ? n : n + (int)gridDim.x;
+        const int cc = ch + 1 < NCH ? ch + 1 : 0;
+        if (nn < g.R) {
+          const float4 *src4 = reinterpret_cast<const float4 *>(
+              dY + (int64_t)nn * dys + (int64_t)cc * 32 * g.P);
+          KCNN_SLAB_REGS(KCNN_SLAB_LOAD)
+        }
+      }
+      const float *wrow = Wt + (ch * 32 + h) * 32 + l;
+#pragma unroll
+      for (int t = 0; t < BWD_MAXT; t++) {
+        // tiles wave, wave + 8: with waves w and w + 4 sharing a SIMD, every
+        // SIMD gets the same tile count (wave-uniform skip of surplus tiles)
+        __builtin_amdgcn_sched_barrier(0);
+        const int pt = wave + BWD_WAVES * t;
+        if (pt >= ntile) continue;
+        int pb = pt * 32;
+        // opaque per iteration: keeps the frame-invariant operand addresses
+        // of all tiles from being hoisted out of the frame loop (that would
+        // pin ~150 VGPRs)
+        asm volatile("" : "+s"(pb));
+        const int ph = pb + h;
+        if (ch == 0) {
+          const int *qrow = qtab + ph;
+#pragma unroll
+          for (int s = 0; s < 16; s++) {
+            const uint32_t off = min((uint32_t)(abase + qmul * qrow[2 * s]), amax);
+            ain[t][s] = *reinterpret_cast<const float *>(Xb + off);
+          }
+        }
+        if (DX) {
+          const int pa = pb + l < g.P ? pb + l : g.P - 1;
+          const float *srow = Sd + h * SP + pa;
+#pragma unroll
+          for (int s = 0; s < 16; s++)
+            zacc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                srow[2 * s * SP], wrow[2 * s * 32], zacc[t], 0, 0, 0);
+        }
+        const float *scol = Sd + l * SP + ph;
+        if (pb + 32 <= g.P) {  // wave-uniform: a full tile
+#pragma unroll
+          for (int s = 0; s < 16; s++)
+            wacc[ch] = __builtin_amdgcn_mfma_f32_32x32x2f32(ain[t][s], scol[2 * s],
+                                                           wacc[ch], 0, 0, 0);
+        } else {
+          // B bit-masked to +0 past P (the row tail reads the next map's
+          // data); A is finite there (the clamped constant slot)
+#pragma unroll
+          for (int s = 0; s < 16; s++) {
+            const bool pin = ph + 2 * s < g.P;
+            const float bv = __uint_as_float(__float_as_uint(scol[2 * s]) &
+                                             (pin ? 0xffffffffu : 0u));
+            wacc[ch] = __builtin_amdgcn_mfma_f32_32x32x2f32(ain[t][s], bv, wacc[ch], 0, 0, 0);
+          }
+        }
+      }
+      __syncthreads();  // slab consumed
+    }
+    if (DX) {
+#pragma unroll
+      for (int t = 0; t < BWD_MAXT; t++) {
+        const int pt = wave + BWD_WAVES * t;
+        if (pt >= ntile) continue;
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const int pl = pt * 32 + mfma32_row(r, lane);
+          if (pl < g.P && l < g.Kdim) Zs[pl * ZZ + l] = zacc[t][r];
+        }
+      }
+      __syncthreads();
+      float *dxr = dX + (int64_t)n * dxs;
+      const int khkw = g.kh * g.kw;
+      for (int e = tid; e < CHW; e += BWD_THREADS) {
+        uint32_t c, q, wi, hi;
+        g.div_HW.divmod((uint32_t)e, c, q);
+        g.div_H.divmod(q, wi, hi);
+        float sum = 0.0f;
+        for (int kxx = 0; kxx < g.kw; kxx++) {
+          const int px = (int)wi + g.pad_w - kxx;
+          if ((unsigned)px >= (unsigned)g.ow) continue;
+          const float *zr = Zs + (int64_t)(px * g.oh) * ZZ + (int)c * khkw + kxx * g.kh;
+          for (int kyy = 0; kyy < g.kh; kyy++) {
+            const int py = (int)hi + g.pad_h - kyy;
+            if ((unsigned)py < (unsigned)g.oh) sum += zr[py * ZZ + kyy];
+          }
+        }
+        dxr[e] = sum;
+      }
+    }
+  }
+  // sum the waves' partials (each covers its own position tiles) through
+  // LDS in a fixed wave order, then one [Kdim+1][G] partial per workgroup
+  const int E = (g.Kdim + 1) * g.G;
+  float *dst = ws_part + (int64_t)blockIdx.x * E;
+  float *red = Sd;  // [BWD_WAVES][32 * 32]; 32 KB <= the slab buffer
+#pragma unroll
+  for (int ch = 0; ch < NCH; ch++) {
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; r++)
+      red[wave * 1024 + mfma32_row(r, lane) * 32 + l] = wacc[ch][r];
+    __syncthreads();
+    for (int e = tid; e < 1024; e += BWD_THREADS) {
+      const int i = e >> 5, j = e & 31;
+      if (i > g.Kdim) continue;
+      float sum = 0.0f;
+#pragma unroll
+      for (int w = 0; w < BWD_WAVES; w++) sum += red[w * 1024 + e];
+      dst[i * g.G + ch * 32 + j] = sum;
+    }
+  }
+}
+#undef KCNN_SLAB_LOAD
+#undef KCNN_SLAB_STORE
+#undef KCNN_SLAB_REGS
 
 // ---------------------------------------------------------------------------
 // NK = G/2 k-steps, fully unrolled: every A load of a 32-position tile is
@@ -326,11 +641,29 @@ unsigned frame_grid(const ConvGeom &g, int blocks_per_cu) {
 
 }  // namespace
 
+static int env_int(const char *name, int dflt) {
+  const char *s = getenv(name);
+  return s && *s ? atoi(s) : dflt;
+}
+
 int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
                         const float *K, int ks, const float *bias, float *out,
                         int os, hipStream_t st) {
   if (g.Kdim > 64 || g.P < 16) return -1;
   const int Kpad = (g.Kdim + 1) & ~1;
+  static const int variant = env_int("KCNN_FWD_VARIANT", 1);
+  if (variant == 1) {
+    // slab-streamed: T [32][P] staged in LDS, written as whole 16-B lines
+    const int Gp = (g.G + 31) & ~31;
+    const size_t lds = (size_t)align16(Kpad * 8) + (size_t)((32 * g.P + 3) & ~3) * 4 +
+                       (size_t)Kpad * Gp * 4 + (size_t)g.C * g.HW * 4;
+    if (lds <= (size_t)kFrameLdsMax) {
+      const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0);
+      hipLaunchKernelGGL(conv_fwd_slab_kernel, dim3(frame_grid(g, 2)), dim3(256),
+                         lds, st, g, X, xs, K, ks, bias, out, os, Kpad, Gp, vec_ok);
+      return (int)hipGetLastError();
+    }
+  }
   const int ngb = g.G > 64 ? 4 : (g.G > 32 ? 2 : 1);
   const int Gp = (g.G + 32 * ngb - 1) / (32 * ngb) * (32 * ngb);
   const size_t lds = fwd_lds(g, Kpad, Gp);
@@ -393,6 +726,69 @@ int kcnn_conv_wgrad_frame(const ConvGeom &g, const float *X, int xs,
   else
     hipLaunchKernelGGL(conv_wgrad_frame_kernel<2>, dim3(S), dim3(256), lds, st,
                        g, X, xs, dY, dys, part);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  const int Q = (S + 31) / 32;
+  hipLaunchKernelGGL(reduce_pass1, dim3((E + 255) / 256, Q), dim3(256), 0, st,
+                     part, S, E, tmp);
+  hipLaunchKernelGGL(reduce_pass2, dim3((E + 255) / 256), dim3(256), 0, st, tmp,
+                     Q, E, g.Kdim * g.G, g.G, 0, gW, gws, gb);
+  return (int)hipGetLastError();
+}
+
+static size_t bwd_lds(const ConvGeom &g, int SP) {
+  const int NCH = g.G / 32;
+  const size_t chwp = (size_t)g.C * (g.H + 2 * g.pad_h) * (g.W + 2 * g.pad_w);
+  return ((size_t)NCH * 32 * 32 + (size_t)bwd_sd_floats(SP) + 32 +
+          ((chwp + 4) & ~(size_t)3) + (size_t)((g.P + 31) & ~31)) * 4;
+}
+
+static int bwd_sp(const ConvGeom &g) { return g.P; }  // P odd: conflict-free slab reads
+
+size_t kcnn_conv_bwd_frame_ws(const ConvGeom &g) {
+  if (g.Kdim > 31 || g.G % 32 != 0 || g.G > 128 || g.G == 0) return 0;
+  if (g.P < 16 || g.P > 32 * BWD_WAVES * BWD_MAXT || 8 * g.P > BWD_THREADS * BWD_MAXV)
+    return 0;
+  if (bwd_lds(g, bwd_sp(g)) > (size_t)kFrameLdsMax) return 0;
+  const int S = (int)frame_grid(g, 1);
+  const int E = (g.Kdim + 1) * g.G;
+  return (size_t)S * E * 4 + kcnn_reduce_splits_ws(S, E);
+}
+
+int kcnn_conv_bwd_frame(const ConvGeom &g, const float *X, int xs,
+                        const float *dY, int dys, const float *K, int ks,
+                        float *dX, int dxs, float *gW, int gws, float *gb,
+                        void *ws, size_t ws_bytes, hipStream_t st) {
+  static const int enabled = env_int("KCNN_FUSED_BWD", 1);
+  if (!enabled) return -1;
+  const size_t need = kcnn_conv_bwd_frame_ws(g);
+  if (need == 0 || ws == nullptr || ws_bytes < need) return -1;
+  if ((uintptr_t)dY % 16 != 0 || dys % 4 != 0) return -1;  // linear dwordx4 slabs
+  const int S = (int)frame_grid(g, 1);
+  const int E = (g.Kdim + 1) * g.G;
+  const int SP = bwd_sp(g);
+  const int ZZ = g.Kdim | 1;
+  const size_t lds = bwd_lds(g, SP);
+  float *part = static_cast<float *>(ws);
+  float *tmp = part + (size_t)S * E;
+  const int Hp = g.H + 2 * g.pad_h, Wp = g.W + 2 * g.pad_w;
+  const FastDiv dhp((uint32_t)Hp), dhpwp((uint32_t)(Hp * Wp));
+#define KCNN_BWD_LAUNCH(NCH)                                                      \
+  do {                                                                            \
+    if (dX)                                                                       \
+      hipLaunchKernelGGL((conv_bwd_frame_kernel<NCH, true>), dim3(S), dim3(BWD_THREADS), \
+                         lds, st, g, X, xs, dY, dys, K, ks, dX, dxs, part, ZZ, SP, dhp, dhpwp); \
+    else                                                                          \
+      hipLaunchKernelGGL((conv_bwd_frame_kernel<NCH, false>), dim3(S), dim3(BWD_THREADS), \
+                         lds, st, g, X, xs, dY, dys, K, ks, dX, dxs, part, ZZ, SP, dhp, dhpwp); \
+  } while (0)
+  switch (g.G / 32) {
+    case 1: KCNN_BWD_LAUNCH(1); break;
+    case 2: KCNN_BWD_LAUNCH(2); break;
+    case 3: KCNN_BWD_LAUNCH(3); break;
+    default: KCNN_BWD_LAUNCH(4); break;
+  }
+#undef KCNN_BWD_LAUNCH
   int rc = (int)hipGetLastError();
   if (rc) return rc;
   const int Q = (S + 31) / 32;

@@ -570,4 +570,69 @@ int hipF_conv2d_dgrad(const float *out_deriv, MatrixDim out_deriv_dim,
                      workspace_bytes - flip_pad, stream);
 }
 
+size_t hipF_conv2d_backward_workspace_bytes(MatrixDim in_dim, int in_height,
+                                            int in_width, int in_channel,
+                                            int pad_h, int pad_w,
+                                            int kernel_height, int kernel_width,
+                                            int group) {
+  ConvGeom g = make_geom(in_dim.rows, in_height, in_width, in_channel, pad_h,
+                         pad_w, kernel_height, kernel_width, group);
+  if (g.oh <= 0 || g.ow <= 0) return 0;
+  MatrixDim od;
+  od.rows = in_dim.rows;
+  od.cols = g.P * group;
+  od.stride = od.cols;
+  size_t a = kcnn_conv_bwd_frame_ws(g);
+  const size_t b = hipF_conv2d_dgrad_workspace_bytes(
+      od, in_height, in_width, in_channel, pad_h, pad_w, kernel_height,
+      kernel_width, group);
+  const size_t c = hipF_conv2d_wgrad_workspace_bytes(
+      in_dim, in_height, in_width, in_channel, pad_h, pad_w, kernel_height,
+      kernel_width, group);
+  if (b > a) a = b;
+  return c > a ? c : a;
+}
+
+int hipF_conv2d_backward(const float *in, MatrixDim in_dim, int in_height,
+                         int in_width, int in_channel, int pad_h, int pad_w,
+                         const float *out_deriv, MatrixDim out_deriv_dim,
+                         const float *kernel, MatrixDim kernel_dim,
+                         int kernel_height, int kernel_width, int group,
+                         float *in_deriv, MatrixDim in_deriv_dim, float *grad_W,
+                         MatrixDim grad_W_dim, float *grad_b, void *workspace,
+                         size_t workspace_bytes, kcnn_stream_t stream) {
+  hipStream_t st = kcnn::as_stream(stream);
+  ConvGeom g = make_geom(in_dim.rows, in_height, in_width, in_channel, pad_h,
+                         pad_w, kernel_height, kernel_width, group);
+  if (g.oh <= 0 || g.ow <= 0 || in_dim.cols != g.HW * in_channel ||
+      out_deriv_dim.rows != g.R || out_deriv_dim.cols != g.P * group ||
+      kernel_dim.rows != g.Kdim || kernel_dim.cols != group ||
+      grad_W_dim.rows != g.Kdim || grad_W_dim.cols != group || grad_W == nullptr)
+    return (int)hipErrorInvalidValue;
+  if (in_deriv != nullptr &&
+      (in_deriv_dim.rows != g.R || in_deriv_dim.cols != g.HW * in_channel ||
+       pad_h > kernel_height - 1 || pad_w > kernel_width - 1))
+    return (int)hipErrorInvalidValue;
+  if (g.M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  if (g.R > 0 &&
+      kcnn_conv_bwd_frame(g, in, in_dim.stride, out_deriv, out_deriv_dim.stride,
+                          kernel, kernel_dim.stride, in_deriv,
+                          in_deriv ? in_deriv_dim.stride : 0, grad_W,
+                          grad_W_dim.stride, grad_b, workspace, workspace_bytes,
+                          st) == 0)
+    return 0;
+  if (in_deriv != nullptr) {
+    const int rc = hipF_conv2d_dgrad(out_deriv, out_deriv_dim, in_height,
+                                     in_width, in_channel, pad_h, pad_w, kernel,
+                                     kernel_dim, kernel_height, kernel_width,
+                                     group, in_deriv, in_deriv_dim, workspace,
+                                     workspace_bytes, stream);
+    if (rc) return rc;
+  }
+  return hipF_conv2d_wgrad(in, in_dim, in_height, in_width, in_channel, pad_h,
+                           pad_w, out_deriv, out_deriv_dim, kernel_height,
+                           kernel_width, group, grad_W, grad_W_dim, grad_b,
+                           workspace, workspace_bytes, stream);
+}
+
 }  // extern "C"

@@ -53,6 +53,13 @@ int kcnn_conv_fwd_frame(const kcnn::ConvGeom &g, const float *X, int xs,
 int kcnn_conv_dgrad_frame(const kcnn::ConvGeom &g, const float *dY, int dys,
                           const float *K, int ks, float *dX, int dxs,
                           hipStream_t st);
+// Fused backward (one pass over dY): dX (nullable) and gW/gb.  ws must hold
+// kcnn_conv_bwd_frame_ws(g) bytes (0 = shape not eligible).
+size_t kcnn_conv_bwd_frame_ws(const kcnn::ConvGeom &g);
+int kcnn_conv_bwd_frame(const kcnn::ConvGeom &g, const float *X, int xs,
+                        const float *dY, int dys, const float *K, int ks,
+                        float *dX, int dxs, float *gW, int gws, float *gb,
+                        void *ws, size_t ws_bytes, hipStream_t st);
 size_t kcnn_conv_wgrad_frame_ws(const kcnn::ConvGeom &g);
 int kcnn_conv_wgrad_frame(const kcnn::ConvGeom &g, const float *X, int xs,
                           const float *dY, int dys, float *gW, int gws,

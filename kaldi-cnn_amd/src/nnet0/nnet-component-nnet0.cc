@@ -279,6 +279,15 @@ void ConvolutionComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
   ConvolutionComponent *to_update =
       dynamic_cast<ConvolutionComponent *>(to_update_in);
   KALDI_ASSERT(out_deriv.NumCols() == OutputDim());
+  if (!LiteralPath() && to_update != NULL && in_deriv != NULL) {
+    // dX (with the pre-update kernel, as the reference orders it) and the
+    // gradient from one pass over out_deriv, then the update step (:541).
+    Scratch grad(sizeof(BaseFloat) * (size_t)NumGradientParams());
+    BackpropGradient(ChunkInfo(), ChunkInfo(), in_value, in_value, out_deriv,
+                     in_deriv, grad.f());
+    to_update->ApplyGradient(grad.f(), in_value.NumRows());
+    return;
+  }
   if (in_deriv != NULL) {
     if (in_deriv->NumRows() != num_chunks || in_deriv->NumCols() != InputDim())
       in_deriv->Resize(num_chunks, InputDim(), kUndefined);
@@ -553,6 +562,47 @@ void ConvolutionComponent::ComputeGradient(const CuMatrixBase<BaseFloat> &in_val
       in_value.Data(), in_value.Dim(), in_height_, in_width_, in_channel_,
       in_pad_height_, in_pad_width_, out_deriv.Data(), out_deriv.Dim(),
       kernel_height_, kernel_width_, group_, grad, Dense(KernelDim(), group_),
+      grad + (size_t)KernelDim() * group_, ws, ws_bytes, S()));
+}
+
+// Data gradient (:461-540) and the gradient half of Update (:745-775) from
+// one streamed pass over out_deriv.
+void ConvolutionComponent::BackpropGradient(const ChunkInfo &in_info,
+                                            const ChunkInfo &out_info,
+                                            const CuMatrixBase<BaseFloat> &in_value,
+                                            const CuMatrixBase<BaseFloat> &out_value,
+                                            const CuMatrixBase<BaseFloat> &out_deriv,
+                                            CuMatrix<BaseFloat> *in_deriv,
+                                            BaseFloat *grad) const {
+  if (LiteralPath()) {
+    UpdatableComponent::BackpropGradient(in_info, out_info, in_value, out_value,
+                                         out_deriv, in_deriv, grad);
+    return;
+  }
+  const int32 num_chunks = out_deriv.NumRows();
+  KALDI_ASSERT(in_value.NumCols() == InputDim() &&
+               out_deriv.NumCols() == OutputDim() &&
+               in_value.NumRows() == num_chunks);
+  if (in_deriv != NULL) {
+    KALDI_ASSERT(kernel_height_ - 1 - in_pad_height_ >= 0 &&
+                 kernel_width_ - 1 - in_pad_width_ >= 0 &&
+                 "kernel must exceed the padding");                 // :533
+    if (in_deriv->NumRows() != num_chunks || in_deriv->NumCols() != InputDim())
+      in_deriv->Resize(num_chunks, InputDim(), kUndefined);
+  }
+  CuDevice &dev = CuDevice::Instantiate();
+  const size_t ws_bytes = hipF_conv2d_backward_workspace_bytes(
+      in_value.Dim(), in_height_, in_width_, in_channel_, in_pad_height_,
+      in_pad_width_, kernel_height_, kernel_width_, group_);
+  void *ws = ws_bytes ? dev.Workspace(ws_bytes) : nullptr;
+  CuProfileScope prof("ConvolutionComponent::BackpropGradient");
+  MatrixDim idd = in_value.Dim();
+  CNSL_SAFE_CALL(hipF_conv2d_backward(
+      in_value.Data(), in_value.Dim(), in_height_, in_width_, in_channel_,
+      in_pad_height_, in_pad_width_, out_deriv.Data(), out_deriv.Dim(),
+      linear_params_.Data(), linear_params_.Dim(), kernel_height_, kernel_width_,
+      group_, in_deriv ? in_deriv->Data() : nullptr,
+      in_deriv ? in_deriv->Dim() : idd, grad, Dense(KernelDim(), group_),
       grad + (size_t)KernelDim() * group_, ws, ws_bytes, S()));
 }
 

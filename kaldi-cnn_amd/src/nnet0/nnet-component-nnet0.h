@@ -111,6 +111,12 @@ class ConvolutionComponent : public nnet2::UpdatableComponent {
                                const CuMatrixBase<BaseFloat> &out_deriv,
                                BaseFloat *grad) const;
   virtual void ApplyGradient(const BaseFloat *grad, int32 num_sample);
+  // dX and the gradient from one pass over out_deriv (hipF_conv2d_backward).
+  virtual void BackpropGradient(const ChunkInfo &in_info, const ChunkInfo &out_info,
+                                const CuMatrixBase<BaseFloat> &in_value,
+                                const CuMatrixBase<BaseFloat> &out_value,
+                                const CuMatrixBase<BaseFloat> &out_deriv,
+                                CuMatrix<BaseFloat> *in_deriv, BaseFloat *grad) const;
 
   // Mutable parameter access for hosts (C-ABI).
   CuMatrix<BaseFloat> &LinearParamsMutable() { return linear_params_; }

@@ -137,6 +137,17 @@ class UpdatableComponent : public Component {
     (void)grad; (void)num_sample;
     KALDI_ERR << Type() << " does not support ApplyGradient";
   }
+  // Backprop without update (in_deriv nullable) + ComputeGradient in one
+  // call; components with a fused backward kernel override it.
+  virtual void BackpropGradient(const ChunkInfo &in_info, const ChunkInfo &out_info,
+                                const CuMatrixBase<BaseFloat> &in_value,
+                                const CuMatrixBase<BaseFloat> &out_value,
+                                const CuMatrixBase<BaseFloat> &out_deriv,
+                                CuMatrix<BaseFloat> *in_deriv, BaseFloat *grad) const {
+    if (in_deriv != NULL)
+      Backprop(in_info, out_info, in_value, out_value, out_deriv, NULL, in_deriv);
+    ComputeGradient(in_value, out_deriv, grad);
+  }
 
  protected:
   BaseFloat learning_rate_;

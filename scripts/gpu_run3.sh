@@ -1,0 +1,8 @@
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python -m pytest tests/test_gpu_components.py -m gpu -x -q -p no:cacheprovider -k "backprop_gradient or conv_component" > gpurun_out/pytest_bwd.log 2>&1 || { echo "pytest_bwd_rc=$?" >> gpurun_out/pytest_bwd.log; exit 3; }
+timeout -k 10 300 python scripts/microbench.py --reps 20 > gpurun_out/micro3.log 2>&1 || exit 4
+KCNN_FWD_VARIANT=0 timeout -k 10 200 python scripts/microbench.py --reps 20 --only fwd > gpurun_out/micro3_fwd0.log 2>&1 || exit 5
+timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; echo "pytest_rc=$?" >> gpurun_out/pytest_gpu.log
+echo done

@@ -56,6 +56,7 @@ def main():
         "fwd": (lambda: conv.Propagate(x, y), conv_b),
         "dgrad": (lambda: conv.Backprop(x, None, dy, dx, update=False), conv_b),
         "wgrad": (lambda: conv.ComputeGradient(x, dy, grad), conv_b),
+        "bwd_fused": (lambda: conv.BackpropGradient(x, dy, dx, grad), conv_b + x.numel() * 4),
         "pool_fwd": (lambda: pool.Propagate(y, p), bench.POOL_FWD_BYTES * B),
         "pool_bwd": (lambda: pool.Backprop(y, p, dp, dyp), bench.POOL_BWD_BYTES * B),
     }

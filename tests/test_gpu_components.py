@@ -97,6 +97,77 @@ def test_conv_component(kc, path, name):
     assert_bound(host(comp.BiasParams()), oc.b, np.abs(b0) + lr * gb_s, what=f"{name} b'")
 
 
+FUSED_BWD = {
+    # shapes in the fused single-pass backward's range (kh*kw*C <= 31,
+    # group in {32, 64, 96, 128}, 16 <= oh*ow <= 512) and at its edges
+    "c2_grid_stride": ((40, 11, 3, 8, 1, 128, 0, 0), 300),  # R > grid
+    "even_P": ((41, 11, 1, 8, 3, 64, 0, 0), 7),              # P = 306
+    "padded": ((12, 10, 2, 3, 3, 32, 1, 1), 5),              # P = 120, pad 1
+    "K31_G96": ((40, 5, 1, 31, 1, 96, 0, 0), 6),             # ones row = 31
+    "P512": ((35, 16, 1, 4, 1, 32, 0, 0), 3),                # max positions
+    "P16": ((5, 5, 2, 2, 2, 128, 0, 0), 4),                  # min positions
+    "oh1": ((8, 40, 1, 8, 3, 64, 0, 0), 5),                  # oh = 1
+}
+
+
+@pytest.mark.parametrize("name", list(FUSED_BWD))
+def test_conv_backprop_gradient(kc, name):
+    """BackpropGradient: dX and [gW | gb] from one pass over dY (fused
+    kernel) against the oracle's Backprop (:461-540) and Update gradient
+    (:738-765); also the gradient-only form and Backprop(update=True)."""
+    cfg, N = FUSED_BWD[name]
+    H, W, C, kh, kw, G, ph, pw = cfg
+    comp, oc = make_pair(kc, cfg, seed=7 + len(name))
+    r = rng(200 + len(name))
+    x = randn(r, (N, H * W * C))
+    f32, y_t, y_s = triple(lambda: oc.propagate(x))
+    assert_bound(host(comp.Propagate(dev(x))), y_t, y_s, what=f"{name} Propagate")
+    dy = randn(r, y_t.shape)
+    _, dx_t, dx_s = triple(lambda: oc.backprop(x, dy, update=False))
+    _, (gW_t, gb_t), (gW_s, gb_s) = triple(lambda: oc.gradient(x, dy))
+    kd = kh * kw * C
+    dx, g = comp.BackpropGradient(dev(x), dev(dy))
+    g = host(g)
+    assert_bound(host(dx), dx_t, dx_s, what=f"{name} dX")
+    assert_bound(g[:kd * G].reshape(kd, G), gW_t, gW_s, what=f"{name} gW")
+    assert_bound(g[kd * G:], gb_t, gb_s, what=f"{name} gb")
+    _, g2 = comp.BackpropGradient(dev(x), dev(dy), want_in_deriv=False)
+    assert_same(host(g2), g, what=f"{name} gradient-only == fused")  # deterministic
+    W0, b0, p0 = oc.W.copy(), oc.b.copy(), oc.prev.copy()
+    with O.accum(1):
+        oc.backprop(x, dy, update=True)
+    dx2 = comp.Backprop(dev(x), None, dev(dy), update=True)
+    assert_same(host(dx2), host(dx), what=f"{name} Backprop(update) dX")
+    lr = 0.02 / N
+    scale_W = np.abs(W0) + np.abs(p0) + lr * gW_s + 1e-30
+    assert_bound(host(comp.LinearParams()), oc.W, scale_W, what=f"{name} W'")
+    assert_bound(host(comp.BiasParams()), oc.b, np.abs(b0) + lr * gb_s, what=f"{name} b'")
+
+
+def test_conv_backprop_gradient_special_values(kc):
+    """Inf in the last map's tail must not leak into other columns: the
+    fused kernel reads row tails past oh*ow (masked to exact zeros)."""
+    cfg = (40, 11, 3, 8, 1, 128, 0, 0)
+    comp, oc = make_pair(kc, cfg, seed=11)
+    r = rng(11)
+    N = 3
+    x = randn(r, (N, 40 * 11 * 3))
+    dy = randn(r, (N, 363 * 128))
+    dy[1, 5 * 363 + 0] = np.inf      # start of map 5: adjacent to map 4's tail
+    dy[2, 127 * 363 + 362] = -np.inf  # very last element of the frame
+    with O.accum(1):
+        gW_t, gb_t = oc.gradient(x, dy)
+        dx_t = oc.backprop(x, dy, update=False)
+    dx, g = comp.BackpropGradient(dev(x), dev(dy))
+    g = host(g)
+    kd = 24
+    gW = g[:kd * 128].reshape(kd, 128)
+    # non-finite pattern identical to the reference's
+    np.testing.assert_array_equal(np.isfinite(gW), np.isfinite(gW_t))
+    np.testing.assert_array_equal(np.isfinite(g[kd * 128:]), np.isfinite(gb_t))
+    np.testing.assert_array_equal(np.isfinite(host(dx)), np.isfinite(dx_t))
+
+
 def test_conv_update_divides_by_local_rows(kc):
     # B10: Update divides the learning rate by in_value.NumRows() (:767).
     cfg = CONVS["tiny"]

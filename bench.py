@@ -34,6 +34,8 @@ PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 matrix (dense)
 # Algorithmic work per frame (SURVEY 8d / BASELINE.md 3).
 CONV_FLOP_PER_PASS = 2 * P * G * KH * KW * C          # 2,230,272
 CONV_BYTES_PER_PASS = 4 * (H * W * C + P * G)         # 191,136
+CONV_BWD_BYTES = 4 * (2 * H * W * C + P * G)          # 196,416: X, dY in; dX out
+CONV_BWD_FLOP = 2 * CONV_FLOP_PER_PASS + 2 * P * G    # dgrad + wgrad + bias grad
 POOL_FWD_BYTES = 4 * (P * G + POOL_OUT)               # 232,320
 POOL_BWD_BYTES = 4 * (2 * P * G + 2 * POOL_OUT)       # 464,640
 FC_FLOP = 3 * 2 * POOL_OUT * FC_OUT                   # 71,368,704
@@ -187,6 +189,7 @@ def main():
         return (ms / n) if n else None
 
     k_fwd = avg("ConvolutionComponent::Propagate")
+    k_bwd = avg("ConvolutionComponent::BackpropGradient")
     k_dgrad = avg("ConvolutionComponent::BackpropData")
     k_wgrad = avg("ConvolutionComponent::ComputeGradient")
     k_pool_f = avg("MaxpoolComponent::Propagate")
@@ -195,12 +198,18 @@ def main():
     kernels = {}
     for name, ms, flop, byts in (
             ("conv_fwd", k_fwd, CONV_FLOP_PER_PASS * B, CONV_BYTES_PER_PASS * B),
+            ("conv_bwd_fused", k_bwd, CONV_BWD_FLOP * B, CONV_BWD_BYTES * B),
             ("conv_dgrad", k_dgrad, CONV_FLOP_PER_PASS * B, CONV_BYTES_PER_PASS * B),
             ("conv_wgrad", k_wgrad, CONV_FLOP_PER_PASS * B, CONV_BYTES_PER_PASS * B),
             ("maxpool_fwd", k_pool_f, 0, POOL_FWD_BYTES * B),
             ("maxpool_bwd", k_pool_b, 0, POOL_BWD_BYTES * B)):
         if ms:
-            kernels[name] = {"ms": round(ms, 4),
+            # the roofline that bounds it: the larger of bytes/peak-BW and
+            # flops/peak-MFMA (algorithmic work)
+            t_hbm = byts / (PEAK_HBM_GBS * 1e6)
+            t_mfma = flop / (PEAK_FP32_MFMA_TFLOPS * 1e9) if flop else 0.0
+            kernels[name] = {"ms": round(ms, 4), "bytes": byts, "flop": flop,
+                             "bound": "mfma" if t_mfma > t_hbm else "hbm",
                              "GB/s": round(byts / ms / 1e6, 1),
                              "hbm_frac": round(byts / ms / 1e6 / PEAK_HBM_GBS, 4),
                              "TFLOP/s": round(flop / ms / 1e9, 2) if flop else None,
@@ -216,10 +225,6 @@ def main():
     roofline = None
     if dom:
         dk = kernels[dom]
-        conv_like = dom.startswith("conv")
-        byts = (CONV_BYTES_PER_PASS if conv_like else
-                POOL_FWD_BYTES if dom == "maxpool_fwd" else POOL_BWD_BYTES) * B
-        achieved = byts / dk["ms"] / 1e6
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
@@ -227,10 +232,16 @@ def main():
                 traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        roofline = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
-                    "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-                    "algorithmic_bytes_per_launch": byts}
+        if dk["bound"] == "mfma":
+            achieved, peak, unit = dk["flop"] / dk["ms"] / 1e9, PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"
+        else:
+            achieved, peak, unit = dk["bytes"] / dk["ms"] / 1e6, PEAK_HBM_GBS, "GB/s"
+        roofline = {"kernel": dom, "bound": dk["bound"], "achieved": round(achieved, 2),
+                    "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
+                    "traffic": traffic,
+                    "algorithmic_bytes_per_launch": dk["bytes"],
+                    "algorithmic_flop_per_launch": dk["flop"],
+                    "launch_ms": dk["ms"]}
 
     if rank == 0:
         result = {

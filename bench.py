@@ -114,6 +114,7 @@ def main():
 
     import torch
     import kcnn
+    import kcnn_dp
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -136,24 +137,15 @@ def main():
     x = torch.randn((B, H * W * C), generator=gen, device="cuda")
     dy = torch.randn((B, FC_OUT), generator=gen, device="cuda") * 1e-2
 
-    grads = {i: torch.empty(c.NumGradientParams(), device="cuda")
-             for i, c in enumerate(net.components) if c.NumGradientParams() > 0}
+    grads = kcnn_dp.gradient_buffers(
+        net, lambda n: torch.empty(n, device="cuda"))
 
     def step():
-        net.Propagate(x)
         if world == 1:
+            net.Propagate(x)
             net.Backprop(dy)                     # reference semantics: update in Backprop
             return
-        pending = []
-        for i in reversed(range(net.NumComponents())):
-            if i in grads:
-                net.BackpropComponent(i, dy, mode=1, grad=grads[i], skip_first_dx=False)
-                pending.append((i, dist.all_reduce(grads[i], async_op=True)))
-            else:
-                net.BackpropComponent(i, dy, mode=2, skip_first_dx=False)
-        for i, work in pending:
-            work.wait()
-            net.components[i].ApplyGradient(grads[i], B * world)
+        kcnn_dp.dp_train_step(net, x, dy, grads, dist, B * world)
 
     for _ in range(args.warmup):
         step()

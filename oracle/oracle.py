@@ -56,7 +56,9 @@ def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(_LIB_PATH):
-            raise RuntimeError(f"oracle not built: {_LIB_PATH} (run make -C oracle)")
+            # test infrastructure: build the checker on first use (gcc only)
+            import subprocess
+            subprocess.run(["make", "-s", "-C", os.path.dirname(_LIB_PATH)], check=True)
         _lib = ctypes.CDLL(_LIB_PATH)
         _lib.orc_last_error.restype = ctypes.c_char_p
     return _lib

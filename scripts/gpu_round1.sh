@@ -1,0 +1,13 @@
+# Round-1 validation + measurement on one MI355X (run via gpurun).
+set -o pipefail
+mkdir -p gpurun_out/r1
+export TMPDIR=/tmp
+O=gpurun_out/r1
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $O/pytest_gpu.log 2>&1; echo "pytest_rc=$?" >> $O/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit 3
+timeout -k 10 600 python bench.py --json-out $O/bench.json > $O/bench.log 2>&1 || exit 4
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof.log 2>&1 || exit 5
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$c -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_$c.log 2>&1 || exit 6
+done
+echo done

@@ -1,0 +1,105 @@
+"""Summarise a rocprofv3 bench profile into profiles/ (committed evidence).
+
+  python scripts/prof_summary.py gpurun_out/r1 profiles r01 --steps 25
+
+Reads <run>/prof/run_kernel_stats.csv (--kernel-trace --stats) and the
+<run>/pmc_FETCH_SIZE, <run>/pmc_WRITE_SIZE counter passes; writes
+  profiles/<tag>_kernel_stats.md   per-kernel calls / average / share
+  profiles/<tag>_kernel_stats.csv  the raw rocprofv3 stats table
+  profiles/pmc_traffic.json        HBM bytes per launch of the hot-path kernels
+                                   (FETCH_SIZE x2 on gfx950 + WRITE_SIZE, per
+                                   MI355X_MICROARCH.md's HBM section)
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+
+# hot-path kernel -> bench.py kernel-table key
+HOT = {
+    "conv_bwd_frame_kernel": "conv_bwd_fused",
+    "conv_fwd_slab_kernel": "conv_fwd",
+    "conv_fwd_frame_kernel": "conv_fwd",
+    "MaxpoolProp": "maxpool_fwd",
+    "MaxpoolBackprop": "maxpool_bwd",
+}
+
+
+def short(name):
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    m = re.match(r"([A-Za-z_][A-Za-z0-9_:]*(<[^()]*>)?)", name)
+    return (m.group(1) if m else name)[:80]
+
+
+def kernel_key(name):
+    for k, v in HOT.items():
+        if k in name:
+            return v
+    return None
+
+
+def pmc_means(d, counter):
+    """Mean per dispatch of `counter` for each kernel name (summed over dims)."""
+    per = collections.defaultdict(float)
+    n = collections.defaultdict(set)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if row["Counter_Name"] != counter:
+                continue
+            k = row["Kernel_Name"]
+            per[k] += float(row["Counter_Value"])
+            n[k].add(row["Dispatch_Id"])
+    return {k: per[k] / len(n[k]) for k in per}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("run")
+    ap.add_argument("out")
+    ap.add_argument("tag")
+    ap.add_argument("--steps", type=int, default=25, help="bench steps profiled (warmup+timed)")
+    a = ap.parse_args()
+    os.makedirs(a.out, exist_ok=True)
+    stats = os.path.join(a.run, "prof", "run_kernel_stats.csv")
+    rows = list(csv.DictReader(open(stats)))
+    shutil.copy(stats, os.path.join(a.out, f"{a.tag}_kernel_stats.csv"))
+    lines = [f"# {a.tag}: rocprofv3 --kernel-trace --stats, `python bench.py --steps 20 "
+             f"--warmup 5 --no-cpu-baseline` (c2, N=4096, 1x MI355X)", "",
+             "| kernel | calls | avg us | total ms | % |", "|---|---:|---:|---:|---:|"]
+    for r in rows:
+        lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} "
+                     f"| {float(r['TotalDurationNs']) / 1e6:.2f} | {float(r['Percentage']):.1f} |")
+    total_ms = sum(float(r["TotalDurationNs"]) for r in rows) / 1e6
+    lines += ["", f"GPU kernel time per step: {total_ms / a.steps:.3f} ms over {a.steps} steps."]
+    fetch = pmc_means(os.path.join(a.run, "pmc_FETCH_SIZE"), "FETCH_SIZE")
+    write = pmc_means(os.path.join(a.run, "pmc_WRITE_SIZE"), "WRITE_SIZE")
+    traffic = {}
+    lines += ["", "## HBM traffic per launch (PMC, separate passes)", "",
+              "FETCH_SIZE and WRITE_SIZE are in KB; on gfx950 FETCH_SIZE counts half the bytes "
+              "of 16-B/lane streaming reads, so read bytes = 2 x FETCH_SIZE x 1024.", "",
+              "| kernel | FETCH_SIZE (KB) | WRITE_SIZE (KB) | HBM bytes / launch |",
+              "|---|---:|---:|---:|"]
+    for k in sorted(set(fetch) | set(write)):
+        key = kernel_key(k)
+        if key is None:
+            continue
+        f_kb, w_kb = fetch.get(k, 0.0), write.get(k, 0.0)
+        byts = 2 * f_kb * 1024 + w_kb * 1024
+        traffic.setdefault(key, {"kernel": short(k), "hbm_bytes_per_launch": 0.0})
+        traffic[key]["hbm_bytes_per_launch"] += byts
+        lines.append(f"| `{short(k)}` | {f_kb:.0f} | {w_kb:.0f} | {byts:.3e} |")
+    with open(os.path.join(a.out, f"{a.tag}_kernel_stats.md"), "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    if traffic:
+        for v in traffic.values():
+            v["hbm_bytes_per_launch"] = round(v["hbm_bytes_per_launch"])
+        json.dump(traffic, open(os.path.join(a.out, "pmc_traffic.json"), "w"), indent=1)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()

@@ -205,6 +205,140 @@ __global__ __launch_bounds__(256) void conv_fwd_slab_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Forward with every MFMA operand in registers.  Per wave: the kernel
+// W[k][g] for all (up to 4) 32-filter groups is loaded once (KS*4 VGPRs); per
+// frame the im2col values of the wave's position tiles are gathered once
+// from the LDS-resident map (FT*KS VGPRs) and reused by every filter group,
+// so the MFMA chains run with no LDS traffic.  Each 32-filter output slab
+// (a contiguous 32 x P run of Y) is staged in LDS and streamed out with
+// 16-B stores; bias fused.  KS = k-steps (Kdim <= 2*KS, padded taps carry
+// zero weights), FT = position tiles per wave (P <= 4*32*FT).
+template <int KS, int FT>
+__global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs,
+    const float *__restrict__ K, int ks, const float *__restrict__ bias,
+    float *__restrict__ out, int os, int vec_ok, int dbg) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float *T = reinterpret_cast<float *>(smem);                 // [32][P]
+  float *Bs = T + ((32 * g.P + 3) & ~3);                      // [128] bias
+  int2 *koff = reinterpret_cast<int2 *>(Bs + 128);             // [2*KS] taps
+  float *Xs = reinterpret_cast<float *>(koff + 2 * KS);         // [C*HW]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l = lane & 31, h = lane >> 5;
+  const int NG = (g.G + 31) >> 5;  // <= 4 (host check)
+  if (tid < 128) Bs[tid] = (bias && tid < g.G) ? bias[tid] : 0.0f;
+  // A operand: W[k = 2s + h][gb*32 + l]
+  float wreg[4][KS];
+#pragma unroll
+  for (int gb = 0; gb < 4; gb++)
+#pragma unroll
+    for (int s = 0; s < KS; s++) {
+      const int k = 2 * s + h, gg = gb * 32 + l;
+      wreg[gb][s] = (k < g.Kdim && gg < g.G) ? K[(int64_t)k * ks + gg] : 0.0f;
+    }
+  // tap k -> (channel offset, kx << 16 | ky); padded taps never in bounds
+  if (tid < 2 * KS) {
+    int2 v = make_int2(0, 0x3fff << 16);
+    if (tid < g.Kdim) {
+      uint32_t c, r, qx, qy;
+      g.div_khkw.divmod((uint32_t)tid, c, r);
+      g.div_kh.divmod(r, qx, qy);
+      v = make_int2((int)c * g.HW, (int)((qx << 16) | qy));
+    }
+    koff[tid] = v;
+  }
+  const int CHW = g.C * g.HW;
+  const int ntile = (g.P + 31) >> 5;
+  long long tm[6] = {0, 0, 0, 0, 0, 0};
+  long long tprev = clock64();
+#define KCNN_TMARK(i) if (dbg & 16) { const long long tn = clock64(); tm[i] += tn - tprev; tprev = tn; }
+  // the next frame's map is prefetched into registers while this one runs
+  constexpr int XV = 8;  // CHW <= 2048 (host check)
+  float xv[XV];
+#pragma unroll
+  for (int i = 0; i < XV; i++)
+    if (blockIdx.x < (unsigned)g.R && tid + 256 * i < CHW)
+      xv[i] = X[(int64_t)blockIdx.x * xs + tid + 256 * i];
+  for (int n = blockIdx.x; n < g.R; n += gridDim.x) {
+    __syncthreads();  // previous frame's Xs / T reads done
+    KCNN_TMARK(5)
+#pragma unroll
+    for (int i = 0; i < XV; i++)
+      if (tid + 256 * i < CHW) Xs[tid + 256 * i] = xv[i];
+    if (n + (int)gridDim.x < g.R) {
+#pragma unroll
+      for (int i = 0; i < XV; i++)
+        if (tid + 256 * i < CHW)
+          xv[i] = X[(int64_t)(n + gridDim.x) * xs + tid + 256 * i];
+    }
+    __syncthreads();
+    KCNN_TMARK(0)
+    float bx[FT][KS];
+#pragma unroll
+    for (int t = 0; t < FT; t++) {
+      const int p = (wave + 4 * t) * 32 + l;
+      const bool pv = p < g.P;
+      uint32_t px = 0, py = 0;
+      g.div_oh.divmod((uint32_t)(pv ? p : 0), px, py);
+#pragma unroll
+      for (int s = 0; s < KS; s++) {
+        const int2 ko = koff[2 * s + h];
+        const int xx = (int)px + (ko.y >> 16) - g.pad_w;
+        const int yy = (int)py + (ko.y & 0xffff) - g.pad_h;
+        const bool ok = pv && (unsigned)xx < (unsigned)g.W && (unsigned)yy < (unsigned)g.H;
+        const float v = Xs[ok ? ko.x + xx * g.H + yy : 0];
+        bx[t][s] = ok ? v : 0.0f;
+      }
+    }
+    KCNN_TMARK(1)
+#pragma unroll
+    for (int gb = 0; gb < 4; gb++) {
+      if (gb >= NG) break;
+      float bsv[16];  // this lane's 16 accumulator rows' bias, read ahead
+#pragma unroll
+      for (int r = 0; r < 16; r++) bsv[r] = Bs[gb * 32 + mfma32_row(r, lane)];
+#pragma unroll
+      for (int t = 0; t < FT; t++) {
+        const int pt = wave + 4 * t;
+        if (pt >= ntile) continue;  // wave-uniform
+        floatx16 acc = zero16();
+#pragma unroll
+        for (int s = 0; s < KS; s++)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wreg[gb][s], bx[t][s], acc, 0, 0, 0);
+        const int p = pt * 32 + l;
+        if (p < g.P) {
+#pragma unroll
+          for (int r = 0; r < 16; r++)
+            T[mfma32_row(r, lane) * g.P + p] = acc[r] + bsv[r];
+        }
+      }
+      KCNN_TMARK(2)
+      __syncthreads();
+      KCNN_TMARK(3)
+      const int rows = g.G - gb * 32 < 32 ? g.G - gb * 32 : 32;
+      const int cnt = rows * g.P;
+      float *dst = out + (int64_t)n * os + (int64_t)gb * 32 * g.P;
+      if (vec_ok) {
+        const float4 *src4 = reinterpret_cast<const float4 *>(T);
+        float4 *dst4 = reinterpret_cast<float4 *>(dst);
+        for (int e = tid; e < (cnt >> 2); e += 256) dst4[e] = src4[e];
+        for (int e = (cnt & ~3) + tid; e < cnt; e += 256) dst[e] = T[e];
+      } else {
+        for (int e = tid; e < cnt; e += 256) dst[e] = T[e];
+      }
+      KCNN_TMARK(4)
+      __syncthreads();
+      KCNN_TMARK(5)
+    }
+  }
+  if ((dbg & 16) && blockIdx.x == 0 && lane == 0)
+    printf("fwd wave %d: xload %lld gather %lld mfma %lld bar1 %lld store %lld bar2 %lld\n",
+           wave, tm[0], tm[1], tm[2], tm[3], tm[4], tm[5]);
+#undef KCNN_TMARK
+}
+
+// ---------------------------------------------------------------------------
 // Fused backward: data AND weight gradient from a single pass over dY.
 // dY of one frame is streamed in 32-map slabs (32 x P floats, contiguous and
 // 16-B aligned in HBM): linear dwordx4 loads, prefetched into registers one
@@ -651,8 +785,28 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
                         int os, hipStream_t st) {
   if (g.Kdim > 64 || g.P < 16) return -1;
   const int Kpad = (g.Kdim + 1) & ~1;
-  static const int variant = env_int("KCNN_FWD_VARIANT", 1);
-  if (variant == 1) {
+  static const int variant = env_int("KCNN_FWD_VARIANT", 2);
+  if (variant == 2 && g.Kdim <= 32 && g.G <= 128 && g.P <= 4 * 32 * 3 &&
+      g.C * g.HW <= 256 * 8) {
+    const size_t lds = (size_t)((32 * g.P + 3) & ~3) * 4 + 128 * 4 + 32 * 8 +
+                       (size_t)g.C * g.HW * 4;
+    if (lds <= (size_t)kFrameLdsMax) {
+      const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0);
+      const int ksn = (g.Kdim + 1) / 2;
+      const unsigned grid = frame_grid(g, 2);
+#define KCNN_FWD_REGS(KS_)                                                         \
+  hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3>), dim3(grid), dim3(256), lds, st, \
+                     g, X, xs, K, ks, bias, out, os, vec_ok, dbg)
+      static const int dbg = env_int("KCNN_FWD_DEBUG", 0);
+      if (ksn <= 4) KCNN_FWD_REGS(4);
+      else if (ksn <= 8) KCNN_FWD_REGS(8);
+      else if (ksn <= 12) KCNN_FWD_REGS(12);
+      else KCNN_FWD_REGS(16);
+#undef KCNN_FWD_REGS
+      return (int)hipGetLastError();
+    }
+  }
+  if (variant >= 1) {
     // slab-streamed: T [32][P] staged in LDS, written as whole 16-B lines
     const int Gp = (g.G + 31) & ~31;
     const size_t lds = (size_t)align16(Kpad * 8) + (size_t)((32 * g.P + 3) & ~3) * 4 +

@@ -296,6 +296,127 @@ struct BiasUpdate {
   __device__ void operator()(int64_t, int j) const { b[j] = a_g * gb[j] + b[j]; }
 };
 
+// ---------------------------------------------------------------------------
+// Channel-group pooling (non-overlap, ph = pw = 1: the c2 1x1x4 intermap pool).
+// The pc maps of one pool group are a contiguous run of a row (pc*plane
+// floats) and so is the group's output (plane floats), so a workgroup moves
+// whole groups with 16-B loads/stores; the cross-map max / routing goes
+// through LDS.  Same window order and comparison as MaxpoolProp (A.8/A.9).
+constexpr int kPoolGroups = 4;  // groups per workgroup iteration
+
+struct PoolGroups {
+  int64_t total;     // rows * groups per row
+  FastDiv div_gpr;   // groups per row
+  FastDiv div_gs4;   // pc*plane/4 (float4 per group)
+  FastDiv div_plane;
+  int plane, pc;
+};
+
+__device__ __forceinline__ int64_t group_off(const PoolGroups &pg, int64_t G,
+                                             int64_t stride, int64_t size) {
+  uint32_t row, gi;
+  pg.div_gpr.divmod((uint32_t)G, row, gi);
+  return (int64_t)row * stride + (int64_t)gi * size;
+}
+
+__global__ __launch_bounds__(256) void maxpool_group_prop_kernel(
+    const float *__restrict__ src, int64_t ss, float *__restrict__ dst,
+    int64_t ds, PoolGroups pg) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];  // [kPoolGroups][pc*plane]
+  const int gs = pg.pc * pg.plane, gs4 = gs >> 2;
+  for (int64_t gb = (int64_t)blockIdx.x * kPoolGroups; gb < pg.total;
+       gb += (int64_t)gridDim.x * kPoolGroups) {
+    const int ng = pg.total - gb < kPoolGroups ? (int)(pg.total - gb) : kPoolGroups;
+    for (int e = threadIdx.x; e < ng * gs4; e += 256) {
+      uint32_t k, f;
+      pg.div_gs4.divmod((uint32_t)e, k, f);
+      const float4 *g4 = reinterpret_cast<const float4 *>(
+          src + group_off(pg, gb + k, ss, gs));
+      reinterpret_cast<float4 *>(sm)[e] = g4[f];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < ng * pg.plane; e += 256) {
+      uint32_t k, q;
+      pg.div_plane.divmod((uint32_t)e, k, q);
+      const float *m = sm + k * gs + q;
+      float val = -1e20f;
+      for (int c = 0; c < pg.pc; c++) {
+        const float v = m[c * pg.plane];
+        if (val < v) val = v;
+      }
+      dst[group_off(pg, gb + k, ds, pg.plane) + q] = val;
+    }
+    __syncthreads();
+  }
+}
+
+// Writes every element of the group (routed derivative or 0): the fused
+// in_deriv->Resize(kSetZero) of MaxpoolComponent::Backprop (:889).
+__global__ __launch_bounds__(256) void maxpool_group_backprop_kernel(
+    const float *__restrict__ x, int64_t xs, const float *__restrict__ y,
+    int64_t ys, const float *__restrict__ dy, int64_t dys,
+    float *__restrict__ dx, int64_t dxs, PoolGroups pg) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];  // [2][kPoolGroups][plane]
+  float *sy = sm, *sd = sm + kPoolGroups * pg.plane;
+  const int gs = pg.pc * pg.plane, gs4 = gs >> 2;
+  for (int64_t gb = (int64_t)blockIdx.x * kPoolGroups; gb < pg.total;
+       gb += (int64_t)gridDim.x * kPoolGroups) {
+    const int ng = pg.total - gb < kPoolGroups ? (int)(pg.total - gb) : kPoolGroups;
+    for (int e = threadIdx.x; e < ng * pg.plane; e += 256) {
+      uint32_t k, q;
+      pg.div_plane.divmod((uint32_t)e, k, q);
+      sy[e] = y[group_off(pg, gb + k, ys, pg.plane) + q];
+      sd[e] = dy[group_off(pg, gb + k, dys, pg.plane) + q];  // own stride (B14)
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < ng * gs4; e += 256) {
+      uint32_t k, f;
+      pg.div_gs4.divmod((uint32_t)e, k, f);
+      const int64_t gx = group_off(pg, gb + k, xs, gs);
+      const int64_t gd = group_off(pg, gb + k, dxs, gs);
+      const float4 v = reinterpret_cast<const float4 *>(x + gx)[f];
+      uint32_t c, q;
+      pg.div_plane.divmod(4 * f, c, q);
+      const float *yk = sy + k * pg.plane, *dk = sd + k * pg.plane;
+      float o[4];
+      const float in[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        o[t] = in[t] == yk[q] ? dk[q] : 0.0f;
+        if (++q == (uint32_t)pg.plane) q = 0;
+      }
+      reinterpret_cast<float4 *>(dx + gd)[f] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+    __syncthreads();
+  }
+}
+
+// The group kernels apply when the pool is channel-only and every group of
+// every row starts 16-B aligned.
+bool pool_groups_ok(const void *a, int64_t stride, int plane, int pc, int ph,
+                    int pw, int mode) {
+  return mode == 0 && ph == 1 && pw == 1 && ((plane * pc) & 3) == 0 &&
+         (stride & 3) == 0 && ((uintptr_t)a & 15) == 0 &&
+         (size_t)kPoolGroups * plane * pc * 4 <= 64 * 1024;
+}
+
+PoolGroups make_pool_groups(int64_t rows, int cols_out, int plane, int pc) {
+  PoolGroups pg;
+  const int gpr = cols_out / plane;
+  pg.total = rows * gpr;
+  pg.div_gpr = FastDiv((uint32_t)gpr);
+  pg.div_gs4 = FastDiv((uint32_t)(plane * pc / 4));
+  pg.div_plane = FastDiv((uint32_t)plane);
+  pg.plane = plane;
+  pg.pc = pc;
+  return pg;
+}
+
+unsigned pool_grid(int64_t total) {
+  int64_t b = (total + kPoolGroups - 1) / kPoolGroups;
+  return (unsigned)(b < 2048 ? (b > 0 ? b : 1) : 2048);
+}
+
 PoolGeom make_pool_geom(int in_h, int in_w, int ph, int pw, int pc, int mode,
                         int out_cols) {
   PoolGeom g;
@@ -410,6 +531,20 @@ int hipF_maxpool_prop(const float *src, MatrixDim src_dim, float *pool,
                       int pool_height_dim, int pool_width_dim,
                       int pool_channel_dim, int mode, kcnn_stream_t stream) {
   if (mode != 0) pool_height_dim = pool_width_dim = 1;  // cnsl-cu-kernels.cu:316
+  const int plane = in_height * in_width;
+  if (pool_groups_ok(src, src_dim.stride, plane, pool_channel_dim,
+                     pool_height_dim, pool_width_dim, mode) &&
+      (int64_t)pool_dim.rows * (pool_dim.cols / plane) < ((int64_t)1 << 31) &&
+      pool_dim.cols % plane == 0 && src_dim.cols == pool_dim.cols * pool_channel_dim) {
+    PoolGroups pg = make_pool_groups(pool_dim.rows, pool_dim.cols, plane,
+                                     pool_channel_dim);
+    if (pg.total == 0) return 0;
+    hipLaunchKernelGGL(maxpool_group_prop_kernel, dim3(pool_grid(pg.total)),
+                       dim3(256), (size_t)kPoolGroups * plane * pool_channel_dim * 4,
+                       kcnn::as_stream(stream), src, (int64_t)src_dim.stride, pool,
+                       (int64_t)pool_dim.stride, pg);
+    return kcnn::launch_status();
+  }
   PoolGeom g = make_pool_geom(in_height, in_width, pool_height_dim,
                               pool_width_dim, pool_channel_dim, mode,
                               pool_dim.cols);
@@ -425,6 +560,25 @@ int hipF_maxpool_backprop(const float *in_val, MatrixDim in_val_dim,
                           int pool_width_dim, int pool_channel_dim, int mode,
                           int write_all, kcnn_stream_t stream) {
   hipStream_t st = kcnn::as_stream(stream);
+  const int plane0 = in_height * in_width;
+  if (write_all &&
+      pool_groups_ok(in_val, in_val_dim.stride, plane0, pool_channel_dim,
+                     pool_height_dim, pool_width_dim, mode) &&
+      pool_groups_ok(dest, dest_dim.stride, plane0, pool_channel_dim,
+                     pool_height_dim, pool_width_dim, mode) &&
+      out_val_dim.cols % plane0 == 0 &&
+      in_val_dim.cols == out_val_dim.cols * pool_channel_dim &&
+      (int64_t)out_val_dim.rows * (out_val_dim.cols / plane0) < ((int64_t)1 << 31)) {
+    PoolGroups pg = make_pool_groups(out_val_dim.rows, out_val_dim.cols, plane0,
+                                     pool_channel_dim);
+    if (pg.total == 0) return 0;
+    hipLaunchKernelGGL(maxpool_group_backprop_kernel, dim3(pool_grid(pg.total)),
+                       dim3(256), (size_t)2 * kPoolGroups * plane0 * 4, st, in_val,
+                       (int64_t)in_val_dim.stride, out_val, (int64_t)out_val_dim.stride,
+                       out_deriv, (int64_t)out_deriv_dim.stride, dest,
+                       (int64_t)dest_dim.stride, pg);
+    return kcnn::launch_status();
+  }
   if (mode == 0) {
     PoolGeom g = make_pool_geom(in_height, in_width, pool_height_dim,
                                 pool_width_dim, pool_channel_dim, 0,

@@ -31,6 +31,7 @@ using namespace kcnn;
 namespace {
 
 constexpr int kFrameLdsMax = 96 * 1024;
+constexpr int kBwdLdsMax = 160 * 1024;  // the fused backward: one workgroup per CU
 constexpr int ZS = 33;  // padded row stride (floats) of the LDS Z / dY tiles
 
 __host__ __device__ inline int align16(int bytes) { return (bytes + 15) & ~15; }
@@ -572,256 +573,6 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_frame_kernel(
 #undef KCNN_SLAB_REGS
 
 // ---------------------------------------------------------------------------
-// Fused backward, variant 2: the dY slab is prefetched straight into the
-// MFMA operand layout of the owning wave (dY[g = 2s+h][p = tile + l]: two
-// 128-B row segments per load).  The data gradient consumes those registers
-// directly (no LDS read for its A operand) while the slab is written to LDS
-// for the weight gradient, which needs dY transposed (g on the lanes); the
-// next slab's loads go into the same registers as soon as the data gradient
-// has consumed them, and land during the weight-gradient MFMAs.
-template <int NCH, bool DX>
-__global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_reg_kernel(
-    ConvGeom g, const float *__restrict__ X, int xs,
-    const float *__restrict__ dY, int dys, const float *__restrict__ K, int ks,
-    float *__restrict__ dX, int dxs, float *__restrict__ ws_part, int ZZ,
-    int SP, unsigned long long wg0, unsigned long long wg1, int dbg) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float *Wt = reinterpret_cast<float *>(smem);         // [NCH*32][32]
-  float *Sd = Wt + NCH * 32 * 32;                      // [32][SP]
-  float *Xs = Sd + bwd_sd_floats(SP) + 32;             // [C][Wp][Hp] + {1}
-  int *qtab = reinterpret_cast<int *>(Xs + ((g.C * (g.H + 2 * g.pad_h) *
-                                              (g.W + 2 * g.pad_w) + 4) & ~3));
-  float *Zs = Sd;                                       // [P][ZZ] after the slabs
-  // wgrad A operands (im2col values) of the frame: [tile][s][lane]
-  float *ainL = reinterpret_cast<float *>(qtab + ((g.P + 31) & ~31));
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l = lane & 31, h = lane >> 5;
-  for (int e = tid; e < NCH * 32 * 32; e += BWD_THREADS) {
-    const int gg = e >> 5, k = e & 31;
-    Wt[e] = (gg < g.G && k < g.Kdim) ? K[(int64_t)k * ks + gg] : 0.0f;
-  }
-  const int Hp = g.H + 2 * g.pad_h, Wp = g.W + 2 * g.pad_w;
-  const int CHWp = g.C * Hp * Wp;
-  int abase = CHWp * 4, qmul = 0;
-  if (l < g.Kdim) {
-    uint32_t c, r, qx, qy;
-    g.div_khkw.divmod((uint32_t)l, c, r);
-    g.div_kh.divmod(r, qx, qy);
-    abase = ((int)c * Hp * Wp + (int)qx * Hp + (int)qy) * 4;
-    qmul = 1;
-  }
-  for (int e = tid; e < CHWp; e += BWD_THREADS) Xs[e] = 0.0f;  // padded border
-  if (tid == 0) Xs[CHWp] = 1.0f;
-  for (int p = tid; p < ((g.P + 31) & ~31); p += BWD_THREADS) {
-    uint32_t px, py;
-    g.div_oh.divmod((uint32_t)p, px, py);
-    qtab[p] = p < g.P ? ((int)px * Hp + (int)py) * 4 : 0x3fffffff;
-  }
-  const uint32_t amax = (uint32_t)CHWp * 4;
-  const char *Xb = reinterpret_cast<const char *>(Xs);
-  const bool unpadded = g.pad_h == 0 && g.pad_w == 0;
-  const int CHW = g.C * g.HW;
-  const int ntile = (g.P + 31) >> 5;
-  // this lane's dY column in each owned tile (clamped: lanes past P load a
-  // valid address; their values are never committed or kept)
-  int pcol[BWD_MAXT];
-  bool tval[BWD_MAXT];
-#pragma unroll
-  for (int t = 0; t < BWD_MAXT; t++) {
-    const int pt = wave + BWD_WAVES * t;
-    tval[t] = pt < ntile;
-    const int p = pt * 32 + l;
-    pcol[t] = p < g.P ? p : g.P - 1;
-  }
-
-  floatx16 wacc[NCH];
-#pragma unroll
-  for (int c = 0; c < NCH; c++) wacc[c] = zero16();
-  float pre[1][BWD_MAXT][16];
-  float xv[BWD_MAXX];
-#define KCNN_PREFETCH(buf, nn, cc)                                                   \
-  do {                                                                               \
-    const float *src_ = dY + (int64_t)(nn) * dys + (int64_t)(cc) * 32 * g.P + h * g.P; \
-    _Pragma("unroll") for (int t = 0; t < BWD_MAXT; t++) {                           \
-      if (!tval[t]) continue;                                                        \
-      _Pragma("unroll") for (int s = 0; s < 16; s++)                                 \
-        pre[buf][t][s] = src_[(int64_t)(2 * s) * g.P + pcol[t]];                     \
-    }                                                                                \
-  } while (0)
-#define KCNN_XLOAD(nn)                                                               \
-  _Pragma("unroll") for (int i = 0; i < BWD_MAXX; i++)                              \
-    if (tid + BWD_THREADS * i < CHW) xv[i] = X[(int64_t)(nn) * xs + tid + BWD_THREADS * i];
-  if (blockIdx.x < (unsigned)g.R) {
-    KCNN_PREFETCH(0, blockIdx.x, 0);
-    KCNN_XLOAD(blockIdx.x)
-  }
-  long long tm[7] = {0, 0, 0, 0, 0, 0, 0};
-  long long tprev = clock64();
-#define KCNN_TMARK(i) if (dbg & 16) { const long long tn = clock64(); tm[i] += tn - tprev; tprev = tn; }
-  for (int n = blockIdx.x; n < g.R; n += gridDim.x) {
-    __syncthreads();  // previous frame's Zs / Xs reads are done
-    KCNN_TMARK(6)
-#pragma unroll
-    for (int i = 0; i < BWD_MAXX; i++) {
-      const int e = tid + BWD_THREADS * i;
-      if (e < CHW) {
-        int slot = e;
-        if (!unpadded) {
-          uint32_t c, q, wi, hi;
-          g.div_HW.divmod((uint32_t)e, c, q);
-          g.div_H.divmod(q, wi, hi);
-          slot = (int)c * Hp * Wp + ((int)wi + g.pad_w) * Hp + (int)hi + g.pad_h;
-        }
-        Xs[slot] = xv[i];
-      }
-    }
-    floatx16 zacc[BWD_MAXT];
-#pragma unroll
-    for (int t = 0; t < BWD_MAXT; t++) zacc[t] = zero16();
-#pragma unroll
-    for (int ch = 0; ch < NCH; ch++) {
-      const int cur = 0;
-      KCNN_TMARK(6)
-      // commit the slab (each owned tile's 32 x 32 block) for the wgrad
-#pragma unroll
-      for (int t = 0; t < BWD_MAXT; t++) {
-        if (!tval[t]) continue;
-        const int p = (wave + BWD_WAVES * t) * 32 + l;
-        if (p < g.P) {
-#pragma unroll
-          for (int s = 0; s < 16; s++) Sd[(2 * s + h) * SP + p] = pre[cur][t][s];
-        }
-      }
-      KCNN_TMARK(0)
-      const float *wrow = Wt + (ch * 32 + h) * 32 + l;
-      if (DX) {  // dgrad from registers: Z[p][k] += dY[g][p] W[k][g]
-#pragma unroll
-        for (int t = 0; t < BWD_MAXT; t++) {
-          if (!tval[t]) continue;
-#pragma unroll
-          for (int s = 0; s < 16; s++)
-            zacc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(pre[cur][t][s], wrow[2 * s * 32],
-                                                           zacc[t], 0, 0, 0);
-        }
-      }
-      KCNN_TMARK(1)
-      {  // the next slab into the registers the dgrad just released
-        const int nn = ch + 1 < NCH ? n : n + (int)gridDim.x;
-        const int cc = ch + 1 < NCH ? ch + 1 : 0;
-        if (nn < g.R) {
-          KCNN_PREFETCH(cur, nn, cc);
-          if (ch + 1 == NCH) { KCNN_XLOAD(nn) }
-        }
-      }
-      KCNN_TMARK(2)
-      __syncthreads();  // slab complete in LDS (and, at ch 0, the frame map)
-      KCNN_TMARK(3)
-      // weight gradient: tiles handed out by the host so that every wave
-      // runs three 16-MFMA chunks per slab (dgrad + wgrad), two per phase at
-      // most (wg: 8 bits per wave, 0xff = none)
-#pragma unroll
-      for (int j = 0; j < 2; j++) {
-        const int pt = (int)(((j ? wg1 : wg0) >> (8 * wave)) & 0xff);
-        if (pt == 0xff) continue;
-        int pb = pt * 32;
-        asm volatile("" : "+s"(pb));
-        const int ph = pb + h;
-        float *ainw = ainL + pt * 16 * 64 + lane;
-        float ain[16];
-        if (ch == 0) {  // gathered once per frame by the wave that uses it
-          const int *qrow = qtab + ph;
-#pragma unroll
-          for (int s = 0; s < 16; s++) {
-            const uint32_t off = min((uint32_t)(abase + qmul * qrow[2 * s]), amax);
-            ain[s] = *reinterpret_cast<const float *>(Xb + off);
-            ainw[s * 64] = ain[s];
-          }
-        } else {
-#pragma unroll
-          for (int s = 0; s < 16; s++) ain[s] = ainw[s * 64];
-        }
-        const float *scol = Sd + l * SP + ph;
-        if (pb + 32 <= g.P) {  // wave-uniform: a full tile
-#pragma unroll
-          for (int s = 0; s < 16; s++)
-            wacc[ch] = __builtin_amdgcn_mfma_f32_32x32x2f32(ain[s], scol[2 * s],
-                                                           wacc[ch], 0, 0, 0);
-        } else {
-#pragma unroll
-          for (int s = 0; s < 16; s++) {
-            const bool pin = ph + 2 * s < g.P;
-            const float bv = __uint_as_float(__float_as_uint(scol[2 * s]) &
-                                             (pin ? 0xffffffffu : 0u));
-            wacc[ch] = __builtin_amdgcn_mfma_f32_32x32x2f32(ain[s], bv, wacc[ch], 0, 0, 0);
-          }
-        }
-      }
-      KCNN_TMARK(4)
-      __syncthreads();  // slab consumed
-      KCNN_TMARK(5)
-    }
-    if (DX) {
-#pragma unroll
-      for (int t = 0; t < BWD_MAXT; t++) {
-        if (!tval[t]) continue;
-        const int pt = wave + BWD_WAVES * t;
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-          const int pl = pt * 32 + mfma32_row(r, lane);
-          if (pl < g.P && l < g.Kdim) Zs[pl * ZZ + l] = zacc[t][r];
-        }
-      }
-      __syncthreads();
-      float *dxr = dX + (int64_t)n * dxs;
-      const int khkw = g.kh * g.kw;
-      for (int e = tid; e < CHW; e += BWD_THREADS) {
-        uint32_t c, q, wi, hi;
-        g.div_HW.divmod((uint32_t)e, c, q);
-        g.div_H.divmod(q, wi, hi);
-        float sum = 0.0f;
-        for (int kxx = 0; kxx < g.kw; kxx++) {
-          const int px = (int)wi + g.pad_w - kxx;
-          if ((unsigned)px >= (unsigned)g.ow) continue;
-          const float *zr = Zs + (int64_t)(px * g.oh) * ZZ + (int)c * khkw + kxx * g.kh;
-          for (int kyy = 0; kyy < g.kh; kyy++) {
-            const int py = (int)hi + g.pad_h - kyy;
-            if ((unsigned)py < (unsigned)g.oh) sum += zr[py * ZZ + kyy];
-          }
-        }
-        dxr[e] = sum;
-      }
-    }
-  }
-  KCNN_TMARK(6)
-  if ((dbg & 16) && blockIdx.x == 0 && lane == 0)
-    printf("bwd2 wave %d: commit %lld dgrad %lld prefetch %lld bar1 %lld wgrad %lld bar2 %lld other %lld\n",
-           wave, tm[0], tm[1], tm[2], tm[3], tm[4], tm[5], tm[6]);
-#undef KCNN_TMARK
-#undef KCNN_PREFETCH
-#undef KCNN_XLOAD
-  const int E = (g.Kdim + 1) * g.G;
-  float *dst = ws_part + (int64_t)blockIdx.x * E;
-  float *red = Sd;  // [BWD_WAVES][32 * 32]
-#pragma unroll
-  for (int ch = 0; ch < NCH; ch++) {
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 16; r++)
-      red[wave * 1024 + mfma32_row(r, lane) * 32 + l] = wacc[ch][r];
-    __syncthreads();
-    for (int e = tid; e < 1024; e += BWD_THREADS) {
-      const int i = e >> 5, j = e & 31;
-      if (i > g.Kdim) continue;
-      float sum = 0.0f;
-#pragma unroll
-      for (int w = 0; w < BWD_WAVES; w++) sum += red[w * 1024 + e];
-      dst[i * g.G + ch * 32 + j] = sum;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Fused backward, variant 3: dY slabs reach LDS by LDS-DMA
 // (global_load_lds_dwordx4, 1 KiB per wave-instruction, no VGPRs), double
 // buffered, one slab ahead; one barrier per slab.  From the slab in LDS the
@@ -836,28 +587,35 @@ typedef __attribute__((address_space(1))) void glob_void_t;
 __host__ __device__ inline int bwd_dma_buf_floats(int P) {
   return ((32 * P * 4 + 1023) & ~1023) / 4;  // whole 1-KiB DMA chunks
 }
+// both slab buffers; also holds Z [P][Kdim|1] (< 32 P) and the final
+// [8 waves][32 x 32] reduction
+__host__ __device__ inline int bwd_dma_sd_floats(int P) {
+  const int two = 2 * bwd_dma_buf_floats(P);
+  return two > BWD_WAVES * 1024 ? two : BWD_WAVES * 1024;
+}
 
-template <int NCH, bool DX>
+template <int NCH, bool DX, bool WG>
 __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
     ConvGeom g, const float *__restrict__ X, int xs,
     const float *__restrict__ dY, int dys, const float *__restrict__ K, int ks,
     float *__restrict__ dX, int dxs, float *__restrict__ ws_part, int ZZ,
-    unsigned long long wg0, unsigned long long wg1) {
+    unsigned long long wg0, unsigned long long wg1, int dbg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int P = g.P;
   const int BUF = bwd_dma_buf_floats(P);
   float *Wt = reinterpret_cast<float *>(smem);         // [NCH*32][32]
   float *Sd0 = Wt + NCH * 32 * 32;                     // [32][P] x 2 buffers
-  float *Xs = Sd0 + 2 * BUF;                           // [C][Wp][Hp] + {1}
+  float *Xs = Sd0 + bwd_dma_sd_floats(P);              // [C][Wp][Hp] + {1}
   int *qtab = reinterpret_cast<int *>(Xs + ((g.C * (g.H + 2 * g.pad_h) *
                                               (g.W + 2 * g.pad_w) + 4) & ~3));
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = lane & 31, h = lane >> 5;
-  for (int e = tid; e < NCH * 32 * 32; e += BWD_THREADS) {
-    const int gg = e >> 5, k = e & 31;
-    Wt[e] = (gg < g.G && k < g.Kdim) ? K[(int64_t)k * ks + gg] : 0.0f;
-  }
+  if (DX)  // K and X are only read by the pass that needs them
+    for (int e = tid; e < NCH * 32 * 32; e += BWD_THREADS) {
+      const int gg = e >> 5, k = e & 31;
+      Wt[e] = (gg < g.G && k < g.Kdim) ? K[(int64_t)k * ks + gg] : 0.0f;
+    }
   const int Hp = g.H + 2 * g.pad_h, Wp = g.W + 2 * g.pad_w;
   const int CHWp = g.C * Hp * Wp;
   int abase = CHWp * 4, qmul = 0;
@@ -887,7 +645,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
   // lanes past the slab re-read its last float4 (kept inside the matrix;
   // the LDS tail they fill is never read)
   auto dma_slab = [&](int n, int c, int b) {
-    const float *src = dY + (int64_t)n * dys + (int64_t)c * slab;
+    const float *src = dY + (int64_t)((dbg & 2) ? 0 : n) * dys + (int64_t)c * slab;
     float *dst = Sd0 + b * BUF;
     for (int q = wave; q < nchunk; q += BWD_WAVES) {
       int off = q * 256 + lane * 4;
@@ -903,8 +661,12 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
   float xv[BWD_MAXX];
 #define KCNN_XLOAD(nn)                                                               \
   _Pragma("unroll") for (int i = 0; i < BWD_MAXX; i++)                              \
-    if (tid + BWD_THREADS * i < CHW) xv[i] = X[(int64_t)(nn) * xs + tid + BWD_THREADS * i];
+    if (WG && tid + BWD_THREADS * i < CHW)                                         \
+      xv[i] = X[(int64_t)(nn) * xs + tid + BWD_THREADS * i];
   int cur = 0;
+  long long tm[7] = {0, 0, 0, 0, 0, 0, 0};
+  long long tprev = clock64();
+#define KCNN_TMARK(i) if (dbg & 16) { const long long tn = clock64(); tm[i] += tn - tprev; tprev = tn; }
   if (blockIdx.x < (unsigned)g.R) {
     dma_slab(blockIdx.x, 0, 0);
     KCNN_XLOAD(blockIdx.x)
@@ -914,7 +676,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
 #pragma unroll
     for (int i = 0; i < BWD_MAXX; i++) {
       const int e = tid + BWD_THREADS * i;
-      if (e < CHW) {
+      if (WG && e < CHW) {
         int slot = e;
         if (!unpadded) {
           uint32_t c, q, wi, hi;
@@ -932,7 +694,9 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
 #pragma unroll
     for (int ch = 0; ch < NCH; ch++) {
       // slab (n, ch) landed; the other buffer's readers are done
+      KCNN_TMARK(6)
       __syncthreads();
+      KCNN_TMARK(0)
       {
         const int nn = ch + 1 < NCH ? n : n + (int)gridDim.x;
         const int cc = ch + 1 < NCH ? ch + 1 : 0;
@@ -941,6 +705,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
           if (ch + 1 == NCH) { KCNN_XLOAD(nn) }
         }
       }
+      KCNN_TMARK(1)
       const float *Sd = Sd0 + cur * BUF;
       const float *wrow = Wt + (ch * 32 + h) * 32 + l;
       if (DX) {  // Z[p][k] += dY[g][p] W[k][g] on the wave's own tiles
@@ -951,14 +716,30 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
           int pb = pt * 32;
           asm volatile("" : "+s"(pb));
           const float *srow = Sd + h * P + (pb + l < P ? pb + l : P - 1);
+          // half-tiles of 8 k-steps: all operand reads first, then the
+          // MFMAs (the default schedule waits on each read right before
+          // its MFMA, which serialises the LDS latency)
 #pragma unroll
-          for (int s = 0; s < 16; s++)
-            zacc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(srow[2 * s * P], wrow[2 * s * 32],
-                                                           zacc[t], 0, 0, 0);
+          for (int s0 = 0; s0 < 16; s0 += 8) {
+            float da[8], db[8];
+#pragma unroll
+            for (int s = 0; s < 8; s++) {
+              da[s] = srow[2 * (s0 + s) * P];
+              db[s] = wrow[2 * (s0 + s) * 32];
+            }
+#pragma unroll
+            for (int s = 0; s < 8; s++)
+              zacc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(da[s], db[s], zacc[t], 0, 0, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);  // LDS reads
+            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);   // MFMAs
+            __builtin_amdgcn_sched_barrier(0);
+          }
         }
       }
+      KCNN_TMARK(2)
 #pragma unroll
       for (int j = 0; j < 2; j++) {
+        if (!WG) break;
         const int pt = (int)(((j ? wg1 : wg0) >> (8 * wave)) & 0xff);
         if (pt == 0xff) continue;
         int pb = pt * 32;
@@ -975,9 +756,18 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
         const float *scol = Sd + l * P + ph;
         if (pb + 32 <= P) {  // wave-uniform: a full tile
 #pragma unroll
-          for (int s = 0; s < 16; s++)
-            wacc[ch] = __builtin_amdgcn_mfma_f32_32x32x2f32(ain[j][s], scol[2 * s],
-                                                           wacc[ch], 0, 0, 0);
+          for (int s0 = 0; s0 < 16; s0 += 8) {
+            float wb[8];
+#pragma unroll
+            for (int s = 0; s < 8; s++) wb[s] = scol[2 * (s0 + s)];
+#pragma unroll
+            for (int s = 0; s < 8; s++)
+              wacc[ch] = __builtin_amdgcn_mfma_f32_32x32x2f32(ain[j][s0 + s], wb[s],
+                                                             wacc[ch], 0, 0, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // LDS reads
+            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);  // MFMAs
+            __builtin_amdgcn_sched_barrier(0);
+          }
         } else {
           // B bit-masked to +0 past P (a row tail reads the next map's data)
 #pragma unroll
@@ -989,6 +779,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
           }
         }
       }
+      KCNN_TMARK(3)
       if (ch + 1 < NCH) cur ^= 1;
     }
     if (DX) {
@@ -1007,6 +798,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
       __syncthreads();
       float *dxr = dX + (int64_t)n * dxs;
       const int khkw = g.kh * g.kw;
+      if (!(dbg & 4))
       for (int e = tid; e < CHW; e += BWD_THREADS) {
         uint32_t c, q, wi, hi;
         g.div_HW.divmod((uint32_t)e, c, q);
@@ -1024,12 +816,19 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
         dxr[e] = sum;
       }
     }
+    KCNN_TMARK(4)
     cur ^= 1;  // the next frame's first slab is in the other buffer
   }
+  KCNN_TMARK(5)
+  if ((dbg & 16) && blockIdx.x == 0 && lane == 0)
+    printf("bwd3 wave %d: barrier %lld dma %lld dgrad %lld wgrad %lld tail %lld end %lld other %lld\n",
+           wave, tm[0], tm[1], tm[2], tm[3], tm[4], tm[5], tm[6]);
+#undef KCNN_TMARK
 #undef KCNN_XLOAD
+  if (!WG) return;
   const int E = (g.Kdim + 1) * g.G;
   float *dst = ws_part + (int64_t)blockIdx.x * E;
-  float *red = Sd0;  // [BWD_WAVES][32 * 32] <= 2 buffers; no DMA in flight
+  float *red = Sd0;  // [BWD_WAVES][32 * 32]; no DMA in flight any more
 #pragma unroll
   for (int ch = 0; ch < NCH; ch++) {
     __syncthreads();
@@ -1381,32 +1180,39 @@ size_t kcnn_conv_bwd_frame_ws(const ConvGeom &g) {
   if (g.Kdim > 31 || g.G % 32 != 0 || g.G > 128 || g.G == 0) return 0;
   if (g.P < 16 || g.P > 32 * BWD_WAVES * BWD_MAXT || 8 * g.P > BWD_THREADS * BWD_MAXV)
     return 0;
-  if (bwd_lds(g, bwd_sp(g)) > (size_t)kFrameLdsMax) return 0;
   const int S = (int)frame_grid(g, 1);
   const int E = (g.Kdim + 1) * g.G;
   return (size_t)S * E * 4 + kcnn_reduce_splits_ws(S, E);
 }
 
+static size_t bwd_dma_lds(const ConvGeom &g) {
+  return ((size_t)(g.G / 32) * 32 * 32 + (size_t)bwd_dma_sd_floats(g.P) +
+          (((size_t)g.C * (g.H + 2 * g.pad_h) * (g.W + 2 * g.pad_w) + 4) & ~(size_t)3) +
+          (size_t)((g.P + 31) & ~31)) * 4;
+}
+
+// dX (nullable) and/or gW, gb (nullable) from one pass over dY.  gW == NULL
+// runs the data gradient only and needs no workspace.
 int kcnn_conv_bwd_frame(const ConvGeom &g, const float *X, int xs,
                         const float *dY, int dys, const float *K, int ks,
                         float *dX, int dxs, float *gW, int gws, float *gb,
                         void *ws, size_t ws_bytes, hipStream_t st) {
   static const int enabled = env_int("KCNN_FUSED_BWD", 1);
-  if (!enabled) return -1;
-  const size_t need = kcnn_conv_bwd_frame_ws(g);
-  if (need == 0 || ws == nullptr || ws_bytes < need) return -1;
-  if ((uintptr_t)dY % 16 != 0 || dys % 4 != 0) return -1;  // linear dwordx4 slabs
+  static const int variant = env_int("KCNN_BWD_VARIANT", 3);  // 1: register-staged
+  static const int bdbg = env_int("KCNN_BWD_DEBUG", 0);
+  if (!enabled || (dX == nullptr && gW == nullptr)) return -1;
+  if (g.Kdim > 31 || g.G % 32 != 0 || g.G > 128 || g.G == 0) return -1;
+  if (g.P < 16 || g.P > 32 * BWD_WAVES * BWD_MAXT || 8 * g.P > BWD_THREADS * BWD_MAXV)
+    return -1;
+  if ((uintptr_t)dY % 16 != 0 || dys % 4 != 0) return -1;  // 16-B slab loads
   const int S = (int)frame_grid(g, 1);
   const int E = (g.Kdim + 1) * g.G;
-  const int SP = bwd_sp(g);
   const int ZZ = g.Kdim | 1;
-  const size_t lds = bwd_lds(g, SP);
   float *part = static_cast<float *>(ws);
-  float *tmp = part + (size_t)S * E;
-  const int Hp = g.H + 2 * g.pad_h, Wp = g.W + 2 * g.pad_w;
-  const FastDiv dhp((uint32_t)Hp), dhpwp((uint32_t)(Hp * Wp));
-  static const int variant = env_int("KCNN_BWD_VARIANT", 3);
-  static const int bdbg = env_int("KCNN_BWD_DEBUG", 0);
+  if (gW != nullptr) {
+    const size_t need = kcnn_conv_bwd_frame_ws(g);
+    if (need == 0 || ws == nullptr || ws_bytes < need) return -1;
+  }
   // weight-gradient tiles per wave: dgrad tile T belongs to wave T % 8; the
   // wgrad tiles go to the least-loaded waves, so all waves carry the same
   // number of 16-MFMA chunks (deterministic: the same table with or without dX)
@@ -1425,65 +1231,54 @@ int kcnn_conv_bwd_frame(const ConvGeom &g, const float *X, int xs,
       nw[best]++;
     }
   }
-  const size_t lds2 = lds + (size_t)BWD_WAVES * BWD_MAXT * 16 * 64 * 4;  // + ainL
-  const size_t lds3 = ((size_t)(g.G / 32) * 32 * 32 + 2 * (size_t)bwd_dma_buf_floats(g.P) +
-                       (((size_t)g.C * (g.H + 2 * g.pad_h) * (g.W + 2 * g.pad_w) + 4) & ~(size_t)3) +
-                       (size_t)((g.P + 31) & ~31)) * 4;
-  if (variant == 3 && g.C * g.HW <= BWD_THREADS * BWD_MAXX && lds3 <= (size_t)(160 * 1024) &&
-      2 * bwd_dma_buf_floats(g.P) >= BWD_WAVES * 1024 && (g.P * ZZ) <= bwd_dma_buf_floats(g.P)) {
-#define KCNN_BWD3_LAUNCH(NCH)                                                       \
-  do {                                                                              \
-    if (dX)                                                                         \
-      hipLaunchKernelGGL((conv_bwd_dma_kernel<NCH, true>), dim3(S), dim3(BWD_THREADS), \
-                         lds3, st, g, X, xs, dY, dys, K, ks, dX, dxs, part, ZZ, wg[0], wg[1]); \
-    else                                                                            \
-      hipLaunchKernelGGL((conv_bwd_dma_kernel<NCH, false>), dim3(S), dim3(BWD_THREADS), \
-                         lds3, st, g, X, xs, dY, dys, K, ks, dX, dxs, part, ZZ, wg[0], wg[1]); \
+  const size_t lds3 = bwd_dma_lds(g);
+  if (variant == 3 && g.C * g.HW <= BWD_THREADS * BWD_MAXX &&
+      lds3 <= (size_t)kBwdLdsMax) {
+#define KCNN_BWD3(NCH, DXB, WGB)                                                     \
+  hipLaunchKernelGGL((conv_bwd_dma_kernel<NCH, DXB, WGB>), dim3(S), dim3(BWD_THREADS), \
+                     lds3, st, g, X, xs, dY, dys, K, ks, dX, dxs, part, ZZ, wg[0], wg[1], bdbg)
+#define KCNN_BWD3_NCH(NCH)                                  \
+  do {                                                      \
+    if (dX && gW) KCNN_BWD3(NCH, true, true);               \
+    else if (gW) KCNN_BWD3(NCH, false, true);               \
+    else KCNN_BWD3(NCH, true, false);                       \
   } while (0)
     switch (g.G / 32) {
-      case 1: KCNN_BWD3_LAUNCH(1); break;
-      case 2: KCNN_BWD3_LAUNCH(2); break;
-      case 3: KCNN_BWD3_LAUNCH(3); break;
-      default: KCNN_BWD3_LAUNCH(4); break;
+      case 1: KCNN_BWD3_NCH(1); break;
+      case 2: KCNN_BWD3_NCH(2); break;
+      case 3: KCNN_BWD3_NCH(3); break;
+      default: KCNN_BWD3_NCH(4); break;
     }
-#undef KCNN_BWD3_LAUNCH
-  } else if (variant == 2 && g.C * g.HW <= BWD_THREADS * BWD_MAXX && lds2 <= (size_t)(160 * 1024)) {
-#define KCNN_BWD2_LAUNCH(NCH)                                                       \
-  do {                                                                              \
-    if (dX)                                                                         \
-      hipLaunchKernelGGL((conv_bwd_reg_kernel<NCH, true>), dim3(S), dim3(BWD_THREADS), \
-                         lds2, st, g, X, xs, dY, dys, K, ks, dX, dxs, part, ZZ, SP, wg[0], wg[1], bdbg); \
-    else                                                                            \
-      hipLaunchKernelGGL((conv_bwd_reg_kernel<NCH, false>), dim3(S), dim3(BWD_THREADS), \
-                         lds2, st, g, X, xs, dY, dys, K, ks, dX, dxs, part, ZZ, SP, wg[0], wg[1], bdbg); \
-  } while (0)
-    switch (g.G / 32) {
-      case 1: KCNN_BWD2_LAUNCH(1); break;
-      case 2: KCNN_BWD2_LAUNCH(2); break;
-      case 3: KCNN_BWD2_LAUNCH(3); break;
-      default: KCNN_BWD2_LAUNCH(4); break;
-    }
-#undef KCNN_BWD2_LAUNCH
+#undef KCNN_BWD3_NCH
+#undef KCNN_BWD3
   } else {
-#define KCNN_BWD_LAUNCH(NCH)                                                      \
-  do {                                                                            \
-    if (dX)                                                                       \
+    // register-staged variant: needs the gradient outputs
+    if (gW == nullptr) return -1;
+    const int SP = bwd_sp(g);
+    const size_t lds = bwd_lds(g, SP);
+    if (lds > (size_t)kFrameLdsMax) return -1;
+    const int Hp = g.H + 2 * g.pad_h, Wp = g.W + 2 * g.pad_w;
+    const FastDiv dhp((uint32_t)Hp), dhpwp((uint32_t)(Hp * Wp));
+#define KCNN_BWD1(NCH)                                                              \
+  do {                                                                              \
+    if (dX)                                                                         \
       hipLaunchKernelGGL((conv_bwd_frame_kernel<NCH, true>), dim3(S), dim3(BWD_THREADS), \
                          lds, st, g, X, xs, dY, dys, K, ks, dX, dxs, part, ZZ, SP, dhp, dhpwp); \
-    else                                                                          \
+    else                                                                            \
       hipLaunchKernelGGL((conv_bwd_frame_kernel<NCH, false>), dim3(S), dim3(BWD_THREADS), \
                          lds, st, g, X, xs, dY, dys, K, ks, dX, dxs, part, ZZ, SP, dhp, dhpwp); \
   } while (0)
-  switch (g.G / 32) {
-    case 1: KCNN_BWD_LAUNCH(1); break;
-    case 2: KCNN_BWD_LAUNCH(2); break;
-    case 3: KCNN_BWD_LAUNCH(3); break;
-    default: KCNN_BWD_LAUNCH(4); break;
-  }
-#undef KCNN_BWD_LAUNCH
+    switch (g.G / 32) {
+      case 1: KCNN_BWD1(1); break;
+      case 2: KCNN_BWD1(2); break;
+      case 3: KCNN_BWD1(3); break;
+      default: KCNN_BWD1(4); break;
+    }
+#undef KCNN_BWD1
   }
   int rc = (int)hipGetLastError();
-  if (rc) return rc;
+  if (rc || gW == nullptr) return rc;
+  float *tmp = part + (size_t)S * E;
   const int Q = (S + 31) / 32;
   hipLaunchKernelGGL(reduce_pass1, dim3((E + 255) / 256, Q), dim3(256), 0, st,
                      part, S, E, tmp);

@@ -459,8 +459,10 @@ size_t hipF_conv2d_wgrad_workspace_bytes(MatrixDim in_dim, int in_height,
   ConvGeom g = make_geom(in_dim.rows, in_height, in_width, in_channel, pad_h,
                          pad_w, kernel_height, kernel_width, group);
   if (g.oh <= 0 || g.ow <= 0) return 0;
-  const size_t a = kcnn_conv_wgrad_frame_ws(g), b = plan_wgrad(g).ws_bytes;
-  return a > b ? a : b;
+  size_t a = kcnn_conv_wgrad_frame_ws(g);
+  const size_t b = plan_wgrad(g).ws_bytes, c = kcnn_conv_bwd_frame_ws(g);
+  if (b > a) a = b;
+  return c > a ? c : a;
 }
 
 int hipF_conv2d_wgrad(const float *in, MatrixDim in_dim, int in_height,
@@ -478,6 +480,12 @@ int hipF_conv2d_wgrad(const float *in, MatrixDim in_dim, int in_height,
       grad_W_dim.rows != g.Kdim || grad_W_dim.cols != group)
     return (int)hipErrorInvalidValue;
   if (g.M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  // the fused backward's gradient-only pass (one stream of dY)
+  if (g.M > 0 && kcnn_conv_bwd_frame(g, in, in_dim.stride, out_deriv,
+                                     out_deriv_dim.stride, nullptr, 0, nullptr, 0,
+                                     grad_W, grad_W_dim.stride, grad_b, workspace,
+                                     workspace_bytes, st) == 0)
+    return 0;
   if (g.M > 0 && kcnn_conv_wgrad_frame(g, in, in_dim.stride, out_deriv,
                                        out_deriv_dim.stride, grad_W,
                                        grad_W_dim.stride, grad_b, workspace,
@@ -540,6 +548,11 @@ int hipF_conv2d_dgrad(const float *out_deriv, MatrixDim out_deriv_dim,
     return (int)hipErrorInvalidValue;
   if (g.R == 0) return 0;
   if (g.M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  // the fused backward's data-gradient-only pass
+  if (kcnn_conv_bwd_frame(g, nullptr, 0, out_deriv, out_deriv_dim.stride, kernel,
+                          kernel_dim.stride, in_deriv, in_deriv_dim.stride, nullptr,
+                          0, nullptr, nullptr, 0, st) == 0)
+    return 0;
   if (kcnn_conv_dgrad_frame(g, out_deriv, out_deriv_dim.stride, kernel,
                             kernel_dim.stride, in_deriv, in_deriv_dim.stride,
                             st) == 0)

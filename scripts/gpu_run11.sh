@@ -1,5 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-KCNN_BWD_DEBUG=16 timeout -k 10 100 python scripts/microbench.py --reps 2 --only bwd_fused > gpurun_out/micro11.log 2>&1 || exit 5
+for d in 0 4; do
+KCNN_BWD_DEBUG=$d timeout -k 10 100 python scripts/microbench.py --reps 20 --only bwd_fused,bwd_fused_nodx > gpurun_out/micro11_$d.log 2>&1 || exit 5
+done
 echo done

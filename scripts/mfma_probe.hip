@@ -35,12 +35,34 @@ __global__ __launch_bounds__(256) void probe(float *out, long long *cyc, int ite
         const float v = lds[(s * 64 + lane + it) & 4095];
         a0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v, y, a0, 0, 0, 0);
       }
-    } else {
+    } else if (MODE == 3) {
       float v[16];
 #pragma unroll
       for (int s = 0; s < 16; s++) v[s] = lds[(s * 64 + lane + it) & 4095];
 #pragma unroll
       for (int s = 0; s < 16; s++) a0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[s], y, a0, 0, 0, 0);
+    } else if (MODE == 4) {  // A and B from LDS, read just before
+#pragma unroll
+      for (int s = 0; s < 16; s++) {
+        const float v = lds[(s * 64 + lane + it) & 4095];
+        const float w = lds[(s * 64 + 2048 + lane + it) & 4095];
+        a0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v, w, a0, 0, 0, 0);
+      }
+    } else {  // A and B from LDS, 8 steps staged
+#pragma unroll
+      for (int s0 = 0; s0 < 16; s0 += 8) {
+        float v[8], w[8];
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+          v[s] = lds[((s0 + s) * 64 + lane + it) & 4095];
+          w[s] = lds[((s0 + s) * 64 + 2048 + lane + it) & 4095];
+        }
+#pragma unroll
+        for (int s = 0; s < 8; s++) a0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[s], w[s], a0, 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   }
   const long long t1 = clock64();
@@ -91,6 +113,8 @@ int main() {
     run<1>("2 interleaved chains, registers", 256, bpc);
     run<2>("A from LDS, read just before", 256, bpc);
     run<3>("A from LDS, 16 reads ahead", 256, bpc);
+    run<4>("A,B from LDS, read just before", 256, bpc);
+    run<5>("A,B from LDS, 8 steps staged", 256, bpc);
   }
   return 0;
 }

@@ -57,6 +57,8 @@ def main():
         "dgrad": (lambda: conv.Backprop(x, None, dy, dx, update=False), conv_b),
         "wgrad": (lambda: conv.ComputeGradient(x, dy, grad), conv_b),
         "bwd_fused": (lambda: conv.BackpropGradient(x, dy, dx, grad), conv_b + x.numel() * 4),
+        "bwd_fused_nodx": (lambda: conv.BackpropGradient(x, dy, None, grad, want_in_deriv=False),
+                           conv_b),
         "pool_fwd": (lambda: pool.Propagate(y, p), bench.POOL_FWD_BYTES * B),
         "pool_bwd": (lambda: pool.Backprop(y, p, dp, dyp), bench.POOL_BWD_BYTES * B),
     }

@@ -21,7 +21,11 @@ import shutil
 
 # hot-path kernel -> bench.py kernel-table key
 HOT = {
+    "conv_bwd_dma_kernel": "conv_bwd_fused",
     "conv_bwd_frame_kernel": "conv_bwd_fused",
+    "conv_fwd_regs_kernel": "conv_fwd",
+    "maxpool_group_prop_kernel": "maxpool_fwd",
+    "maxpool_group_backprop_kernel": "maxpool_bwd",
     "conv_fwd_slab_kernel": "conv_fwd",
     "conv_fwd_frame_kernel": "conv_fwd",
     "MaxpoolProp": "maxpool_fwd",

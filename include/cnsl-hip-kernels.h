@@ -106,6 +106,16 @@ int hipF_maxpool_backprop(const float *in_val, MatrixDim in_val_dim,
                           int pool_width_dim, int pool_channel_dim, int mode,
                           int write_all, kcnn_stream_t stream);
 
+/* ModPermuteChannel (conv2D.cc:685-727, kernel cnsl-cu-kernels.cu:505-528,
+ * launcher cnsl-cu-kernels.h:45 cudaF_mod_permute_channels): moves the
+ * in_height x in_width maps of `comp` into channel slot
+ * c*num_component + comp_idx of `container` (or back when
+ * from_comp_to_container == 0). */
+int hipF_mod_permute_channels(float *comp, MatrixDim comp_dim, float *container,
+                              MatrixDim container_dim, int comp_idx,
+                              int num_component, int in_height, int in_width,
+                              int from_comp_to_container, kcnn_stream_t stream);
+
 /* ---- convolution (MFMA implicit GEMM) ------------------------------------
  * Replaces the im2col + cuBLAS sgemm + copy + col2im sequence of
  * CuMatrixBase::Conv2D (conv2D.cc:43-201; launchers cnsl-cu-kernels.h:25,

@@ -72,6 +72,12 @@ int kcnn_mat_tp_inside_block(const float *m, MatrixDim dim, int group,
                              int block_size, float *out, MatrixDim out_dim);
 int kcnn_mat_mod_permute_row(const float *m, MatrixDim dim, int in_channel,
                              int block_size, float *out, MatrixDim out_dim);
+/* CuMatrixBase::ModPermuteChannel (conv2D.cc:685-727); comp is written when
+ * from_comp_to_container == 0. */
+int kcnn_mat_mod_permute_channel(float *comp, MatrixDim dim, int comp_idx,
+                                 int num_component, int in_height, int in_width,
+                                 float *container, MatrixDim container_dim,
+                                 int from_comp_to_container);
 int kcnn_mat_maxpool_prop(const float *in, MatrixDim in_dim, int in_height,
                           int in_width, int pool_height_dim,
                           int pool_width_dim, int pool_channel_dim,

@@ -243,6 +243,17 @@ def ModPermuteRow(this, in_channel, block_size, out=None):
     return out
 
 
+def ModPermuteChannel(this, comp_idx, num_component, in_height, in_width,
+                      container, from_comp_to_container):
+    """conv2D.cc:685-727; writes `container` (or `this` when
+    from_comp_to_container is False)."""
+    _ensure_init()
+    check(lib().kcnn_mat_mod_permute_channel(
+        ptr(this), dim(this), comp_idx, num_component, in_height, in_width,
+        ptr(container), dim(container), int(bool(from_comp_to_container))))
+    return container if from_comp_to_container else this
+
+
 def Maxpool_prop(this, in_height, in_width, pool_height_dim, pool_width_dim,
                  pool_channel_dim, overlap, overlap2D, out):
     _ensure_init()

@@ -232,6 +232,17 @@ int kcnn_mat_tp_inside_block(const float *m, MatrixDim dim, int group,
     x.TpInsideBlock(group, block_size, &o);
   });
 }
+int kcnn_mat_mod_permute_channel(float *comp, MatrixDim dim, int comp_idx,
+                                 int num_component, int in_height, int in_width,
+                                 float *container, MatrixDim container_dim,
+                                 int from_comp_to_container) {
+  return guard([&] {
+    auto c = view(comp, dim);
+    auto k = view(container, container_dim);
+    c.ModPermuteChannel(comp_idx, num_component, in_height, in_width, &k,
+                        from_comp_to_container != 0);
+  });
+}
 int kcnn_mat_mod_permute_row(const float *m, MatrixDim dim, int in_channel,
                              int block_size, float *out, MatrixDim out_dim) {
   return guard([&] {

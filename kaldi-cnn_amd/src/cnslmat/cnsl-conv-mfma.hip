@@ -358,12 +358,6 @@ WgradPlan plan_wgrad(const ConvGeom &g) {
   return pl;
 }
 
-// Frame-resident kernels apply when the kernel volume is small (input layers).
-size_t wgrad_ws_bytes(const ConvGeom &g) {
-  const size_t f = kcnn_conv_wgrad_frame_ws(g);
-  return f ? f : plan_wgrad(g).ws_bytes;
-}
-
 }  // namespace
 
 extern "C" {

@@ -162,6 +162,20 @@ struct CopyRowsAt {
   }
 };
 
+// conv2D.cc:706-725 / cnsl-cu-kernels.cu:505-528.
+struct ModPermuteChannels {
+  float *comp; MatrixDim comp_dim; float *cont; MatrixDim cont_dim;
+  int comp_idx, num_component, plane, to_container; FastDiv div_plane;
+  __device__ void operator()(int64_t i, int j) const {
+    uint32_t chan, pos;
+    div_plane.divmod((uint32_t)j, chan, pos);
+    const int64_t o = i * cont_dim.stride +
+                      ((int64_t)chan * num_component + comp_idx) * plane + pos;
+    if (to_container) cont[o] = comp[i * comp_dim.stride + j];
+    else comp[i * comp_dim.stride + j] = cont[o];
+  }
+};
+
 // ---------------------------------------------------------------------------
 // Max pooling.  Window of output column j (same enumeration order as the
 // reference: channel, width, height; cnsl-cu-kernels.cu:253-263).
@@ -517,6 +531,23 @@ int hipF_mod_permute_row(const float *in, MatrixDim in_dim, float *out,
   ModPermuteRow f{in, in_dim, out, out_dim, block_size,
                   FastDiv((uint32_t)in_channel)};
   return launch_elem2d(in_dim.rows, in_dim.cols, f, kcnn::as_stream(stream));
+}
+
+int hipF_mod_permute_channels(float *comp, MatrixDim comp_dim, float *container,
+                              MatrixDim container_dim, int comp_idx,
+                              int num_component, int in_height, int in_width,
+                              int from_comp_to_container, kcnn_stream_t stream) {
+  const int plane = in_height * in_width;
+  if (plane <= 0 || comp_idx < 0 || comp_idx >= num_component ||
+      container_dim.rows < comp_dim.rows ||
+      (comp_dim.cols > 0 &&
+       ((int64_t)((comp_dim.cols - 1) / plane) * num_component + comp_idx) * plane +
+               (comp_dim.cols - 1) % plane >= container_dim.cols))
+    return (int)hipErrorInvalidValue;
+  ModPermuteChannels f{comp, comp_dim, container, container_dim, comp_idx,
+                       num_component, plane, from_comp_to_container,
+                       FastDiv((uint32_t)plane)};
+  return launch_elem2d(comp_dim.rows, comp_dim.cols, f, kcnn::as_stream(stream));
 }
 
 int hipF_copy_rows_at(const float *src, MatrixDim src_dim, float *dest,

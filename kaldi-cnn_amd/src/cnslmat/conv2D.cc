@@ -180,6 +180,20 @@ void CuMatrixBase<Real>::Maxpool_backprop(
       pool_height_dim, pool_width_dim, pool_channel_dim, mode, 0, S()));
 }
 
+// conv2D.cc:685-727.  No resize: container is caller-sized (the reference
+// only asserts it is non-NULL).
+template <typename Real>
+void CuMatrixBase<Real>::ModPermuteChannel(int32 comp_idx, int32 num_component,
+                                           int32 in_height, int32 in_width,
+                                           CuMatrixBase<Real> *container,
+                                           bool fromCompToContainer) {
+  KALDI_ASSERT(container != NULL);                                    // :688
+  CuProfileScope prof("ModPermuteChannel");
+  CNSL_SAFE_CALL(hipF_mod_permute_channels(
+      data_, Dim(), container->Data(), container->Dim(), comp_idx,
+      num_component, in_height, in_width, fromCompToContainer ? 1 : 0, S()));
+}
+
 // Member-wise explicit instantiation (the class itself is instantiated in
 // kaldi-lite/cu-matrix.cc).
 template void CuMatrixBase<float>::Conv2D(const CuMatrixBase<float> &, int32,
@@ -196,6 +210,8 @@ template void CuMatrixBase<float>::TpInsideBlock(int32, int32,
                                                  CuMatrix<float> *) const;
 template void CuMatrixBase<float>::ModPermuteRow(int32, int32,
                                                  CuMatrix<float> *) const;
+template void CuMatrixBase<float>::ModPermuteChannel(int32, int32, int32, int32,
+                                                     CuMatrixBase<float> *, bool);
 template void CuMatrixBase<float>::Maxpool_prop(int32, int32, int32, int32,
                                                 int32, bool, bool,
                                                 CuMatrixBase<float> *) const;

@@ -159,8 +159,10 @@ class CuMatrixBase {
                         int32 in_width, int32 pool_height_dim,
                         int32 pool_width_dim, int32 pool_channel_dim,
                         bool overlap, bool overlap2D) const;
-  // ModPermuteChannel (cu-matrix.h:481) is only used by the unregistered
-  // ConvolutionComponentContainer: out of scope.
+  // (used by the reference's unregistered ConvolutionComponentContainer)
+  void ModPermuteChannel(int32 comp_idx, int32 num_component, int32 in_height,
+                         int32 in_width, CuMatrixBase<Real> *container,
+                         bool fromCompToContainer);
 
  protected:
   CuMatrixBase() : data_(nullptr), num_cols_(0), num_rows_(0), stride_(0) {}

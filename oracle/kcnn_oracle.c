@@ -371,6 +371,24 @@ int orc_mod_permute_row(const orc_mat *m, int in_channel, int block_size,
   return 0;
 }
 
+/* conv2D.cc:706-725 (CPU branch of ModPermuteChannel). */
+int orc_mod_permute_channel(orc_mat *comp, int comp_idx, int num_component,
+                            int in_height, int in_width, orc_mat *container,
+                            int from_comp_to_container) {
+  const int plane = in_height * in_width;
+  for (int i = 0; i < comp->rows; i++) {
+    for (int j = 0; j < comp->cols; j++) {
+      const int chan_idx = j / plane, pos_idx = j % plane;
+      const int out_chan_idx = chan_idx * num_component + comp_idx;
+      const int oc = out_chan_idx * plane + pos_idx;
+      CHECK(i < container->rows && oc < container->cols);
+      if (from_comp_to_container) AT(container, i, oc) = AT(comp, i, j);
+      else AT(comp, i, j) = AT(container, i, oc);
+    }
+  }
+  return 0;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Window enumeration shared by Maxpool_prop/backprop.  For output column j it
  * lists the input columns of its pooling window in the reference's loop

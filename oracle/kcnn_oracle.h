@@ -76,6 +76,10 @@ int orc_tp_inside_block(const orc_mat *m, int group, int block_size,
 /* conv2D.cc:429-463 (CPU :452-462). */
 int orc_mod_permute_row(const orc_mat *m, int in_channel, int block_size,
                         orc_mat *out);
+/* conv2D.cc:706-725 */
+int orc_mod_permute_channel(orc_mat *comp, int comp_idx, int num_component,
+                            int in_height, int in_width, orc_mat *container,
+                            int from_comp_to_container);
 /* conv2D.cc:465-559; non-overlap CPU :531-557, overlap :541-542,
  * overlap2D follows the GPU kernel cnsl-cu-kernels.cu:405-452 (the CPU
  * branch :503-528 does not compile as committed). */

@@ -157,6 +157,13 @@ def mod_permute_row(m, C, bs):
     return out
 
 
+def mod_permute_channel(comp, comp_idx, num_component, H, W, container, to_container):
+    _chk(lib().orc_mod_permute_channel(ctypes.byref(mat(comp)), comp_idx, num_component,
+                                       H, W, ctypes.byref(mat(container)),
+                                       int(bool(to_container))))
+    return container if to_container else comp
+
+
 def maxpool_prop(x, H, W, ph, pw, pc, out_dim, overlap=False, overlap2D=False):
     out = np.zeros((x.shape[0], out_dim), np.float32)
     _chk(lib().orc_maxpool_prop(ctypes.byref(mat(x)), H, W, ph, pw, pc,

@@ -112,6 +112,20 @@ def test_mod_permute_row(kc, C, bs, cols):
                 O.mod_permute_row(m, C, bs), "ModPermuteRow")
 
 
+@pytest.mark.parametrize("H,W,C,K,R", [(33, 11, 4, 2, 5), (2, 3, 1, 3, 7), (1, 1, 5, 4, 2)])
+def test_mod_permute_channel(kc, H, W, C, K, R):
+    r = rng(H + W + C + K)
+    comp = randn(r, (R, C * H * W))
+    cont = randn(r, (R, K * C * H * W))
+    for k in range(K):
+        exp = O.mod_permute_channel(comp, k, K, H, W, cont.copy(), True)
+        got = kc.ModPermuteChannel(padded(comp), k, K, H, W, padded(cont), True)
+        assert_same(host(got), exp, "ModPermuteChannel to container")
+        back = kc.ModPermuteChannel(padded(np.zeros_like(comp)), k, K, H, W,
+                                    padded(exp), False)
+        assert_same(host(back), comp, "ModPermuteChannel from container")
+
+
 POOLS = [  # (H, W, C, ph, pw, pc, overlap, overlap2D)
     (33, 11, 128, 1, 1, 4, False, False),   # BASELINE c2: 1x1x4 intermap pool
     (8, 9, 256, 2, 1, 4, False, False),     # c5 P2

@@ -131,6 +131,17 @@ def test_reshape_helpers_match_appendix_a():
         exp[(i % C) * bs + i // C] = M[i]
     assert_same(mp, exp, "ModPermuteRow")
 
+    H0, W0, K = 3, 2, 3                                        # conv2D.cc:706-725
+    comp = randn(r, (R, C * H0 * W0))
+    cont = randn(r, (R, K * C * H0 * W0))
+    exp = cont.copy()
+    for j in range(C * H0 * W0):
+        exp[:, ((j // (H0 * W0)) * K + 1) * H0 * W0 + j % (H0 * W0)] = comp[:, j]
+    assert_same(O.mod_permute_channel(comp, 1, K, H0, W0, cont.copy(), True), exp,
+                "ModPermuteChannel to container")
+    back = O.mod_permute_channel(np.zeros_like(comp), 1, K, H0, W0, exp, False)
+    assert_same(back, comp, "ModPermuteChannel from container")
+
     M = randn(r, (R, G * bs))
     v = randn(r, (G,))
     exp = M + np.repeat(v, bs)[None, :]                        # A.2

@@ -11,6 +11,7 @@
 // the only one of these on the training step -- wave-contiguous output
 // columns so every wave reads and writes whole 256-B row segments.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include "hip-util.h"
 
@@ -364,6 +365,79 @@ __global__ __launch_bounds__(256) void maxpool_group_prop_kernel(
   }
 }
 
+// Direct channel-group forward: no LDS and no barriers.  Output e of the
+// flattened [rows x cols_out] index space reads its PC inputs straight from
+// HBM; consecutive lanes read consecutive floats of each map, so every load
+// instruction is a 256-B coalesced run and each input byte is read once.  All
+// kPoolDirectOut * PC loads of a thread are issued before the first max.
+constexpr int kPoolDirectOut = 8;
+
+template <int PC>
+__global__ __launch_bounds__(256) void maxpool_direct_prop_kernel(
+    const float *__restrict__ src, int64_t ss, float *__restrict__ dst,
+    int64_t ds, uint32_t total, FastDiv div_cols, FastDiv div_plane, int plane) {
+  const uint32_t base = blockIdx.x * (256u * kPoolDirectOut) + threadIdx.x;
+  float v[kPoolDirectOut][PC];
+  int64_t out[kPoolDirectOut];
+#pragma unroll
+  for (int t = 0; t < kPoolDirectOut; t++) {
+    const uint32_t e = base + 256u * t;
+    const uint32_t ec = e < total ? e : total - 1;
+    uint32_t row, j, k, q;
+    div_cols.divmod(ec, row, j);
+    div_plane.divmod(j, k, q);
+    const float *m = src + (int64_t)row * ss + (int64_t)k * PC * plane + q;
+#pragma unroll
+    for (int c = 0; c < PC; c++) v[t][c] = m[c * plane];
+    out[t] = e < total ? (int64_t)row * ds + j : -1;
+  }
+#pragma unroll
+  for (int t = 0; t < kPoolDirectOut; t++) {
+    float val = -1e20f;
+#pragma unroll
+    for (int c = 0; c < PC; c++)
+      if (val < v[t][c]) val = v[t][c];
+    if (out[t] >= 0) dst[out[t]] = val;
+  }
+}
+
+// Direct channel-group backprop (write_all semantics, like the group kernel
+// below): output e routes dP[e] to every input of its window equal to P[e].
+template <int PC>
+__global__ __launch_bounds__(256) void maxpool_direct_backprop_kernel(
+    const float *__restrict__ x, int64_t xs, const float *__restrict__ y,
+    int64_t ys, const float *__restrict__ dy, int64_t dys,
+    float *__restrict__ dx, int64_t dxs, uint32_t total, FastDiv div_cols,
+    FastDiv div_plane, int plane) {
+  const uint32_t base = blockIdx.x * (256u * kPoolDirectOut) + threadIdx.x;
+  float v[kPoolDirectOut][PC], pv[kPoolDirectOut], dv[kPoolDirectOut];
+  int64_t in_off[kPoolDirectOut];
+  bool ok[kPoolDirectOut];
+#pragma unroll
+  for (int t = 0; t < kPoolDirectOut; t++) {
+    const uint32_t e = base + 256u * t;
+    ok[t] = e < total;
+    const uint32_t ec = ok[t] ? e : total - 1;
+    uint32_t row, j, k, q;
+    div_cols.divmod(ec, row, j);
+    div_plane.divmod(j, k, q);
+    const int64_t w = (int64_t)k * PC * plane + q;
+    const float *m = x + (int64_t)row * xs + w;
+#pragma unroll
+    for (int c = 0; c < PC; c++) v[t][c] = m[c * plane];
+    pv[t] = y[(int64_t)row * ys + j];
+    dv[t] = dy[(int64_t)row * dys + j];  // own stride (B14)
+    in_off[t] = (int64_t)row * dxs + w;
+  }
+#pragma unroll
+  for (int t = 0; t < kPoolDirectOut; t++) {
+    if (!ok[t]) continue;
+#pragma unroll
+    for (int c = 0; c < PC; c++)
+      dx[in_off[t] + c * plane] = v[t][c] == pv[t] ? dv[t] : 0.0f;
+  }
+}
+
 // Writes every element of the group (routed derivative or 0): the fused
 // in_deriv->Resize(kSetZero) of MaxpoolComponent::Backprop (:889).
 __global__ __launch_bounds__(256) void maxpool_group_backprop_kernel(
@@ -405,6 +479,15 @@ __global__ __launch_bounds__(256) void maxpool_group_backprop_kernel(
   }
 }
 
+// KCNN_POOL_DIRECT=0 selects the LDS-staged group forward (A/B measurements).
+bool env_pool_direct() {
+  static const int v = [] {
+    const char *e = getenv("KCNN_POOL_DIRECT");
+    return e ? atoi(e) : 1;
+  }();
+  return v != 0;
+}
+
 // The group kernels apply when the pool is channel-only and every group of
 // every row starts 16-B aligned.
 bool pool_groups_ok(const void *a, int64_t stride, int plane, int pc, int ph,
@@ -426,9 +509,27 @@ PoolGroups make_pool_groups(int64_t rows, int cols_out, int plane, int pc) {
   return pg;
 }
 
-unsigned pool_grid(int64_t total) {
-  int64_t b = (total + kPoolGroups - 1) / kPoolGroups;
-  return (unsigned)(b < 2048 ? (b > 0 ? b : 1) : 2048);
+// Grid-stride pool kernels launch exactly one resident wave of workgroups:
+// with more blocks than fit (the forward's 23 KB of LDS allows 6 per CU at
+// c2), the surplus runs as a second, mostly idle round.
+template <typename K>
+unsigned pool_grid(int64_t total, K kernel, size_t lds_bytes) {
+  static thread_local int dev = -1, cus = 0;
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) d = 0;
+  if (d != dev) {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) !=
+        hipSuccess || cus <= 0)
+      cus = 256;
+    dev = d;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds_bytes) !=
+          hipSuccess || per_cu <= 0)
+    per_cu = 1;
+  const int64_t b = (total + kPoolGroups - 1) / kPoolGroups;
+  const int64_t cap = (int64_t)cus * per_cu;
+  return (unsigned)(b < cap ? (b > 0 ? b : 1) : cap);
 }
 
 PoolGeom make_pool_geom(int in_h, int in_w, int ph, int pw, int pc, int mode,
@@ -563,6 +664,23 @@ int hipF_maxpool_prop(const float *src, MatrixDim src_dim, float *pool,
                       int pool_channel_dim, int mode, kcnn_stream_t stream) {
   if (mode != 0) pool_height_dim = pool_width_dim = 1;  // cnsl-cu-kernels.cu:316
   const int plane = in_height * in_width;
+  const int64_t nout = (int64_t)pool_dim.rows * pool_dim.cols;
+  if (mode == 0 && pool_height_dim == 1 && pool_width_dim == 1 &&
+      pool_channel_dim >= 2 && pool_channel_dim <= 4 && pool_dim.cols % plane == 0 &&
+      src_dim.cols == pool_dim.cols * pool_channel_dim && nout < ((int64_t)1 << 31) &&
+      env_pool_direct()) {
+    if (nout == 0) return 0;
+    const unsigned blocks =
+        (unsigned)((nout + 256 * kPoolDirectOut - 1) / (256 * kPoolDirectOut));
+    auto kern = pool_channel_dim == 4   ? maxpool_direct_prop_kernel<4>
+                : pool_channel_dim == 3 ? maxpool_direct_prop_kernel<3>
+                                        : maxpool_direct_prop_kernel<2>;
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, kcnn::as_stream(stream),
+                       src, (int64_t)src_dim.stride, pool, (int64_t)pool_dim.stride,
+                       (uint32_t)nout, FastDiv((uint32_t)pool_dim.cols),
+                       FastDiv((uint32_t)plane), plane);
+    return kcnn::launch_status();
+  }
   if (pool_groups_ok(src, src_dim.stride, plane, pool_channel_dim,
                      pool_height_dim, pool_width_dim, mode) &&
       (int64_t)pool_dim.rows * (pool_dim.cols / plane) < ((int64_t)1 << 31) &&
@@ -570,9 +688,10 @@ int hipF_maxpool_prop(const float *src, MatrixDim src_dim, float *pool,
     PoolGroups pg = make_pool_groups(pool_dim.rows, pool_dim.cols, plane,
                                      pool_channel_dim);
     if (pg.total == 0) return 0;
-    hipLaunchKernelGGL(maxpool_group_prop_kernel, dim3(pool_grid(pg.total)),
-                       dim3(256), (size_t)kPoolGroups * plane * pool_channel_dim * 4,
-                       kcnn::as_stream(stream), src, (int64_t)src_dim.stride, pool,
+    const size_t lds = (size_t)kPoolGroups * plane * pool_channel_dim * 4;
+    hipLaunchKernelGGL(maxpool_group_prop_kernel,
+                       dim3(pool_grid(pg.total, maxpool_group_prop_kernel, lds)),
+                       dim3(256), lds, kcnn::as_stream(stream), src, (int64_t)src_dim.stride, pool,
                        (int64_t)pool_dim.stride, pg);
     return kcnn::launch_status();
   }
@@ -592,6 +711,24 @@ int hipF_maxpool_backprop(const float *in_val, MatrixDim in_val_dim,
                           int write_all, kcnn_stream_t stream) {
   hipStream_t st = kcnn::as_stream(stream);
   const int plane0 = in_height * in_width;
+  const int64_t nout = (int64_t)out_val_dim.rows * out_val_dim.cols;
+  if (write_all && mode == 0 && pool_height_dim == 1 && pool_width_dim == 1 &&
+      pool_channel_dim >= 2 && pool_channel_dim <= 4 && out_val_dim.cols % plane0 == 0 &&
+      in_val_dim.cols == out_val_dim.cols * pool_channel_dim &&
+      nout < ((int64_t)1 << 31) && env_pool_direct()) {
+    if (nout == 0) return 0;
+    const unsigned blocks =
+        (unsigned)((nout + 256 * kPoolDirectOut - 1) / (256 * kPoolDirectOut));
+    auto kern = pool_channel_dim == 4   ? maxpool_direct_backprop_kernel<4>
+                : pool_channel_dim == 3 ? maxpool_direct_backprop_kernel<3>
+                                        : maxpool_direct_backprop_kernel<2>;
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, st, in_val, (int64_t)in_val_dim.stride, out_val,
+                       (int64_t)out_val_dim.stride, out_deriv,
+                       (int64_t)out_deriv_dim.stride, dest, (int64_t)dest_dim.stride,
+                       (uint32_t)nout, FastDiv((uint32_t)out_val_dim.cols),
+                       FastDiv((uint32_t)plane0), plane0);
+    return kcnn::launch_status();
+  }
   if (write_all &&
       pool_groups_ok(in_val, in_val_dim.stride, plane0, pool_channel_dim,
                      pool_height_dim, pool_width_dim, mode) &&
@@ -603,8 +740,10 @@ int hipF_maxpool_backprop(const float *in_val, MatrixDim in_val_dim,
     PoolGroups pg = make_pool_groups(out_val_dim.rows, out_val_dim.cols, plane0,
                                      pool_channel_dim);
     if (pg.total == 0) return 0;
-    hipLaunchKernelGGL(maxpool_group_backprop_kernel, dim3(pool_grid(pg.total)),
-                       dim3(256), (size_t)2 * kPoolGroups * plane0 * 4, st, in_val,
+    const size_t lds = (size_t)2 * kPoolGroups * plane0 * 4;
+    hipLaunchKernelGGL(maxpool_group_backprop_kernel,
+                       dim3(pool_grid(pg.total, maxpool_group_backprop_kernel, lds)),
+                       dim3(256), lds, st, in_val,
                        (int64_t)in_val_dim.stride, out_val, (int64_t)out_val_dim.stride,
                        out_deriv, (int64_t)out_deriv_dim.stride, dest,
                        (int64_t)dest_dim.stride, pg);

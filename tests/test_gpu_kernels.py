@@ -132,6 +132,9 @@ POOLS = [  # (H, W, C, ph, pw, pc, overlap, overlap2D)
     (1, 12, 256, 1, 2, 1, False, False),    # nnet.config maxpool
     (6, 4, 8, 2, 2, 2, False, False),
     (3, 5, 6, 3, 5, 3, False, False),
+    (5, 3, 12, 1, 1, 3, False, False),      # channel-only pc=3 (direct kernel)
+    (7, 2, 8, 1, 1, 2, False, False),       # channel-only pc=2
+    (3, 3, 16, 1, 1, 8, False, False),      # channel-only pc=8 (group kernel)
     (4, 3, 6, 1, 1, 3, True, False),        # overlap (1-D channel sliding)
     (2, 3, 16, 1, 1, 2, False, True),       # overlap2D (4x4 map, 2x2 window)
     (3, 2, 25, 1, 1, 3, False, True),

@@ -38,6 +38,11 @@ CONV_BWD_BYTES = 4 * (2 * H * W * C + P * G)          # 196,416: X, dY in; dX ou
 CONV_BWD_FLOP = 2 * CONV_FLOP_PER_PASS + 2 * P * G    # dgrad + wgrad + bias grad
 POOL_FWD_BYTES = 4 * (P * G + POOL_OUT)               # 232,320
 POOL_BWD_BYTES = 4 * (2 * P * G + 2 * POOL_OUT)       # 464,640
+# Conv -> Maxpool run fused by the kcnn_nnet runtime (kcnn_set_fusion):
+# forward reads X, writes Y, the pooled output and a 1-byte routing mask; the
+# pool backward reads the mask and dP and writes dY.
+CONV_POOL_FWD_BYTES = 4 * (H * W * C + P * G + POOL_OUT) + POOL_OUT  # 246,840
+POOL_BWD_MASK_BYTES = POOL_OUT + 4 * (POOL_OUT + P * G)               # 243,936
 FC_FLOP = 3 * 2 * POOL_OUT * FC_OUT                   # 71,368,704
 
 
@@ -110,6 +115,8 @@ def main():
     ap.add_argument("--frames-per-gpu", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--no-fusion", action="store_true",
+                    help="run Conv and Maxpool as separate components")
     args = ap.parse_args()
 
     import torch
@@ -127,6 +134,7 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
     kcnn.init(local_rank)
+    kcnn.set_fusion(not args.no_fusion)
     kcnn.set_randn_seed(20261015)  # identical initial params on every replica
 
     B = args.frames_per_gpu
@@ -186,6 +194,8 @@ def main():
     k_wgrad = avg("ConvolutionComponent::ComputeGradient")
     k_pool_f = avg("MaxpoolComponent::Propagate")
     k_pool_b = avg("MaxpoolComponent::Backprop")
+    k_fwd_pool = avg("ConvolutionComponent::PropagateMaxpool")
+    k_pool_bm = avg("MaxpoolComponent::BackpropFromMask")
     k_fc = prof.get("AddMatMat", (0.0, 0))
     kernels = {}
     for name, ms, flop, byts in (
@@ -194,7 +204,9 @@ def main():
             ("conv_dgrad", k_dgrad, CONV_FLOP_PER_PASS * B, CONV_BYTES_PER_PASS * B),
             ("conv_wgrad", k_wgrad, CONV_FLOP_PER_PASS * B, CONV_BYTES_PER_PASS * B),
             ("maxpool_fwd", k_pool_f, 0, POOL_FWD_BYTES * B),
-            ("maxpool_bwd", k_pool_b, 0, POOL_BWD_BYTES * B)):
+            ("maxpool_bwd", k_pool_b, 0, POOL_BWD_BYTES * B),
+            ("conv_fwd_maxpool", k_fwd_pool, CONV_FLOP_PER_PASS * B, CONV_POOL_FWD_BYTES * B),
+            ("maxpool_bwd_mask", k_pool_bm, 0, POOL_BWD_MASK_BYTES * B)):
         if ms:
             # the roofline that bounds it: the larger of bytes/peak-BW and
             # flops/peak-MFMA (algorithmic work)
@@ -246,7 +258,8 @@ def main():
             "config": {"workload": "c2: Conv(40x11x3, 8x1, 128) -> Maxpool(1x1x4) -> "
                                    "FC(11616->1024), fwd+bwd+update",
                        "frames_per_gpu": B, "global_batch": B * world,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}",
+                       "conv_maxpool_fusion": not args.no_fusion},
             "roofline": roofline,
             "kernels": kernels,
         }

@@ -106,6 +106,16 @@ int hipF_maxpool_backprop(const float *in_val, MatrixDim in_val_dim,
                           int pool_width_dim, int pool_channel_dim, int mode,
                           int write_all, kcnn_stream_t stream);
 
+/* MaxpoolComponent::Backprop (nnet-component-nnet0.cc:882-892, Resize to
+ * zero + Maxpool_backprop A.9) of a channel-only pool from the mask written
+ * by hipF_conv2d_maxpool: in_deriv[n][(pc*(j/P) + c)*P + j%P] = bit c of
+ * mask[n * mask_stride + j] ? out_deriv[n][j] : 0, every element written. */
+int hipF_maxpool_backprop_mask(const unsigned char *mask, int mask_stride,
+                               const float *out_deriv, MatrixDim out_deriv_dim,
+                               float *in_deriv, MatrixDim in_deriv_dim,
+                               int in_height, int in_width,
+                               int pool_channel_dim, kcnn_stream_t stream);
+
 /* ModPermuteChannel (conv2D.cc:685-727, kernel cnsl-cu-kernels.cu:505-528,
  * launcher cnsl-cu-kernels.h:45 cudaF_mod_permute_channels): moves the
  * in_height x in_width maps of `comp` into channel slot
@@ -136,6 +146,24 @@ int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
                 int group, const float *bias, float *out, MatrixDim out_dim,
                 int concat, void *workspace, size_t workspace_bytes,
                 kcnn_stream_t stream);
+
+/* ConvolutionComponent::Propagate (nnet-component-nnet0.cc:423-446) followed
+ * by a channel-only MaxpoolComponent::Propagate (:869-880, pool 1 x 1 x
+ * pool_channel_dim, no overlap) in one pass: out as hipF_conv2d(concat=1),
+ * pool = Maxpool_prop(out) (conv2D.cc:465-559, bit-identical), and
+ * mask[n * mask_stride + j] bit c = (out[n][(pc*(j/P) + c)*P + j%P] ==
+ * pool[n][j]) with P = oh*ow -- the routing MaxpoolComponent::Backprop
+ * (:882-892) derives from in_value == out_value.  pool_channel_dim in
+ * {2, 4, 8}.  Returns -1 without launching when the geometry is not covered
+ * (the caller then runs the two components separately). */
+int hipF_conv2d_maxpool(const float *in, MatrixDim in_dim, int in_height,
+                        int in_width, int in_channel, int pad_h, int pad_w,
+                        const float *kernel, MatrixDim kernel_dim,
+                        int kernel_height, int kernel_width, int group,
+                        const float *bias, float *out, MatrixDim out_dim,
+                        float *pool, MatrixDim pool_dim, unsigned char *mask,
+                        int mask_stride, int pool_channel_dim,
+                        kcnn_stream_t stream);
 
 /* Weight gradient of ConvolutionComponent::Update (nnet-component-nnet0.cc:
  * 738-765 + :775): grad_W[c*kh*kw + kx*kh + ky][g] = sum_{n,p} X[n][..] *

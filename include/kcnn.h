@@ -47,6 +47,11 @@ int kcnn_set_stream(kcnn_stream_t stream);
 int kcnn_synchronize(void);
 int kcnn_set_literal_path(int literal);  /* replay reference call sequences */
 int kcnn_set_profiling(int on);
+/* kcnn_nnet_* runtime: run a ConvolutionComponent followed by a channel-only
+ * MaxpoolComponent (1 x 1 x pc) as one fused forward that also saves the
+ * pool's routing mask, and backprop that pool from the mask.  Outputs and
+ * derivatives are identical either way.  Default on (env KCNN_FUSE=0: off). */
+int kcnn_set_fusion(int on);
 /* Writes the per-function hipEvent profile (CuDevice::PrintProfile). */
 int kcnn_profile_string(char *buf, size_t len);
 void kcnn_set_randn_seed(uint64_t seed);
@@ -171,6 +176,10 @@ int kcnn_nnet_propagate(kcnn_nnet *n, const float *in, MatrixDim in_dim);
 /* Device pointer + dims of layer i's output (i = -1: the input copy). */
 int kcnn_nnet_output(const kcnn_nnet *n, int i, const float **data,
                      MatrixDim *dim);
+/* Device pointer + dims of d(input_i) left by the last backprop of
+ * component i (rows = 0 before one ran, or when it was skipped). */
+int kcnn_nnet_input_deriv(const kcnn_nnet *n, int i, const float **data,
+                          MatrixDim *dim);
 /* Backprop of component i given d(output_i) = the buffer filled by the
  * previous call (or `out_deriv` for the last component).  mode 0: reference
  * (update in place); 1: write the gradient into grad (device, length

@@ -131,6 +131,11 @@ def set_profiling(on: bool):
     check(lib().kcnn_set_profiling(int(bool(on))))
 
 
+def set_fusion(on: bool):
+    """kcnn_nnet runtime: fuse Conv -> channel-only Maxpool (see kcnn.h)."""
+    check(lib().kcnn_set_fusion(int(bool(on))))
+
+
 def profile_string() -> str:
     buf = ctypes.create_string_buffer(1 << 16)
     check(lib().kcnn_profile_string(buf, len(buf)))
@@ -488,6 +493,13 @@ class Nnet:
         p = ctypes.c_void_p()
         d = MatrixDim()
         check(lib().kcnn_nnet_output(self._h, i, ctypes.byref(p), ctypes.byref(d)))
+        return _device_view(p.value, d)
+
+    def InputDeriv(self, i):
+        """d(input of component i) from the last backprop, as a torch view."""
+        p = ctypes.c_void_p()
+        d = MatrixDim()
+        check(lib().kcnn_nnet_input_deriv(self._h, i, ctypes.byref(p), ctypes.byref(d)))
         return _device_view(p.value, d)
 
     def BackpropComponent(self, i, out_deriv=None, mode=0, grad=None,

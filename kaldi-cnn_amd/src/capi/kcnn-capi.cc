@@ -4,8 +4,10 @@
 // borrowed CuMatrix views.
 #include "kcnn.h"
 
+#include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <fstream>
 #include <memory>
 #include <sstream>
@@ -32,11 +34,27 @@ struct kcnn_nnet {
   std::vector<CuMatrix<BaseFloat>> fwd;    // fwd[0] borrowed input, fwd[i+1] = out_i
   std::vector<CuMatrix<BaseFloat>> deriv;  // deriv[i] = d input_i
   int num_chunks = 0;
-  ~kcnn_nnet() { for (auto *c : comps) delete c; }
+  // Conv -> channel-only Maxpool pairs run fused: routing mask of pool i
+  // ([rows x OutputDim] bytes), valid for the minibatch of the last Propagate
+  std::vector<unsigned char *> mask;
+  std::vector<size_t> mask_bytes;
+  std::vector<char> mask_valid;
+  ~kcnn_nnet() {
+    for (auto *m : mask)
+      if (m) CuDevice::Instantiate().Free(m);
+    for (auto *c : comps) delete c;
+  }
 };
 
 namespace {
 thread_local std::string g_err;
+
+// Runtime fusion of Conv -> channel-only Maxpool (kcnn_set_fusion; env
+// KCNN_FUSE=0 turns it off).
+int g_fusion = [] {
+  const char *e = getenv("KCNN_FUSE");
+  return e && *e ? atoi(e) : 1;
+}();
 
 int fail(const char *what) {
   g_err = what;
@@ -140,6 +158,10 @@ int kcnn_synchronize(void) {
 }
 int kcnn_set_literal_path(int literal) {
   cnsl::nnet0::SetLiteralPath(literal != 0);
+  return 0;
+}
+int kcnn_set_fusion(int on) {
+  g_fusion = on != 0;
   return 0;
 }
 int kcnn_set_profiling(int on) {
@@ -471,6 +493,9 @@ kcnn_nnet *kcnn_nnet_new(const char *config) {
     for (auto *c : n->comps) n->handles.push_back(kcnn_component{c});
     n->fwd.resize(n->comps.size() + 1);
     n->deriv.resize(n->comps.size());
+    n->mask.assign(n->comps.size(), nullptr);
+    n->mask_bytes.assign(n->comps.size(), 0);
+    n->mask_valid.assign(n->comps.size(), 0);
   });
   return rc ? nullptr : n.release();
 }
@@ -481,12 +506,45 @@ kcnn_component *kcnn_nnet_component(kcnn_nnet *n, int i) {
   return &n->handles[i];
 }
 
+// The non-virtual Component::Propagate's sizing (nnet-component.h:203-215):
+// resize (zero-filled) only when the size differs.
+static void size_output(CuMatrix<BaseFloat> *m, int rows, int cols) {
+  if (m->NumRows() != rows || m->NumCols() != cols) m->Resize(rows, cols);
+}
+
+// Component i (Conv) and i+1 (channel-only Maxpool) in one fused pass;
+// false when the pair does not qualify.
+static bool propagate_pair(kcnn_nnet *n, size_t i) {
+  using cnsl::nnet0::ConvolutionComponent;
+  using cnsl::nnet0::MaxpoolComponent;
+  if (!g_fusion || i + 1 >= n->comps.size()) return false;
+  auto *conv = dynamic_cast<ConvolutionComponent *>(n->comps[i]);
+  auto *pool = dynamic_cast<MaxpoolComponent *>(n->comps[i + 1]);
+  if (!conv || !pool || pool->FusableChannelPool() == 0) return false;
+  const int rows = n->fwd[i].NumRows();
+  const size_t need = (size_t)rows * pool->OutputDim();
+  if (n->mask_bytes[i + 1] < need) {
+    if (n->mask[i + 1]) CuDevice::Instantiate().Free(n->mask[i + 1]);
+    n->mask[i + 1] = static_cast<unsigned char *>(CuDevice::Instantiate().Malloc(need));
+    n->mask_bytes[i + 1] = need;
+  }
+  size_output(&n->fwd[i + 1], rows, conv->OutputDim());
+  size_output(&n->fwd[i + 2], rows, pool->OutputDim());
+  if (!conv->PropagateMaxpool(n->fwd[i], &n->fwd[i + 1], *pool, &n->fwd[i + 2],
+                              n->mask[i + 1], pool->OutputDim()))
+    return false;
+  n->mask_valid[i + 1] = 1;
+  return true;
+}
+
 int kcnn_nnet_propagate(kcnn_nnet *n, const float *in, MatrixDim in_dim) {
   return guard([&] {
     KALDI_ASSERT(in_dim.cols == n->comps[0]->InputDim());
     borrow(&n->fwd[0], in, in_dim);
     n->num_chunks = in_dim.rows;
+    std::fill(n->mask_valid.begin(), n->mask_valid.end(), 0);
     for (size_t i = 0; i < n->comps.size(); i++) {
+      if (propagate_pair(n, i)) { i++; continue; }
       ChunkInfo ii(n->comps[i]->InputDim(), n->num_chunks, 0, 0);
       ChunkInfo oi(n->comps[i]->OutputDim(), n->num_chunks, 0, 0);
       n->comps[i]->Propagate(ii, oi, n->fwd[i], &n->fwd[i + 1]);
@@ -499,6 +557,16 @@ int kcnn_nnet_output(const kcnn_nnet *n, int i, const float **data,
   return guard([&] {
     KALDI_ASSERT(i >= -1 && i < (int)n->comps.size());
     const CuMatrix<BaseFloat> &m = n->fwd[i + 1];
+    *data = m.Data();
+    *dim = m.Dim();
+  });
+}
+
+int kcnn_nnet_input_deriv(const kcnn_nnet *n, int i, const float **data,
+                          MatrixDim *dim) {
+  return guard([&] {
+    KALDI_ASSERT(i >= 0 && i < (int)n->comps.size());
+    const CuMatrix<BaseFloat> &m = n->deriv[i];
     *data = m.Data();
     *dim = m.Dim();
   });
@@ -522,6 +590,12 @@ int kcnn_nnet_backprop_component(kcnn_nnet *n, int i, const float *out_deriv,
     if (i == 0 && skip_first_dx && u) dx = nullptr;
     if (mode == 1 && u) {
       u->BackpropGradient(ii, oi, n->fwd[i], n->fwd[i + 1], od, dx, grad);
+      return;
+    }
+    if (n->mask_valid[i]) {  // pool of a fused pair: route through its mask
+      auto *pool = dynamic_cast<cnsl::nnet0::MaxpoolComponent *>(c);
+      KALDI_ASSERT(pool != NULL);
+      pool->BackpropFromMask(n->mask[i], pool->OutputDim(), od, dx);
       return;
     }
     Component *to_update = (mode == 0 && u) ? c : nullptr;

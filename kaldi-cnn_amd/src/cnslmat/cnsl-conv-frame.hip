@@ -214,11 +214,18 @@ __global__ __launch_bounds__(256) void conv_fwd_slab_kernel(
 // (a contiguous 32 x P run of Y) is staged in LDS and streamed out with
 // 16-B stores; bias fused.  KS = k-steps (Kdim <= 2*KS, padded taps carry
 // zero weights), FT = position tiles per wave (P <= 4*32*FT).
-template <int KS, int FT>
+// PC > 0 also runs the channel-only max pool that follows the convolution
+// (MaxpoolComponent with pool 1 x 1 x PC, nnet-component-nnet0.cc:869-880)
+// on the LDS-resident slab: pool[n][j*P + q] = max over maps PC*j .. PC*j+PC-1
+// (same start value and comparison as A.8), plus the routing mask
+// mask[n][j*P + q] bit c = (Y[PC*j + c][q] == pool value) that the pool's
+// Backprop (A.9) would recompute from Y.
+template <int KS, int FT, int PC>
 __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
     ConvGeom g, const float *__restrict__ X, int xs,
     const float *__restrict__ K, int ks, const float *__restrict__ bias,
-    float *__restrict__ out, int os, int vec_ok, int dbg) {
+    float *__restrict__ out, int os, int vec_ok, int dbg,
+    float *__restrict__ pool, int ps, unsigned char *__restrict__ mask, int ms) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float *T = reinterpret_cast<float *>(smem);                 // [32][P]
   float *Bs = T + ((32 * g.P + 3) & ~3);                      // [128] bias
@@ -327,6 +334,29 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
         for (int e = (cnt & ~3) + tid; e < cnt; e += 256) dst[e] = T[e];
       } else {
         for (int e = tid; e < cnt; e += 256) dst[e] = T[e];
+      }
+      if constexpr (PC > 0) {  // rows % PC == 0 (host check)
+        const int cnt_p = rows / PC * g.P;
+        const int64_t pb = (int64_t)(gb * 32 / PC) * g.P;
+        float *pd = pool + (int64_t)n * ps + pb;
+        unsigned char *md = mask + (int64_t)n * ms + pb;
+        for (int e = tid; e < cnt_p; e += 256) {
+          uint32_t j, q;
+          g.div_P.divmod((uint32_t)e, j, q);
+          const float *t = T + (int)j * PC * g.P + (int)q;
+          float v[PC];
+#pragma unroll
+          for (int c = 0; c < PC; c++) v[c] = t[c * g.P];
+          float val = -1e20f;
+#pragma unroll
+          for (int c = 0; c < PC; c++)
+            if (val < v[c]) val = v[c];
+          unsigned m = 0;
+#pragma unroll
+          for (int c = 0; c < PC; c++) m |= (v[c] == val ? 1u : 0u) << c;
+          pd[e] = val;
+          md[e] = (unsigned char)m;
+        }
       }
       KCNN_TMARK(4)
       __syncthreads();
@@ -599,7 +629,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
     ConvGeom g, const float *__restrict__ X, int xs,
     const float *__restrict__ dY, int dys, const float *__restrict__ K, int ks,
     float *__restrict__ dX, int dxs, float *__restrict__ ws_part, int ZZ,
-    unsigned long long wg0, unsigned long long wg1, int dbg) {
+    unsigned long long wg0, unsigned long long wg1, int zsep, int dbg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int P = g.P;
   const int BUF = bwd_dma_buf_floats(P);
@@ -608,6 +638,10 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
   float *Xs = Sd0 + bwd_dma_sd_floats(P);              // [C][Wp][Hp] + {1}
   int *qtab = reinterpret_cast<int *>(Xs + ((g.C * (g.H + 2 * g.pad_h) *
                                               (g.W + 2 * g.pad_w) + 4) & ~3));
+  // zsep: Z [P][ZZ] has its own buffer, so frame n's col2im runs inside frame
+  // n+1's slab phases (next to the other waves' MFMAs) instead of in a
+  // barrier-bounded tail; else Z reuses the last slab's buffer
+  float *Zsep = reinterpret_cast<float *>(qtab + ((P + 31) & ~31));
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = lane & 31, h = lane >> 5;
@@ -663,7 +697,56 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
   _Pragma("unroll") for (int i = 0; i < BWD_MAXX; i++)                              \
     if (WG && tid + BWD_THREADS * i < CHW)                                         \
       xv[i] = X[(int64_t)(nn) * xs + tid + BWD_THREADS * i];
-  int cur = 0;
+  // X values (in xv) into the padded frame buffer
+#define KCNN_XCOMMIT()                                                               \
+  _Pragma("unroll") for (int i = 0; i < BWD_MAXX; i++) {                            \
+    const int e = tid + BWD_THREADS * i;                                             \
+    if (WG && e < CHW) {                                                             \
+      int slot = e;                                                                  \
+      if (!unpadded) {                                                               \
+        uint32_t c, q, wi, hi;                                                       \
+        g.div_HW.divmod((uint32_t)e, c, q);                                          \
+        g.div_H.divmod(q, wi, hi);                                                   \
+        slot = (int)c * Hp * Wp + ((int)wi + g.pad_w) * Hp + (int)hi + g.pad_h;      \
+      }                                                                              \
+      Xs[slot] = xv[i];                                                              \
+    }                                                                                \
+  }
+  // dX[nn][e] for e in [e0, e1) from Z: the col2im sum over the taps
+  const int khkw = g.kh * g.kw;
+  auto col2im = [&](const float *Zs, int nn, int e0, int e1) {
+    float *dxr = dX + (int64_t)nn * dxs;
+    for (int e = e0 + tid; e < e1; e += BWD_THREADS) {
+      uint32_t c, q, wi, hi;
+      g.div_HW.divmod((uint32_t)e, c, q);
+      g.div_H.divmod(q, wi, hi);
+      float sum = 0.0f;
+      for (int kxx = 0; kxx < g.kw; kxx++) {
+        const int px = (int)wi + g.pad_w - kxx;
+        if ((unsigned)px >= (unsigned)g.ow) continue;
+        const float *zr = Zs + (int64_t)(px * g.oh) * ZZ + (int)c * khkw + kxx * g.kh;
+        // 8 taps' reads in flight at once (out-of-range taps add +0)
+        for (int k0 = 0; k0 < g.kh; k0 += 8) {
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            const int py = (int)hi + g.pad_h - (k0 + u);
+            const bool ok = k0 + u < g.kh && (unsigned)py < (unsigned)g.oh;
+            v[u] = zr[ok ? py * ZZ + k0 + u : 0];
+            v[u] = ok ? v[u] : 0.0f;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; u++) sum += v[u];
+        }
+      }
+      dxr[e] = sum;
+    }
+  };
+  // deferred col2im: pieces in phases 0 .. npiece-1 of the next frame, all
+  // before that frame's last slab barrier (Z is rewritten after it)
+  const int npiece = NCH > 1 ? NCH - 1 : 1;
+  const int piece = (CHW + npiece - 1) / npiece;
+  int cur = 0, nprev = -1;
   long long tm[7] = {0, 0, 0, 0, 0, 0, 0};
   long long tprev = clock64();
 #define KCNN_TMARK(i) if (dbg & 16) { const long long tn = clock64(); tm[i] += tn - tprev; tprev = tn; }
@@ -671,22 +754,9 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
     dma_slab(blockIdx.x, 0, 0);
     KCNN_XLOAD(blockIdx.x)
   }
+  __syncthreads();  // zeroed border before the first commit
+  if (blockIdx.x < (unsigned)g.R) { KCNN_XCOMMIT() }
   for (int n = blockIdx.x; n < g.R; n += gridDim.x) {
-    __syncthreads();  // previous frame's Zs / Xs readers are done
-#pragma unroll
-    for (int i = 0; i < BWD_MAXX; i++) {
-      const int e = tid + BWD_THREADS * i;
-      if (WG && e < CHW) {
-        int slot = e;
-        if (!unpadded) {
-          uint32_t c, q, wi, hi;
-          g.div_HW.divmod((uint32_t)e, c, q);
-          g.div_H.divmod(q, wi, hi);
-          slot = (int)c * Hp * Wp + ((int)wi + g.pad_w) * Hp + (int)hi + g.pad_h;
-        }
-        Xs[slot] = xv[i];
-      }
-    }
     floatx16 zacc[BWD_MAXT];
 #pragma unroll
     for (int t = 0; t < BWD_MAXT; t++) zacc[t] = zero16();
@@ -701,14 +771,16 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
         const int nn = ch + 1 < NCH ? n : n + (int)gridDim.x;
         const int cc = ch + 1 < NCH ? ch + 1 : 0;
         if (nn < g.R) {
-          dma_slab(nn, cc, cur ^ 1);
+          if (!(dbg & 64)) dma_slab(nn, cc, cur ^ 1);
           if (ch + 1 == NCH) { KCNN_XLOAD(nn) }
         }
       }
+      if (DX && zsep && nprev >= 0 && ch < npiece && !(dbg & 4))
+        col2im(Zsep, nprev, ch * piece, min(CHW, (ch + 1) * piece));
       KCNN_TMARK(1)
       const float *Sd = Sd0 + cur * BUF;
       const float *wrow = Wt + (ch * 32 + h) * 32 + l;
-      if (DX) {  // Z[p][k] += dY[g][p] W[k][g] on the wave's own tiles
+      if (DX && !(dbg & 128)) {  // Z[p][k] += dY[g][p] W[k][g] on the wave's own tiles
 #pragma unroll
         for (int t = 0; t < BWD_MAXT; t++) {
           const int pt = wave + BWD_WAVES * t;
@@ -739,7 +811,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
       KCNN_TMARK(2)
 #pragma unroll
       for (int j = 0; j < 2; j++) {
-        if (!WG) break;
+        if (!WG || (dbg & 128)) break;
         const int pt = (int)(((j ? wg1 : wg0) >> (8 * wave)) & 0xff);
         if (pt == 0xff) continue;
         int pb = pt * 32;
@@ -769,24 +841,44 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
             __builtin_amdgcn_sched_barrier(0);
           }
         } else {
-          // B bit-masked to +0 past P (a row tail reads the next map's data)
+          // B bit-masked to +0 past P (a row tail reads the next map's
+          // data); batched like the full tile, or this wave's serialised
+          // reads hold every other wave at the next slab barrier
 #pragma unroll
-          for (int s = 0; s < 16; s++) {
-            const bool pin = ph + 2 * s < P;
-            const float bv = __uint_as_float(__float_as_uint(scol[2 * s]) &
-                                             (pin ? 0xffffffffu : 0u));
-            wacc[ch] = __builtin_amdgcn_mfma_f32_32x32x2f32(ain[j][s], bv, wacc[ch], 0, 0, 0);
+          for (int s0 = 0; s0 < 16; s0 += 8) {
+            float wb[8];
+#pragma unroll
+            for (int s = 0; s < 8; s++) wb[s] = scol[2 * (s0 + s)];
+#pragma unroll
+            for (int s = 0; s < 8; s++) {
+              const bool pin = ph + 2 * (s0 + s) < P;
+              wb[s] = __uint_as_float(__float_as_uint(wb[s]) & (pin ? 0xffffffffu : 0u));
+            }
+#pragma unroll
+            for (int s = 0; s < 8; s++)
+              wacc[ch] = __builtin_amdgcn_mfma_f32_32x32x2f32(ain[j][s0 + s], wb[s],
+                                                             wacc[ch], 0, 0, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // LDS reads
+            __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);  // VALU masks
+            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);  // MFMAs
+            __builtin_amdgcn_sched_barrier(0);
           }
         }
       }
       KCNN_TMARK(3)
       if (ch + 1 < NCH) cur ^= 1;
     }
+    // with one slab per frame, this frame's gather / col2im readers are
+    // only fenced by a barrier here
+    if (NCH == 1) __syncthreads();
     if (DX) {
-      __syncthreads();  // every wave is done with the last slab's buffer
-      float *Zs = Sd0 + cur * BUF;  // [P][ZZ] in the last slab's buffer
+      // zsep: Z's readers (the previous col2im) finished before the last slab
+      // barrier; else every wave must be done with the last slab's buffer
+      if (!zsep) __syncthreads();
+      float *Zs = zsep ? Zsep : Sd0 + cur * BUF;
 #pragma unroll
       for (int t = 0; t < BWD_MAXT; t++) {
+        if (dbg & 256) break;
         const int pt = wave + BWD_WAVES * t;
         if (pt >= ntile) continue;
 #pragma unroll
@@ -795,29 +887,22 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
           if (pl < P && l < g.Kdim) Zs[pl * ZZ + l] = zacc[t][r];
         }
       }
-      __syncthreads();
-      float *dxr = dX + (int64_t)n * dxs;
-      const int khkw = g.kh * g.kw;
-      if (!(dbg & 4))
-      for (int e = tid; e < CHW; e += BWD_THREADS) {
-        uint32_t c, q, wi, hi;
-        g.div_HW.divmod((uint32_t)e, c, q);
-        g.div_H.divmod(q, wi, hi);
-        float sum = 0.0f;
-        for (int kxx = 0; kxx < g.kw; kxx++) {
-          const int px = (int)wi + g.pad_w - kxx;
-          if ((unsigned)px >= (unsigned)g.ow) continue;
-          const float *zr = Zs + (int64_t)(px * g.oh) * ZZ + (int)c * khkw + kxx * g.kh;
-          for (int kyy = 0; kyy < g.kh; kyy++) {
-            const int py = (int)hi + g.pad_h - kyy;
-            if ((unsigned)py < (unsigned)g.oh) sum += zr[py * ZZ + kyy];
-          }
-        }
-        dxr[e] = sum;
+      if (zsep) {
+        nprev = n;
+      } else {
+        __syncthreads();
+        if (!(dbg & 4)) col2im(Zs, n, 0, CHW);
+        __syncthreads();  // Zs (slab buffer) readers done before its next DMA
       }
     }
+    // the next frame's X: this frame's gather (phase 0) is behind a barrier
+    if (WG && n + (int)gridDim.x < g.R) { KCNN_XCOMMIT() }
     KCNN_TMARK(4)
     cur ^= 1;  // the next frame's first slab is in the other buffer
+  }
+  if (DX && zsep && nprev >= 0) {
+    __syncthreads();
+    col2im(Zsep, nprev, 0, CHW);
   }
   KCNN_TMARK(5)
   if ((dbg & 16) && blockIdx.x == 0 && lane == 0)
@@ -825,6 +910,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
            wave, tm[0], tm[1], tm[2], tm[3], tm[4], tm[5], tm[6]);
 #undef KCNN_TMARK
 #undef KCNN_XLOAD
+#undef KCNN_XCOMMIT
   if (!WG) return;
   const int E = (g.Kdim + 1) * g.G;
   float *dst = ws_part + (int64_t)blockIdx.x * E;
@@ -1072,8 +1158,8 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
       const int ksn = (g.Kdim + 1) / 2;
       const unsigned grid = frame_grid(g, 2);
 #define KCNN_FWD_REGS(KS_)                                                         \
-  hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3>), dim3(grid), dim3(256), lds, st, \
-                     g, X, xs, K, ks, bias, out, os, vec_ok, dbg)
+  hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, 0>), dim3(grid), dim3(256), lds, st, \
+                     g, X, xs, K, ks, bias, out, os, vec_ok, dbg, nullptr, 0, nullptr, 0)
       static const int dbg = env_int("KCNN_FWD_DEBUG", 0);
       if (ksn <= 4) KCNN_FWD_REGS(4);
       else if (ksn <= 8) KCNN_FWD_REGS(8);
@@ -1110,6 +1196,41 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
     hipLaunchKernelGGL(conv_fwd_frame_kernel<1>, dim3(grid), dim3(256), lds, st,
                        g, X, xs, K, ks, bias, out, os, Kpad, Gp);
   }
+  return (int)hipGetLastError();
+}
+
+// Forward + channel-only max pool (pool 1 x 1 x pc) in one pass; -1 when the
+// geometry is outside the register-resident kernel's limits.
+int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
+                             const float *K, int ks, const float *bias,
+                             float *out, int os, float *pool, int ps,
+                             unsigned char *mask, int ms, int pc,
+                             hipStream_t st) {
+  if (!(pc == 2 || pc == 4 || pc == 8) || g.G % pc != 0) return -1;
+  if (g.Kdim > 32 || g.G > 128 || g.P < 16 || g.P > 4 * 32 * 3 ||
+      g.C * g.HW > 256 * 8)
+    return -1;
+  const size_t lds = (size_t)((32 * g.P + 3) & ~3) * 4 + 128 * 4 + 32 * 8 +
+                     (size_t)g.C * g.HW * 4;
+  if (lds > (size_t)kFrameLdsMax) return -1;
+  const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0);
+  const int ksn = (g.Kdim + 1) / 2;
+  const unsigned grid = frame_grid(g, 2);
+#define KCNN_FWD_POOL(KS_, PC_)                                                       \
+  hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_>), dim3(grid), dim3(256), lds, \
+                     st, g, X, xs, K, ks, bias, out, os, vec_ok, 0, pool, ps, mask, ms)
+#define KCNN_FWD_POOL_KS(PC_)                     \
+  do {                                            \
+    if (ksn <= 4) KCNN_FWD_POOL(4, PC_);          \
+    else if (ksn <= 8) KCNN_FWD_POOL(8, PC_);     \
+    else if (ksn <= 12) KCNN_FWD_POOL(12, PC_);   \
+    else KCNN_FWD_POOL(16, PC_);                  \
+  } while (0)
+  if (pc == 2) KCNN_FWD_POOL_KS(2);
+  else if (pc == 4) KCNN_FWD_POOL_KS(4);
+  else KCNN_FWD_POOL_KS(8);
+#undef KCNN_FWD_POOL_KS
+#undef KCNN_FWD_POOL
   return (int)hipGetLastError();
 }
 
@@ -1231,12 +1352,17 @@ int kcnn_conv_bwd_frame(const ConvGeom &g, const float *X, int xs,
       nw[best]++;
     }
   }
-  const size_t lds3 = bwd_dma_lds(g);
+  size_t lds3 = bwd_dma_lds(g);
+  // a separate Z buffer when it fits (deferred col2im, see the kernel)
+  const size_t zbytes = (size_t)g.P * ZZ * 4;
+  const int zsep = dX != nullptr && lds3 + zbytes <= (size_t)kBwdLdsMax &&
+                   !(bdbg & 32);
+  if (zsep) lds3 += zbytes;
   if (variant == 3 && g.C * g.HW <= BWD_THREADS * BWD_MAXX &&
       lds3 <= (size_t)kBwdLdsMax) {
 #define KCNN_BWD3(NCH, DXB, WGB)                                                     \
   hipLaunchKernelGGL((conv_bwd_dma_kernel<NCH, DXB, WGB>), dim3(S), dim3(BWD_THREADS), \
-                     lds3, st, g, X, xs, dY, dys, K, ks, dX, dxs, part, ZZ, wg[0], wg[1], bdbg)
+                     lds3, st, g, X, xs, dY, dys, K, ks, dX, dxs, part, ZZ, wg[0], wg[1], zsep, bdbg)
 #define KCNN_BWD3_NCH(NCH)                                  \
   do {                                                      \
     if (dX && gW) KCNN_BWD3(NCH, true, true);               \

@@ -373,6 +373,34 @@ size_t hipF_conv2d_workspace_bytes(MatrixDim in_dim, int in_height,
   return plan_igemm(g).ws_bytes;
 }
 
+// Conv2D(concat) + bias + channel-only Maxpool_prop in one pass (see
+// include/cnsl-hip-kernels.h).  Returns -1 (nothing launched) when the
+// geometry is not covered, so the caller runs the two components unfused.
+int hipF_conv2d_maxpool(const float *in, MatrixDim in_dim, int in_height,
+                        int in_width, int in_channel, int pad_h, int pad_w,
+                        const float *kernel, MatrixDim kernel_dim,
+                        int kernel_height, int kernel_width, int group,
+                        const float *bias, float *out, MatrixDim out_dim,
+                        float *pool, MatrixDim pool_dim, unsigned char *mask,
+                        int mask_stride, int pool_channel_dim,
+                        kcnn_stream_t stream) {
+  ConvGeom g = make_geom(in_dim.rows, in_height, in_width, in_channel, pad_h,
+                         pad_w, kernel_height, kernel_width, group);
+  if (g.oh <= 0 || g.ow <= 0 || in_dim.cols != g.HW * in_channel ||
+      kernel_dim.rows != g.Kdim || kernel_dim.cols != group ||
+      out_dim.rows != g.R || out_dim.cols != g.P * group ||
+      pool_channel_dim <= 0 || pool_dim.rows != g.R ||
+      pool_dim.cols * pool_channel_dim != out_dim.cols ||
+      mask_stride < pool_dim.cols)
+    return (int)hipErrorInvalidValue;
+  if (g.R == 0) return 0;
+  if (g.M >= ((int64_t)1 << 31)) return -1;
+  return kcnn_conv_fwd_frame_pool(g, in, in_dim.stride, kernel, kernel_dim.stride,
+                                  bias, out, out_dim.stride, pool, pool_dim.stride,
+                                  mask, mask_stride, pool_channel_dim,
+                                  kcnn::as_stream(stream)) == 0 ? 0 : -1;
+}
+
 int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
                 int in_channel, int pad_h, int pad_w, const float *kernel,
                 MatrixDim kernel_dim, int kernel_height, int kernel_width,

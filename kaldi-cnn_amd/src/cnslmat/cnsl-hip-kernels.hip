@@ -438,6 +438,39 @@ __global__ __launch_bounds__(256) void maxpool_direct_backprop_kernel(
   }
 }
 
+// Backprop of the channel-only pool from the routing mask saved by the fused
+// forward (hipF_conv2d_maxpool): dX[(PC j + c) plane + q] = bit c of
+// mask[j plane + q] ? dP[j plane + q] : 0 -- the same values A.9 produces
+// from in_value == out_value, read from 1 byte instead of PC + 1 floats.
+template <int PC>
+__global__ __launch_bounds__(256) void maxpool_mask_backprop_kernel(
+    const unsigned char *__restrict__ mask, int64_t ms,
+    const float *__restrict__ dy, int64_t dys, float *__restrict__ dx,
+    int64_t dxs, uint32_t total, FastDiv div_cols, FastDiv div_plane, int plane) {
+  const uint32_t base = blockIdx.x * (256u * kPoolDirectOut) + threadIdx.x;
+  unsigned mv[kPoolDirectOut];
+  float dv[kPoolDirectOut];
+  int64_t off[kPoolDirectOut];
+#pragma unroll
+  for (int t = 0; t < kPoolDirectOut; t++) {
+    const uint32_t e = base + 256u * t;
+    const uint32_t ec = e < total ? e : total - 1;
+    uint32_t row, j, k, q;
+    div_cols.divmod(ec, row, j);
+    div_plane.divmod(j, k, q);
+    mv[t] = mask[(int64_t)row * ms + j];
+    dv[t] = dy[(int64_t)row * dys + j];
+    off[t] = e < total ? (int64_t)row * dxs + (int64_t)k * PC * plane + q : -1;
+  }
+#pragma unroll
+  for (int t = 0; t < kPoolDirectOut; t++) {
+    if (off[t] < 0) continue;
+#pragma unroll
+    for (int c = 0; c < PC; c++)
+      dx[off[t] + c * plane] = (mv[t] >> c) & 1u ? dv[t] : 0.0f;
+  }
+}
+
 // Writes every element of the group (routed derivative or 0): the fused
 // in_deriv->Resize(kSetZero) of MaxpoolComponent::Backprop (:889).
 __global__ __launch_bounds__(256) void maxpool_group_backprop_kernel(
@@ -632,6 +665,34 @@ int hipF_mod_permute_row(const float *in, MatrixDim in_dim, float *out,
   ModPermuteRow f{in, in_dim, out, out_dim, block_size,
                   FastDiv((uint32_t)in_channel)};
   return launch_elem2d(in_dim.rows, in_dim.cols, f, kcnn::as_stream(stream));
+}
+
+int hipF_maxpool_backprop_mask(const unsigned char *mask, int mask_stride,
+                               const float *out_deriv, MatrixDim out_deriv_dim,
+                               float *in_deriv, MatrixDim in_deriv_dim,
+                               int in_height, int in_width,
+                               int pool_channel_dim, kcnn_stream_t stream) {
+  const int plane = in_height * in_width;
+  const int pc = pool_channel_dim;
+  if (plane <= 0 || !(pc == 2 || pc == 4 || pc == 8) ||
+      out_deriv_dim.cols % plane != 0 || mask_stride < out_deriv_dim.cols ||
+      in_deriv_dim.rows != out_deriv_dim.rows ||
+      in_deriv_dim.cols != out_deriv_dim.cols * pc)
+    return (int)hipErrorInvalidValue;
+  const int64_t nout = (int64_t)out_deriv_dim.rows * out_deriv_dim.cols;
+  if (nout == 0) return 0;
+  if (nout >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  const unsigned blocks =
+      (unsigned)((nout + 256 * kPoolDirectOut - 1) / (256 * kPoolDirectOut));
+  auto kern = pc == 2 ? maxpool_mask_backprop_kernel<2>
+              : pc == 4 ? maxpool_mask_backprop_kernel<4>
+                        : maxpool_mask_backprop_kernel<8>;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, kcnn::as_stream(stream), mask,
+                     (int64_t)mask_stride, out_deriv, (int64_t)out_deriv_dim.stride,
+                     in_deriv, (int64_t)in_deriv_dim.stride, (uint32_t)nout,
+                     FastDiv((uint32_t)out_deriv_dim.cols), FastDiv((uint32_t)plane),
+                     plane);
+  return kcnn::launch_status();
 }
 
 int hipF_mod_permute_channels(float *comp, MatrixDim comp_dim, float *container,

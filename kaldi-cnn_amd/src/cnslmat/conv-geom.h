@@ -50,6 +50,11 @@ __device__ __forceinline__ int mfma32_row(int r, int lane) {
 int kcnn_conv_fwd_frame(const kcnn::ConvGeom &g, const float *X, int xs,
                         const float *K, int ks, const float *bias, float *out,
                         int os, hipStream_t st);
+int kcnn_conv_fwd_frame_pool(const kcnn::ConvGeom &g, const float *X, int xs,
+                             const float *K, int ks, const float *bias,
+                             float *out, int os, float *pool, int ps,
+                             unsigned char *mask, int ms, int pc,
+                             hipStream_t st);
 int kcnn_conv_dgrad_frame(const kcnn::ConvGeom &g, const float *dY, int dys,
                           const float *K, int ks, float *dX, int dxs,
                           hipStream_t st);

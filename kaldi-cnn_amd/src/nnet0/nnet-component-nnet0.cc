@@ -221,6 +221,32 @@ void ConvolutionComponent::Propagate(const ChunkInfo &in_info,
                              ws, ws_bytes, S()));
 }
 
+bool ConvolutionComponent::PropagateMaxpool(const CuMatrixBase<BaseFloat> &in,
+                                            CuMatrixBase<BaseFloat> *out,
+                                            const MaxpoolComponent &pool,
+                                            CuMatrixBase<BaseFloat> *pool_out,
+                                            unsigned char *mask,
+                                            int32 mask_stride) const {
+  const int32 pc = pool.FusableChannelPool();
+  if (LiteralPath() || pc == 0 || mask == NULL) return false;
+  if (pool.In_height() != out_height_ || pool.In_width() != out_width_ ||
+      pool.In_channels() != group_ || pool.InputDim() != OutputDim())
+    return false;
+  KALDI_ASSERT(in.NumCols() == InputDim());
+  KALDI_ASSERT(out->NumRows() == in.NumRows() && out->NumCols() == OutputDim());
+  KALDI_ASSERT(pool_out->NumRows() == in.NumRows() &&
+               pool_out->NumCols() == pool.OutputDim());
+  CuProfileScope prof("ConvolutionComponent::PropagateMaxpool");
+  const int rc = hipF_conv2d_maxpool(
+      in.Data(), in.Dim(), in_height_, in_width_, in_channel_, in_pad_height_,
+      in_pad_width_, linear_params_.Data(), linear_params_.Dim(), kernel_height_,
+      kernel_width_, group_, bias_params_.Data(), out->Data(), out->Dim(),
+      pool_out->Data(), pool_out->Dim(), mask, mask_stride, pc, S());
+  if (rc < 0) return false;
+  CNSL_SAFE_CALL(rc);
+  return true;
+}
+
 void ConvolutionComponent::PropagateLiteral(const ChunkInfo &in_info,
                                             const CuMatrixBase<BaseFloat> &in,
                                             CuMatrixBase<BaseFloat> *out) const {
@@ -769,6 +795,27 @@ void MaxpoolComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
       out_deriv.Data(), out_deriv.Dim(), in_deriv->Data(), in_deriv->Dim(),
       in_height_, in_width_, pool_height_dim_, pool_width_dim_,
       pool_channel_dim_, mode, 1, S()));
+}
+
+int32 MaxpoolComponent::FusableChannelPool() const {
+  const int32 pc = pool_channel_dim_;
+  if (overlap_ || overlap2D_ || pool_height_dim_ != 1 || pool_width_dim_ != 1)
+    return 0;
+  if (!(pc == 2 || pc == 4 || pc == 8) || in_channel_ % pc != 0) return 0;
+  return output_dim_ * pc == input_dim_ ? pc : 0;
+}
+
+void MaxpoolComponent::BackpropFromMask(const unsigned char *mask,
+                                        int32 mask_stride,
+                                        const CuMatrixBase<BaseFloat> &out_deriv,
+                                        CuMatrix<BaseFloat> *in_deriv) const {
+  const int32 pc = FusableChannelPool();
+  KALDI_ASSERT(pc > 0 && mask != NULL && out_deriv.NumCols() == output_dim_);
+  in_deriv->Resize(out_deriv.NumRows(), input_dim_, kUndefined);  // every element written
+  CuProfileScope prof("MaxpoolComponent::BackpropFromMask");
+  CNSL_SAFE_CALL(hipF_maxpool_backprop_mask(
+      mask, mask_stride, out_deriv.Data(), out_deriv.Dim(), in_deriv->Data(),
+      in_deriv->Dim(), in_height_, in_width_, pc, S()));
 }
 
 // :894-934

@@ -31,6 +31,8 @@ namespace nnet0 {
 void SetLiteralPath(bool literal);
 bool LiteralPath();
 
+class MaxpoolComponent;
+
 class ConvolutionComponent : public nnet2::UpdatableComponent {
  public:
   explicit ConvolutionComponent(const ConvolutionComponent &other);
@@ -118,6 +120,17 @@ class ConvolutionComponent : public nnet2::UpdatableComponent {
                                 const CuMatrixBase<BaseFloat> &out_deriv,
                                 CuMatrix<BaseFloat> *in_deriv, BaseFloat *grad) const;
 
+  // Propagate and the Propagate of the channel-only MaxpoolComponent `pool`
+  // that consumes `out`, in one pass (hipF_conv2d_maxpool), also writing the
+  // pool's routing mask [rows x mask_stride bytes] for
+  // MaxpoolComponent::BackpropFromMask.  Returns false, having done nothing,
+  // when the pair is not covered (literal path, other pool shapes, ...).
+  bool PropagateMaxpool(const CuMatrixBase<BaseFloat> &in,
+                        CuMatrixBase<BaseFloat> *out,
+                        const MaxpoolComponent &pool,
+                        CuMatrixBase<BaseFloat> *pool_out, unsigned char *mask,
+                        int32 mask_stride) const;
+
   // Mutable parameter access for hosts (C-ABI).
   CuMatrix<BaseFloat> &LinearParamsMutable() { return linear_params_; }
   CuVector<BaseFloat> &BiasParamsMutable() { return bias_params_; }
@@ -197,6 +210,20 @@ class MaxpoolComponent : public nnet2::Component {
   virtual void Read(std::istream &is, bool binary);
   virtual void Write(std::ostream &os, bool binary) const;
   virtual std::string Info() const;
+
+  inline int32 In_height() const { return in_height_; }
+  inline int32 In_width() const { return in_width_; }
+  inline int32 In_channels() const { return in_channel_; }
+  // pool_channel_dim when the pool is channel-only (1 x 1 x pc, no overlap,
+  // pc in {2, 4, 8}): the shape the convolution forward can fuse; else 0.
+  int32 FusableChannelPool() const;
+  // Backprop (:882-892) from the routing mask written by
+  // ConvolutionComponent::PropagateMaxpool for the same minibatch: identical
+  // in_deriv to Backprop(in_value, out_value, out_deriv, ...), without
+  // reading in_value / out_value.
+  void BackpropFromMask(const unsigned char *mask, int32 mask_stride,
+                        const CuMatrixBase<BaseFloat> &out_deriv,
+                        CuMatrix<BaseFloat> *in_deriv) const;
 
  protected:
   int32 input_dim_;

@@ -61,6 +61,10 @@ def main():
                            conv_b),
         "pool_fwd": (lambda: pool.Propagate(y, p), bench.POOL_FWD_BYTES * B),
         "pool_bwd": (lambda: pool.Backprop(y, p, dp, dyp), bench.POOL_BWD_BYTES * B),
+        # HBM reference points of the same size (torch kernels)
+        "fill_y": (lambda: dyp.fill_(1.0), dyp.numel() * 4),
+        "copy_y": (lambda: dyp.copy_(y), 2 * dyp.numel() * 4),
+        "sum_y": (lambda: y.sum(), y.numel() * 4),
     }
     only = [t for t in a.only.split(",") if t]
     for name, (fn, byts) in tests.items():

@@ -19,18 +19,21 @@ import os
 import re
 import shutil
 
-# hot-path kernel -> bench.py kernel-table key
-HOT = {
-    "conv_bwd_dma_kernel": "conv_bwd_fused",
-    "conv_bwd_frame_kernel": "conv_bwd_fused",
-    "conv_fwd_regs_kernel": "conv_fwd",
-    "maxpool_group_prop_kernel": "maxpool_fwd",
-    "maxpool_group_backprop_kernel": "maxpool_bwd",
-    "conv_fwd_slab_kernel": "conv_fwd",
-    "conv_fwd_frame_kernel": "conv_fwd",
-    "MaxpoolProp": "maxpool_fwd",
-    "MaxpoolBackprop": "maxpool_bwd",
-}
+# hot-path kernel (regex on the demangled name) -> bench.py kernel-table key;
+# first match wins
+HOT = [
+    (r"conv_bwd_dma_kernel", "conv_bwd_fused"),
+    (r"conv_bwd_frame_kernel", "conv_bwd_fused"),
+    (r"conv_fwd_regs_kernel<\d+, \d+, [248]>", "conv_fwd_maxpool"),
+    (r"conv_fwd_regs_kernel", "conv_fwd"),
+    (r"conv_fwd_slab_kernel", "conv_fwd"),
+    (r"conv_fwd_frame_kernel", "conv_fwd"),
+    (r"maxpool_mask_backprop_kernel", "maxpool_bwd_mask"),
+    (r"maxpool_(group|direct)_prop_kernel", "maxpool_fwd"),
+    (r"maxpool_(group|direct)_backprop_kernel", "maxpool_bwd"),
+    (r"MaxpoolProp", "maxpool_fwd"),
+    (r"MaxpoolBackprop", "maxpool_bwd"),
+]
 
 
 def short(name):
@@ -40,8 +43,8 @@ def short(name):
 
 
 def kernel_key(name):
-    for k, v in HOT.items():
-        if k in name:
+    for pat, v in HOT:
+        if re.search(pat, name):
             return v
     return None
 

@@ -1,0 +1,126 @@
+"""GPU tests of the kcnn_nnet runtime (the NnetUpdater-style component stack,
+include/kcnn.h kcnn_nnet_*), in particular its Conv -> channel-only Maxpool
+fusion: ConvolutionComponent::PropagateMaxpool writes Y, the pooled output
+and the pool's routing mask in one pass, and the pool's Backprop runs from
+the mask (MaxpoolComponent::BackpropFromMask).
+
+The fusion is an exact transformation, so every output, input derivative and
+updated parameter must be bit-identical with fusion on and off; the pool
+output and the routed derivative are also checked bitwise against the oracle
+(A.8 / A.9) applied to the GPU's own Y.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from _util import assert_same, dev, host, randn, rng
+
+pytestmark = pytest.mark.gpu
+
+
+def stack(H, W, C, kh, kw, G, pc, fc_out, ph=0, pw=0):
+    oh, ow = H + 2 * ph - kh + 1, W + 2 * pw - kw + 1
+    return "\n".join([
+        f"ConvolutionComponent in-height={H} in-width={W} in-channel={C} "
+        f"in-pad-height={ph} in-pad-width={pw} kernel-height={kh} kernel-width={kw} "
+        f"stride=1 group={G} out-height={oh} out-width={ow} learning-rate=0.02 "
+        f"param-stddev=0.1 bias-stddev=0.5",
+        f"MaxpoolComponent in-height={oh} in-width={ow} in-channel={G} "
+        f"pool-height-dim=1 pool-width-dim=1 pool-channel-dim={pc}",
+        f"FullyConnectedComponent input-dim={oh * ow * G // pc} output-dim={fc_out} "
+        f"learning-rate=0.02 param-stddev=0.05 bias-stddev=1",
+    ]), (oh, ow)
+
+
+STACKS = {
+    # name: (H, W, C, kh, kw, G, pc, fc_out, pad_h, pad_w)
+    "c2": (40, 11, 3, 8, 1, 128, 4, 64, 0, 0),      # BASELINE c2 shape
+    "pc2_G96": (12, 7, 2, 3, 2, 96, 2, 32, 0, 0),
+    "pc8_G64": (9, 5, 1, 2, 2, 64, 8, 16, 0, 0),
+    "G48_pad": (6, 5, 2, 3, 3, 48, 4, 8, 1, 1),     # last filter group of 16 maps
+    "pc3_unfused": (8, 6, 1, 3, 1, 30, 3, 8, 0, 0),  # not fusable: plain path
+}
+
+
+def build(kc, cfg, seed, ties=False):
+    H, W, C, kh, kw, G, pc, fo, ph, pw = cfg
+    text, _ = stack(H, W, C, kh, kw, G, pc, fo, ph, pw)
+    net = kc.Nnet(text)
+    conv, pool, fc = net.components
+    r = rng(seed)
+    Wc = randn(r, (kh * kw * C, G), 0.1)
+    bc = randn(r, (G,), 0.5)
+    if ties:  # the maps of every pool group identical: 4-way (pc-way) ties
+        for j in range(G // pc):
+            Wc[:, j * pc:(j + 1) * pc] = Wc[:, j * pc:j * pc + 1]
+            bc[j * pc:(j + 1) * pc] = bc[j * pc]
+    conv.SetParam(kc.PARAM_LINEAR, dev(Wc))
+    conv.SetParam(kc.PARAM_BIAS, dev(bc))
+    conv.SetParam(kc.PARAM_PREV_GRAD, dev(randn(r, (kh * kw * C, G), 0.01)))
+    fc.SetParam(kc.PARAM_LINEAR, dev(randn(r, (fo, fc.InputDim()), 0.05)))
+    return net
+
+
+def run(kc, cfg, fused, ties=False, N=37, mode=0):
+    kc.set_fusion(fused)
+    try:
+        net = build(kc, cfg, seed=11, ties=ties)
+        r = rng(3)
+        x = dev(randn(r, (N, net.components[0].InputDim())))
+        dy = dev(randn(r, (N, net.components[2].OutputDim()), 0.1))
+        net.Propagate(x)
+        outs = [host(net.Output(i)) for i in range(3)]
+        grads = None
+        if mode == 0:
+            net.Backprop(dy)
+        else:
+            import torch
+            grads = [torch.zeros(c.NumGradientParams(), device="cuda")
+                     if k != 1 else None for k, c in enumerate(net.components)]
+            for i in (2, 1, 0):
+                net.BackpropComponent(i, dy, mode=1, grad=grads[i], skip_first_dx=False)
+            grads = [host(g[None, :]) if g is not None else None for g in grads]
+        derivs = [host(net.InputDeriv(i)) for i in range(3)]
+        params = [host(c.GetParam(w)) for c in (net.components[0], net.components[2])
+                  for w in (kc.PARAM_LINEAR, kc.PARAM_BIAS)]
+        return outs, derivs, params, grads
+    finally:
+        kc.set_fusion(True)
+
+
+@pytest.mark.parametrize("name", sorted(STACKS))
+@pytest.mark.parametrize("ties", [False, True])
+def test_fusion_is_exact(kc, name, ties):
+    cfg = STACKS[name]
+    a = run(kc, cfg, fused=True, ties=ties)
+    b = run(kc, cfg, fused=False, ties=ties)
+    for k, (u, v) in enumerate(zip(a[0], b[0])):
+        assert_same(u, v, f"{name} output {k}")
+    for k, (u, v) in enumerate(zip(a[1], b[1])):
+        assert_same(u, v, f"{name} input deriv {k}")
+    for k, (u, v) in enumerate(zip(a[2], b[2])):
+        assert_same(u, v, f"{name} param {k}")
+
+
+@pytest.mark.parametrize("name", ["c2", "pc2_G96", "pc8_G64"])
+def test_fusion_exact_gradient_mode(kc, name):
+    a = run(kc, STACKS[name], fused=True, mode=1)
+    b = run(kc, STACKS[name], fused=False, mode=1)
+    for k, (u, v) in enumerate(zip(a[3], b[3])):
+        if u is not None:
+            assert_same(u, v, f"{name} grad {k}")
+    assert_same(a[1][0], b[1][0], f"{name} conv input deriv")
+
+
+@pytest.mark.parametrize("ties", [False, True])
+def test_fused_pool_matches_oracle(kc, ties):
+    H, W, C, kh, kw, G, pc, fo, ph, pw = STACKS["c2"]
+    outs, derivs, _, _ = run(kc, STACKS["c2"], fused=True, ties=ties)
+    oh, ow = H - kh + 1, W - kw + 1
+    y, p = outs[0], outs[1]
+    assert_same(p, O.maxpool_prop(y, oh, ow, 1, 1, pc, p.shape[1]), "fused Maxpool_prop")
+    dp = derivs[2]
+    assert_same(derivs[1], O.maxpool_backprop(y, p, dp, oh, ow, 1, 1, pc),
+                "mask-routed Maxpool_backprop")
+    if ties:  # every map of a group is a maximum: all receive the derivative
+        assert (derivs[1] != 0).mean() > 0.99 * (dp != 0).mean()

@@ -71,8 +71,16 @@ __global__ __launch_bounds__(256) void kl_colsum_partial(
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
   int64_t r1 = r0 + rows_per_slab;
   if (r1 > md.rows) r1 = md.rows;
+  // 8 rows' loads in flight per step (a plain loop waits on each load);
+  // rows past the slab add +0, the order of the sum is unchanged
   float s = 0.0f;
-  for (int64_t r = r0; r < r1; r++) s += M[r * md.stride + j];
+  for (int64_t r = r0; r < r1; r += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) v[u] = r + u < r1 ? M[(r + u) * md.stride + j] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < 8; u++) s += v[u];
+  }
   part[(int64_t)blockIdx.y * md.cols + j] = s;
 }
 // pass 2 -- v = beta*v + alpha*sum_slabs (slab order fixed).
@@ -82,7 +90,13 @@ __global__ __launch_bounds__(256) void kl_colsum_final(
   const int j = blockIdx.x * 256 + threadIdx.x;
   if (j >= cols) return;
   float s = 0.0f;
-  for (int b = 0; b < slabs; b++) s += part[(int64_t)b * cols + j];
+  for (int b = 0; b < slabs; b += 8) {
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) t[u] = b + u < slabs ? part[(int64_t)(b + u) * cols + j] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < 8; u++) s += t[u];
+  }
   v[j] = beta == 0.0f ? alpha * s : beta * v[j] + alpha * s;
 }
 
@@ -92,7 +106,13 @@ struct SumPartialsF {
   __device__ void operator()(int64_t i, int j) const {
     const float *q = p + i * n + j;
     float acc = q[0];
-    for (int s = 1; s < S; s++) acc += q[(int64_t)s * pstride];
+    for (int s0 = 1; s0 < S; s0 += 4) {  // 4 partials' loads in flight
+      float t[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) t[u] = s0 + u < S ? q[(int64_t)(s0 + u) * pstride] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < 4; u++) acc += t[u];
+    }
     float *y = c + i * cs + j;
     *y = beta == 0.0f ? acc : acc + beta * *y;
   }

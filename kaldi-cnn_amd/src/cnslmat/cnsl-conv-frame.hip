@@ -687,18 +687,22 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
   const int nchunk = BUF / 256;  // 1-KiB chunks per slab
   const int slab = 32 * P;
 
-  // LDS-DMA of slab (n, c) into buffer b: wave w moves chunks w, w+8, ...;
-  // lanes past the slab re-read its last float4 (kept inside the matrix;
-  // the LDS tail they fill is never read)
+  // LDS-DMA of slab (n, c) into buffer b: wave w moves chunks w, w+8, ...
+  // by buffer_load ... lds -- the chunk offset is a scalar (soffset), the
+  // lane's 16 B a constant voffset, so the issue loop costs no VALU work.
+  // The descriptor spans the frame's row: a last chunk running past the
+  // row reads zeros (hardware range check); past the slab it reads the
+  // next slab's first values into an LDS tail that is never read.
+  const uint32_t row_bytes = (uint32_t)g.G * (uint32_t)P * 4u;
   auto dma_slab = [&](int n, int c, int b, int ln) {
-    const float *src = dY + (int64_t)((dbg & 2) ? 0 : n) * dys + (int64_t)c * slab;
+    const float *base = dY + (int64_t)((dbg & 2) ? 0 : n) * dys;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)row_bytes, 0x00020000);
     float *dst = Sd0 + b * BUF;
-    for (int q = wave; q < nchunk; q += BWD_WAVES) {
-      int off = q * 256 + ln * 4;
-      off = off < slab - 4 ? off : slab - 4;
-      __builtin_amdgcn_global_load_lds((glob_void_t *)(src + off),
-                                       (lds_void_t *)(dst + q * 256), 16, 0, 0);
-    }
+    for (int q = wave; q < nchunk; q += BWD_WAVES)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t *)(dst + q * 256), 16,
+                                               (uint32_t)ln * 16u,
+                                               (uint32_t)(c * slab + q * 256) * 4u, 0, 0);
   };
 
   floatx16 wacc[NCH];
@@ -764,15 +768,17 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
     for (int kx = xlo; kx <= xlo + nx; kx++) {  // kw = 1: one pass
       const int zk = c2b[i] - kx * zax;
       for (int k0 = 0; k0 < g.kh; k0 += 8) {
+        // the 8 taps' reads first (one wait), then the masked sum.  A tap
+        // outside the map reads another position's Z (or, off the LDS
+        // allocation, 0) and is dropped by the mask: no address select
         float v[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {  // 8 taps' reads in flight; +0 outside
-          const bool ok = (unsigned)(k0 + u - ylo) <= (unsigned)ny;
-          v[u] = Zs[ok ? zk - (k0 + u) * zby : 0];
-          v[u] = ok ? v[u] : 0.0f;
-        }
+        for (int u = 0; u < 8; u++) v[u] = Zs[zk - (k0 + u) * zby];
 #pragma unroll
-        for (int u = 0; u < 8; u++) sum += v[u];
+        for (int u = 0; u < 8; u++)
+          sum += (unsigned)(k0 + u - ylo) <= (unsigned)ny ? v[u] : 0.0f;
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // the reads
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     dX[(int64_t)nn * dxs + e] = sum;

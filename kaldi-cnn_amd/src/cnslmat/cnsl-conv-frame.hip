@@ -896,10 +896,13 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
 #pragma unroll
         for (int s = 0; s < 16; s++) wb[s] = scol[2 * s];
         if (pb + 32 > P) {  // wave-uniform
+          // k-step s covers positions ph + 2s, ph = pb + h: with lim =
+          // P - pb - 2s (uniform) both halves are in for lim >= 2, only
+          // h = 0 for lim == 1, neither below
 #pragma unroll
           for (int s = 0; s < 16; s++) {
-            const bool pin = ph + 2 * s < P;
-            wb[s] = __uint_as_float(__float_as_uint(wb[s]) & (pin ? 0xffffffffu : 0u));
+            const int lim = P - pb - 2 * s;
+            if (lim <= 0 || (lim == 1 && h_f)) wb[s] = 0.0f;
           }
         }
 #pragma unroll

@@ -1,12 +1,12 @@
 set -o pipefail
 O=gpurun_out/pmc20
-mkdir -p $O
+rm -rf $O; mkdir -p $O
 export TMPDIR=/tmp
 i=0
-for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_BUSY_CYCLES" \
-           "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU" \
-           "SQ_VALU_MFMA_COEXEC_CYCLES SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
+for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+           "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM" \
+           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
   i=$((i+1))
-  timeout -k 10 200 rocprofv3 --pmc $set --output-format csv -d $O/p$i -o run -- python3 scripts/microbench.py --reps 3 --only bwd_fused,fwd > $O/p$i.log 2>&1 || { echo "rc=$? set $i" >> $O/err.log; exit 5; }
+  timeout -k 10 200 rocprofv3 --pmc $set --output-format csv -d $O/p$i -o run -- python3 scripts/microbench.py --reps 3 --only bwd_fused > $O/p$i.log 2>&1 || { echo "rc=$? set $i" >> $O/err.log; exit 5; }
 done
 echo done

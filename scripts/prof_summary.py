@@ -69,13 +69,14 @@ def main():
     ap.add_argument("out")
     ap.add_argument("tag")
     ap.add_argument("--steps", type=int, default=25, help="bench steps profiled (warmup+timed)")
+    ap.add_argument("--cmd", default="python bench.py --steps 20 --warmup 5 --no-cpu-baseline",
+                    help="the profiled command, for the report header")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     stats = os.path.join(a.run, "prof", "run_kernel_stats.csv")
     rows = list(csv.DictReader(open(stats)))
     shutil.copy(stats, os.path.join(a.out, f"{a.tag}_kernel_stats.csv"))
-    lines = [f"# {a.tag}: rocprofv3 --kernel-trace --stats, `python bench.py --steps 20 "
-             f"--warmup 5 --no-cpu-baseline` (c2, N=4096, 1x MI355X)", "",
+    lines = [f"# {a.tag}: rocprofv3 --kernel-trace --stats, `{a.cmd}` (c2, N=4096, 1x MI355X)", "",
              "| kernel | calls | avg us | total ms | % |", "|---|---:|---:|---:|---:|"]
     for r in rows:
         lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} "
@@ -104,7 +105,11 @@ def main():
     if traffic:
         for v in traffic.values():
             v["hbm_bytes_per_launch"] = round(v["hbm_bytes_per_launch"])
-        json.dump(traffic, open(os.path.join(a.out, "pmc_traffic.json"), "w"), indent=1)
+            v["run"] = a.tag
+        path = os.path.join(a.out, "pmc_traffic.json")
+        merged = json.load(open(path)) if os.path.exists(path) else {}
+        merged.update(traffic)  # kernels of several runs (fused / unfused)
+        json.dump(merged, open(path, "w"), indent=1)
     print("\n".join(lines))
 
 

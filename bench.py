@@ -60,6 +60,45 @@ def stack_config():
     ])
 
 
+# BASELINE configs[4] / SURVEY 8d c5: the deep stack, (H, W, C, kh, kw, G, pad)
+# convolutions and (ph, pw, pc) pools, FC(1792 -> 1024).  A --config option;
+# the default line stays c2 (the configuration BASELINE's metric is quoted on).
+C5_LAYERS = [
+    ("conv", (40, 11, 3, 8, 1, 256, 0)),
+    ("pool", (3, 1, 4)),
+    ("conv", (11, 11, 64, 4, 3, 256, 0)),
+    ("conv", (8, 9, 256, 3, 3, 256, 1)),
+    ("pool", (2, 1, 4)),
+    ("conv", (4, 9, 64, 4, 3, 256, 0)),
+]
+
+
+def c5_config():
+    lines, shape = [], None
+    flop = 0
+    for kind, a in C5_LAYERS:
+        if kind == "conv":
+            h, w, c, kh, kw, g, pad = a
+            oh, ow = h + 2 * pad - kh + 1, w + 2 * pad - kw + 1
+            lines.append(
+                f"ConvolutionComponent in-height={h} in-width={w} in-channel={c} "
+                f"in-pad-height={pad} in-pad-width={pad} kernel-height={kh} "
+                f"kernel-width={kw} stride=1 group={g} out-height={oh} out-width={ow} "
+                f"learning-rate=0.02 param-stddev=0.01 bias-stddev=0.5")
+            flop += 2 * oh * ow * g * kh * kw * c
+            shape = (oh, ow, g)
+        else:
+            ph, pw, pc = a
+            oh, ow, g = shape
+            lines.append(f"MaxpoolComponent in-height={oh} in-width={ow} in-channel={g} "
+                         f"pool-height-dim={ph} pool-width-dim={pw} pool-channel-dim={pc}")
+            shape = (oh // ph, ow // pw, g // pc)
+    fin = shape[0] * shape[1] * shape[2]
+    lines.append(f"FullyConnectedComponent input-dim={fin} output-dim={FC_OUT} "
+                 f"learning-rate=0.02 param-stddev=0.01 bias-stddev=1")
+    return "\n".join(lines), flop, fin
+
+
 def parse_profile(text):
     out = {}
     for line in text.strip().splitlines():
@@ -117,6 +156,8 @@ def main():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--no-fusion", action="store_true",
                     help="run Conv and Maxpool as separate components")
+    ap.add_argument("--config", default="c2", choices=["c2", "c5"],
+                    help="c2 (default, BASELINE's metric) or the c5 deep stack")
     args = ap.parse_args()
 
     import torch
@@ -138,8 +179,11 @@ def main():
     kcnn.set_randn_seed(20261015)  # identical initial params on every replica
 
     B = args.frames_per_gpu
-    net = kcnn.Nnet(stack_config())
-    conv, pool, fc = net.components
+    if args.config == "c5":
+        text, c5_flop, _ = c5_config()
+        net = kcnn.Nnet(text)
+    else:
+        net = kcnn.Nnet(stack_config())
     gen = torch.Generator(device="cuda")
     gen.manual_seed(20261015 + rank)  # each rank its own shard of frames
     x = torch.randn((B, H * W * C), generator=gen, device="cuda")
@@ -181,6 +225,39 @@ def main():
     frames = B * world * args.steps
     value = frames / elapsed
     ms_per_step = elapsed / args.steps * 1e3
+
+    if args.config == "c5":
+        # per-scope milliseconds per step (all layers of a kind together)
+        scopes = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items())}
+        conv_ms = sum(v for k, v in scopes.items() if k.startswith("ConvolutionComponent"))
+        conv_flop = 3 * c5_flop * B  # fwd + dgrad + wgrad per frame
+        if rank == 0:
+            result = {
+                "metric": "frames/sec fwd+bwd, c5 deep Conv/Maxpool stack (BASELINE configs[4])",
+                "value": round(value, 1), "unit": "frames/sec", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                "data": "synthetic N(0,1) frames",
+                "config": {"workload": "c5: C1(40x11x3,8x1,256) P1(3x1x4) C2(11x11x64,4x3,256) "
+                                       "C3(8x9x256,3x3,pad1,256) P2(2x1x4) C4(4x9x64,4x3,256) "
+                                       "FC(1792->1024)", "frames_per_gpu": B,
+                           "parallelism": f"dp{world}"},
+                "conv": {"ms_per_step": round(conv_ms, 4),
+                         "TFLOP/s": round(conv_flop / conv_ms / 1e9, 2) if conv_ms else None,
+                         "mfma_frac": round(conv_flop / conv_ms / 1e9 / PEAK_FP32_MFMA_TFLOPS, 4)
+                         if conv_ms else None},
+                "scopes_ms_per_step": scopes,
+            }
+            line = json.dumps(result)
+            print(line, flush=True)
+            if args.json_out:
+                with open(args.json_out, "w") as f:
+                    f.write(line + "\n")
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     # Per-kernel averages (HIP events around each launch, timed region).
     def avg(key):

@@ -641,7 +641,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
     ConvGeom g, const float *__restrict__ X, int xs,
     const float *__restrict__ dY, int dys, const float *__restrict__ K, int ks,
     float *__restrict__ dX, int dxs, float *__restrict__ ws_part, int ZZ,
-    unsigned long long wg0, unsigned long long wg1, int zsep, int dbg) {
+    unsigned long long wg0, unsigned long long wg1, int zsep, int dx_acc, int dbg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int P = g.P;
   const int BUF = bwd_dma_buf_floats(P);
@@ -781,7 +781,8 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    dX[(int64_t)nn * dxs + e] = sum;
+    float *d = dX + (int64_t)nn * dxs + e;
+    *d = dx_acc ? *d + sum : sum;  // dx_acc: a later filter chunk (G > 128)
   };
   // deferred col2im: pieces in phases 0 .. npiece-1 of the next frame, all
   // before that frame's last slab barrier (Z is rewritten after it)
@@ -1197,6 +1198,17 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
                         const float *K, int ks, const float *bias, float *out,
                         int os, hipStream_t st) {
   if (g.Kdim > 64 || g.P < 16) return -1;
+  if (g.G > 128 && g.G % 32 == 0 && g.Kdim <= 32) {
+    // filter chunks of 128: each is a column range of W, b and Y
+    for (int g0 = 0; g0 < g.G; g0 += 128) {
+      ConvGeom gc = g;
+      gc.G = g.G - g0 < 128 ? g.G - g0 : 128;
+      const int rc = kcnn_conv_fwd_frame(gc, X, xs, K + g0, ks, bias ? bias + g0 : nullptr,
+                                         out + (int64_t)g0 * g.P, os, st);
+      if (rc) return g0 == 0 ? rc : (rc < 0 ? (int)hipErrorLaunchFailure : rc);
+    }
+    return 0;
+  }
   const int Kpad = (g.Kdim + 1) & ~1;
   static const int variant = env_int("KCNN_FWD_VARIANT", 2);
   if (variant == 2 && g.Kdim <= 32 && g.G <= 128 && g.P <= 4 * 32 * 3 &&
@@ -1257,6 +1269,18 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
                              unsigned char *mask, int ms, int pc,
                              hipStream_t st) {
   if (!(pc == 2 || pc == 4 || pc == 8) || g.G % pc != 0) return -1;
+  if (g.G > 128 && g.G % 32 == 0) {  // filter chunks of 128 (pool groups never straddle)
+    for (int g0 = 0; g0 < g.G; g0 += 128) {
+      ConvGeom gc = g;
+      gc.G = g.G - g0 < 128 ? g.G - g0 : 128;
+      const int64_t pofs = (int64_t)(g0 / pc) * g.P;
+      const int rc = kcnn_conv_fwd_frame_pool(gc, X, xs, K + g0, ks, bias ? bias + g0 : nullptr,
+                                              out + (int64_t)g0 * g.P, os, pool + pofs, ps,
+                                              mask + pofs, ms, pc, st);
+      if (rc) return g0 == 0 ? rc : (rc < 0 ? (int)hipErrorLaunchFailure : rc);
+    }
+    return 0;
+  }
   if (g.Kdim > 32 || g.G > 128 || g.P < 16 || g.P > 4 * 32 * 3 ||
       g.C * g.HW > 256 * 8)
     return -1;
@@ -1348,6 +1372,11 @@ static size_t bwd_lds(const ConvGeom &g, int SP) {
 static int bwd_sp(const ConvGeom &g) { return g.P; }  // P odd: conflict-free slab reads
 
 size_t kcnn_conv_bwd_frame_ws(const ConvGeom &g) {
+  if (g.G > 128 && g.G % 32 == 0) {  // chunks of 128 filters share the workspace
+    ConvGeom gc = g;
+    gc.G = 128;
+    return kcnn_conv_bwd_frame_ws(gc);
+  }
   if (g.Kdim > 31 || g.G % 32 != 0 || g.G > 128 || g.G == 0) return 0;
   if (g.P < 16 || g.P > 32 * BWD_WAVES * BWD_MAXT || 8 * g.P > BWD_THREADS * BWD_MAXV)
     return 0;
@@ -1362,12 +1391,11 @@ static size_t bwd_dma_lds(const ConvGeom &g) {
           (size_t)((g.P + 31) & ~31)) * 4;
 }
 
-// dX (nullable) and/or gW, gb (nullable) from one pass over dY.  gW == NULL
-// runs the data gradient only and needs no workspace.
-int kcnn_conv_bwd_frame(const ConvGeom &g, const float *X, int xs,
-                        const float *dY, int dys, const float *K, int ks,
-                        float *dX, int dxs, float *gW, int gws, float *gb,
-                        void *ws, size_t ws_bytes, hipStream_t st) {
+// One filter chunk (G <= 128) of kcnn_conv_bwd_frame; dx_acc adds to dX.
+static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
+                           const float *dY, int dys, const float *K, int ks,
+                           float *dX, int dxs, float *gW, int gws, float *gb,
+                           void *ws, size_t ws_bytes, int dx_acc, hipStream_t st) {
   static const int enabled = env_int("KCNN_FUSED_BWD", 1);
   static const int variant = env_int("KCNN_BWD_VARIANT", 3);  // 1: register-staged
   static const int bdbg = env_int("KCNN_BWD_DEBUG", 0);
@@ -1412,7 +1440,7 @@ int kcnn_conv_bwd_frame(const ConvGeom &g, const float *X, int xs,
       lds3 <= (size_t)kBwdLdsMax) {
 #define KCNN_BWD3(NCH, DXB, WGB)                                                     \
   hipLaunchKernelGGL((conv_bwd_dma_kernel<NCH, DXB, WGB>), dim3(S), dim3(BWD_THREADS), \
-                     lds3, st, g, X, xs, dY, dys, K, ks, dX, dxs, part, ZZ, wg[0], wg[1], zsep, bdbg)
+                     lds3, st, g, X, xs, dY, dys, K, ks, dX, dxs, part, ZZ, wg[0], wg[1], zsep, dx_acc, bdbg)
 #define KCNN_BWD3_NCH(NCH)                                  \
   do {                                                      \
     if (dX && gW) KCNN_BWD3(NCH, true, true);               \
@@ -1428,8 +1456,8 @@ int kcnn_conv_bwd_frame(const ConvGeom &g, const float *X, int xs,
 #undef KCNN_BWD3_NCH
 #undef KCNN_BWD3
   } else {
-    // register-staged variant: needs the gradient outputs
-    if (gW == nullptr) return -1;
+    // register-staged variant: needs the gradient outputs, writes dX
+    if (gW == nullptr || dx_acc) return -1;
     const int SP = bwd_sp(g);
     const size_t lds = bwd_lds(g, SP);
     if (lds > (size_t)kFrameLdsMax) return -1;
@@ -1461,6 +1489,36 @@ int kcnn_conv_bwd_frame(const ConvGeom &g, const float *X, int xs,
   hipLaunchKernelGGL(reduce_pass2, dim3((E + 255) / 256), dim3(256), 0, st, tmp,
                      Q, E, g.Kdim * g.G, g.G, 0, gW, gws, gb);
   return (int)hipGetLastError();
+}
+
+// dX (nullable) and/or gW, gb (nullable) from one pass over dY.  gW == NULL
+// runs the data gradient only and needs no workspace.  G > 128 (c5's
+// 256-filter layers) runs in chunks of 128 filters: dY columns, W columns
+// and gW/gb columns of a chunk are plain offsets into the same matrices, and
+// the chunks after the first add their data gradient into dX (fixed order).
+int kcnn_conv_bwd_frame(const ConvGeom &g, const float *X, int xs,
+                        const float *dY, int dys, const float *K, int ks,
+                        float *dX, int dxs, float *gW, int gws, float *gb,
+                        void *ws, size_t ws_bytes, hipStream_t st) {
+  if (g.G <= 128)
+    return bwd_frame_chunk(g, X, xs, dY, dys, K, ks, dX, dxs, gW, gws, gb, ws,
+                           ws_bytes, 0, st);
+  if (g.G % 32 != 0 || (int64_t)g.G * g.P * 4 % 16 != 0) return -1;
+  static const int variant = env_int("KCNN_BWD_VARIANT", 3);
+  if (variant != 3 && dX != nullptr) return -1;  // chunking needs dX accumulation
+  for (int g0 = 0; g0 < g.G; g0 += 128) {
+    ConvGeom gc = g;
+    gc.G = g.G - g0 < 128 ? g.G - g0 : 128;
+    const int rc = bwd_frame_chunk(
+        gc, X, xs, dY + (int64_t)g0 * g.P, dys, K + g0, ks, dX, dxs,
+        gW ? gW + g0 : nullptr, gws, gb ? gb + g0 : nullptr, ws, ws_bytes, g0 > 0, st);
+    if (rc) {
+      // only the first chunk may decline (nothing written yet); a later
+      // failure is a launch error
+      return g0 == 0 ? rc : (rc < 0 ? (int)hipErrorLaunchFailure : rc);
+    }
+  }
+  return 0;
 }
 
 size_t kcnn_reduce_splits_ws(int S, int E) {

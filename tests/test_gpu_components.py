@@ -27,6 +27,7 @@ CONVS = {
     "c5_C4": (4, 9, 64, 4, 3, 256, 0, 0),               # pad-kernel branch
     "small_pad": (5, 6, 2, 3, 3, 5, 1, 2),
     "tiny": (3, 4, 1, 2, 2, 3, 0, 0),
+    "c5_C1_G256": (40, 11, 3, 8, 1, 256, 0, 0),         # c5 C1: 128-filter chunks
 }
 
 
@@ -107,6 +108,8 @@ FUSED_BWD = {
     "P512": ((35, 16, 1, 4, 1, 32, 0, 0), 3),                # max positions
     "P16": ((5, 5, 2, 2, 2, 128, 0, 0), 4),                  # min positions
     "oh1": ((8, 40, 1, 8, 3, 64, 0, 0), 5),                  # oh = 1
+    "c5_C1_G256": ((40, 11, 3, 8, 1, 256, 0, 0), 6),         # 2 chunks of 128 filters
+    "G224": ((9, 7, 2, 2, 3, 224, 0, 0), 5),                 # chunks 128 + 96
 }
 
 

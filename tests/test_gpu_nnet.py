@@ -39,6 +39,7 @@ STACKS = {
     "pc8_G64": (9, 5, 1, 2, 2, 64, 8, 16, 0, 0),
     "G48_pad": (6, 5, 2, 3, 3, 48, 4, 8, 1, 1),     # last filter group of 16 maps
     "pc3_unfused": (8, 6, 1, 3, 1, 30, 3, 8, 0, 0),  # not fusable: plain path
+    "G256_pc4": (12, 6, 2, 4, 2, 256, 4, 16, 0, 0),  # 2 filter chunks of 128
 }
 
 

@@ -27,6 +27,7 @@
 // kernel (TpBlock + TpInsideBlock + Conv2D + ModPermuteRow + AddRowSumMat,
 // nnet-component-nnet0.cc:745-775) reading X and dY once each.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include "conv-geom.h"
 
@@ -133,7 +134,170 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(
   }
 }
 
-// Fixed-order reduction of split-K partials [S][G][M] + the store epilogue.
+// ---------------------------------------------------------------------------
+// Implicit GEMM, variant 2 (large kernel volumes: c5 C2-C4, the flipped-
+// kernel data gradient).  out[g][m] = sum_k W[k][g] im2col(X)[k][m] with
+// m = n*P + p.  Block = 4 waves, each owning a 64 (g) x 64 (m) block of four
+// 32x32 accumulators; WGG waves along g (tile 64*WGG x 64*(4/WGG)).  K steps
+// of 16 are double-buffered in LDS with one barrier per step; the next
+// step's operands are in flight (registers) while the current one runs.
+//   * VALU work is budgeted: on gfx950 it does not execute beside the fp32
+//     MFMAs, so every VALU op is MFMA idle time.  The im2col row offset of
+//     k (c*H*W + kx*H + ky) and the tap are wave-uniform (scalar ALU); per
+//     gathered element one add builds the offset, and for padded maps a
+//     per-lane bitmask of the taps that fall inside the map (kh*kw <= 32)
+//     drops the others (buffer loads make any stray offset safe).
+//   * Operands per MFMA: one LDS read (A: W tile, B: im2col tile).
+template <int WGG, bool PADDED, int IG2_BK>
+__global__ __launch_bounds__(256) void conv_igemm2_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ Kmat,
+    int ks, const float *__restrict__ bias, float *__restrict__ out, int os, int dbg) {
+  constexpr int WGM = 4 / WGG;
+  constexpr int BG = 64 * WGG, BM = 64 * WGM;
+  constexpr int ANF = IG2_BK * BG / 256;  // A floats per thread per K step (4 or 8)
+  constexpr int BNF = IG2_BK * BM / 256;  // B floats per thread per K step (8 or 16)
+  __shared__ __attribute__((aligned(16))) float As[2][IG2_BK][BG];
+  __shared__ __attribute__((aligned(16))) float Bs[2][IG2_BK][BM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wg = wave % WGG, wm = wave / WGG;
+  const int l = lane & 31, h = lane >> 5;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int g0 = blockIdx.y * BG;
+  const int nk = (g.Kdim + IG2_BK - 1) / IG2_BK;
+
+  // A (W rows, float4 along g): thread -> (row ar + 16/ANF*i?, cols ag..ag+3)
+  constexpr int A_TPR = BG / 4;            // threads per A row
+  const int ar = tid / A_TPR, ag = (tid % A_TPR) * 4;  // rows ar, ar + 256/A_TPR
+  constexpr int A_RSTEP = 256 / A_TPR;
+  // B (im2col): thread's column m, rows br + B_RSTEP * j (br wave-uniform)
+  const int bm = tid % BM;
+  const int br = __builtin_amdgcn_readfirstlane(tid / BM);
+  constexpr int B_RSTEP = 256 / BM;
+  const int64_t mcol = m0 + bm;
+  const bool mvalid = mcol < g.M;
+  int xoff = 0;                  // frame row + (px, py) part of the offset
+  unsigned tapmask = 0xffffffffu;  // taps inside the map (PADDED)
+  {
+    uint32_t n = 0, p = 0, px = 0, py = 0;
+    if (mvalid) {
+      g.div_P.divmod((uint32_t)mcol, n, p);
+      g.div_oh.divmod(p, px, py);
+    }
+    xoff = (int)n * xs + ((int)px - g.pad_w) * g.H + (int)py - g.pad_h;
+    if (PADDED) {
+      tapmask = 0;
+      for (int kx = 0; kx < g.kw; kx++)
+        for (int ky = 0; ky < g.kh; ky++) {
+          const int xx = (int)px + kx - g.pad_w, yy = (int)py + ky - g.pad_h;
+          if ((unsigned)xx < (unsigned)g.W && (unsigned)yy < (unsigned)g.H)
+            tapmask |= 1u << (kx * g.kh + ky);
+        }
+    }
+    if (!mvalid) tapmask = 0;
+  }
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)X, (short)0, (int)((int64_t)g.R * xs * 4 < 0x7fffffff ? (int64_t)g.R * xs * 4 : 0x7fffffff),
+      0x00020000);
+
+  // W rows through a descriptor too: rows past Kdim read 0 (range check)
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)Kmat, (short)0, g.Kdim * ks * 4, 0x00020000);
+  if (!PADDED) tapmask = mvalid ? 0xffffffffu : 0u;
+  float4 areg[ANF / 4];
+  float breg[BNF];
+  unsigned bok = 0;  // bit j: element j of breg is inside the map
+  // branch-free: every load issues back to back; nothing reads a loaded
+  // value before store(), so the loads land while the MFMAs run
+  auto load = [&](int kt) {
+    if (dbg & 1) return;  // timing experiments: no operand loads
+    const int kb = kt * IG2_BK;
+#pragma unroll
+    for (int i = 0; i < ANF / 4; i++) {
+      const int k = kb + ar + A_RSTEP * i;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+          wr, (unsigned)(k * ks + g0 + ag) * 4u, 0, 0);
+      areg[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]),
+                            __uint_as_float(v[2]), __uint_as_float(v[3]));
+    }
+#pragma unroll
+    for (int j = 0; j < BNF; j++) {
+      const int k = kb + br + B_RSTEP * j;  // wave-uniform: scalar index math
+      const int kc = k < g.Kdim ? k : g.Kdim - 1;
+      uint32_t c, r, kx, ky;
+      g.div_khkw.divmod((uint32_t)kc, c, r);
+      g.div_kh.divmod(r, kx, ky);
+      const int koff = (int)c * g.HW + (int)kx * g.H + (int)ky;
+      const int tap = (int)(kx * g.kh + ky);
+      const unsigned vm = k < g.Kdim ? tapmask : 0u;
+      breg[j] = __uint_as_float(
+          __builtin_amdgcn_raw_buffer_load_b32(xr, (unsigned)(xoff + koff) * 4u, 0, 0));
+      bok = j == 0 ? ((vm >> tap) & 1u) : bok | (((vm >> tap) & 1u) << j);
+    }
+  };
+  auto store = [&](int b) {
+    if (dbg & 2) return;  // timing experiments: no LDS stores
+#pragma unroll
+    for (int i = 0; i < ANF / 4; i++)
+      *reinterpret_cast<float4 *>(&As[b][ar + A_RSTEP * i][ag]) = areg[i];
+#pragma unroll
+    for (int j = 0; j < BNF; j++)
+      Bs[b][br + B_RSTEP * j][bm] = (bok >> j) & 1u ? breg[j] : 0.0f;
+  };
+
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[a][b][i] = 0.0f;
+
+  load(0);
+  store(0);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nk; kt++) {
+    if (kt + 1 < nk) load(kt + 1);
+#pragma unroll
+    for (int s = 0; s < IG2_BK / 2; s++) {
+      const float a0 = As[cur][2 * s + h][wg * 64 + l];
+      const float a1 = As[cur][2 * s + h][wg * 64 + 32 + l];
+      const float b0 = Bs[cur][2 * s + h][wm * 64 + l];
+      const float b1 = Bs[cur][2 * s + h][wm * 64 + 32 + l];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // Epilogue: D[g][m], row (r&3) + 8(r>>2) + 4h, column l (concat layout).
+#pragma unroll
+  for (int b = 0; b < 2; b++) {
+    const int64_t mm = m0 + wm * 64 + 32 * b + l;
+    if (mm >= g.M) continue;
+    uint32_t on, op;
+    g.div_P.divmod((uint32_t)mm, on, op);
+    float *orow = out + (int64_t)on * os + op;
+#pragma unroll
+    for (int a = 0; a < 2; a++) {
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int gg = g0 + wg * 64 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (gg >= g.G) continue;
+        float v = acc[a][b][r];
+        if (bias) v = v + bias[gg];
+        orow[(int64_t)gg * g.P] = v;
+      }
+    }
+  }
+}
+
+// Fixed-order reduction of split-K partials [S][G][M] + the store epilogue.// Fixed-order reduction of split-K partials [S][G][M] + the store epilogue.
 __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(
     ConvGeom g, const float *__restrict__ ws, int S,
     const float *__restrict__ bias, float *__restrict__ out, int os,
@@ -435,6 +599,46 @@ int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
     else if (g.G <= 4) KCNN_DIRECT(4);
     else KCNN_DIRECT(8);
 #undef KCNN_DIRECT
+    return kcnn::launch_status();
+  }
+
+  // implicit GEMM v2: concat layout, X addressable with 32-bit offsets, tap
+  // masks for padded maps need kh*kw <= 32
+  static const int ig2 = [] {
+    const char *e = getenv("KCNN_IGEMM2");
+    return e && *e ? atoi(e) : 1;
+  }();
+  const bool padded = g.pad_h > 0 || g.pad_w > 0;
+  const int wgg = g.G > 64 ? 2 : 1;
+  if (ig2 && concat && (int64_t)g.R * in_dim.stride * 4 < ((int64_t)1 << 31) &&
+      (int64_t)g.Kdim * kernel_dim.stride * 4 < ((int64_t)1 << 31) &&
+      g.G % (64 * wgg) == 0 && kernel_dim.stride % 4 == 0 &&
+      (uintptr_t)kernel % 16 == 0 && (!padded || g.kh * g.kw <= 32)) {
+    const int bg = 64 * wgg, bm = 64 * (4 / wgg);
+    dim3 grid2((unsigned)((g.M + bm - 1) / bm), (unsigned)((g.G + bg - 1) / bg));
+  static const int ig2dbg = [] {
+    const char *e = getenv("KCNN_IGEMM2_DEBUG");
+    return e && *e ? atoi(e) : 0;
+  }();
+  static const int ig2bk = [] {
+    const char *e = getenv("KCNN_IGEMM2_BK");
+    return e && *e ? atoi(e) : 16;
+  }();
+#define KCNN_IG2(W_, P_)                                                                  \
+  do {                                                                                    \
+    if (ig2bk == 32)                                                                      \
+      hipLaunchKernelGGL((conv_igemm2_kernel<W_, P_, 32>), grid2, dim3(256), 0, st, g, in, \
+                         in_dim.stride, kernel, kernel_dim.stride, bias, out, out_dim.stride, ig2dbg); \
+    else                                                                                  \
+      hipLaunchKernelGGL((conv_igemm2_kernel<W_, P_, 16>), grid2, dim3(256), 0, st, g, in, \
+                         in_dim.stride, kernel, kernel_dim.stride, bias, out, out_dim.stride, ig2dbg); \
+  } while (0)
+    if (wgg == 2) {
+      if (padded) KCNN_IG2(2, true); else KCNN_IG2(2, false);
+    } else {
+      if (padded) KCNN_IG2(1, true); else KCNN_IG2(1, false);
+    }
+#undef KCNN_IG2
     return kcnn::launch_status();
   }
 

@@ -465,6 +465,185 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Weight gradient v2, for long kernels (c5 C2-C4, nnet.config layer 1):
+//   D[g][k] = sum_t dY[n][g*P + p] * B[t][k],   t = (n, p) over the block's
+//   frames, B = im2col(X) (Appendix A.12), block tile 128 (g) x 128 (k),
+//   each wave 64 x 64 (four 32x32 accumulators) as in conv_igemm2_kernel.
+// The reduction walks the block's frames in chunks of 32 positions, and lane
+// tl of every chunk always stands for the same position (p = 32c + tl, or
+// frame offset tl / P and p = tl % P when P <= 16).  Its map offset and its
+// tap-validity mask are therefore computed once; per step only the frame
+// base moves, and that lives in the (scalar) buffer descriptors, whose range
+// also drops the frames past the split.  Per gathered X element: one add
+// for the offset and two ops for the tap mask (padded maps only); per dY
+// element one add.  Steps are double-buffered in LDS, one barrier each.
+// Bias gradient: the k-tile-0 blocks also sum their dY values (fixed order).
+// Partials go to ws[split][e] (e = g*Kdim + k, then G bias entries) and are
+// reduced in a fixed order (kcnn_reduce_splits_wgrad): deterministic.
+constexpr int W2_BG = 128, W2_BK = 128, W2_LD = 129;
+
+template <int NCH, bool PADDED>
+__global__ __launch_bounds__(256, 2) void conv_wgrad2_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ dY,
+    int dys, float *__restrict__ ws, int fps, int fpc, int ktiles, int nblocks) {
+  __shared__ float As[2][32][W2_LD];  // dY tile [t][g]
+  __shared__ float Bs[2][32][W2_LD];  // im2col tile [t][k]
+  // XCD-aware order: hardware places block b on XCD b % 8; logical ids are
+  // contiguous per XCD, so the tiles of one split (same frames) share an L2.
+  const int nb8 = (nblocks + 7) >> 3;
+  const int bid = (int)(blockIdx.x & 7) * nb8 + (int)(blockIdx.x >> 3);
+  if (bid >= nblocks) return;
+  const int ntiles = ktiles * (g.G / W2_BG);
+  const int split = bid / ntiles, tile = bid - split * ntiles;
+  const int k0 = (tile % ktiles) * W2_BK, g0 = (tile / ktiles) * W2_BG;
+  const int nbeg = split * fps;
+  const int nend = min(g.R, nbeg + fps);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wg = wave & 1, wk = wave >> 1;
+  const int l = lane & 31, h = lane >> 5;
+  const int tl = tid & 31, rs = tid >> 5;  // t-lane; row sub-index 0..7
+
+  // This thread's im2col columns k = k0 + rs + 8j (fixed for the kernel).
+  unsigned koff4[16];
+  uint32_t tapj[PADDED ? 16 : 1];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const int k = k0 + rs + 8 * j;
+    uint32_t c = 0, r = 0, kx = 0, ky = 0;
+    if (k < g.Kdim) {
+      g.div_khkw.divmod((uint32_t)k, c, r);
+      g.div_kh.divmod(r, kx, ky);
+    }
+    koff4[j] = k < g.Kdim ? (unsigned)(((int)c * g.HW + (int)kx * g.H + (int)ky) * 4)
+                          : 0x40000000u;
+    if (PADDED) tapj[j] = (kx << 8) | ky;
+  }
+  // This lane's position in each chunk; bad[c] bit j: column j's tap falls
+  // outside the map at this position (padded maps).
+  unsigned voffA[NCH], lpos4[NCH], bad[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; c++) {
+    int fo = 0, p = 32 * c + tl;
+    if (fpc > 1) { fo = tl / g.P; p = tl - fo * g.P; }
+    const bool valid = fpc > 1 ? fo < fpc : p < g.P;
+    uint32_t px = 0, py = 0;
+    if (valid) g.div_oh.divmod((uint32_t)p, px, py);
+    voffA[c] = valid ? (unsigned)((fo * dys + rs * g.P + p) * 4) : 0x80000000u;
+    const int lp = fo * xs + ((int)px - g.pad_w) * g.H + (int)py - g.pad_h;
+    lpos4[c] = valid ? (unsigned)(lp * 4) : 0x40000000u;
+    unsigned b = 0;
+    if (PADDED) {
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int xx = (int)px + (int)(tapj[j] >> 8) - g.pad_w;
+        const int yy = (int)py + (int)(tapj[j] & 255) - g.pad_h;
+        if ((unsigned)xx >= (unsigned)g.W || (unsigned)yy >= (unsigned)g.H) b |= 1u << j;
+      }
+    }
+    bad[c] = b;
+  }
+
+  float areg[16], breg[16], bacc[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) bacc[j] = 0.0f;
+  const bool do_bias = k0 == 0;
+  // dY row offsets are wave-uniform: they go in soffset (valid lanes stay
+  // inside the descriptor's range, masked lanes' voffset alone exceeds it).
+  const unsigned gstep4 = (unsigned)(8 * g.P * 4), gbase4 = (unsigned)(g0 * g.P * 4);
+
+  // All loads issue back to back; nothing reads them before store().
+  auto load = [&](int n, int c) {
+    const int nf = min(fpc, nend - n);
+    const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(dY + (int64_t)n * dys), (short)0, nf * dys * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(X + (int64_t)n * xs), (short)0, nf * xs * 4, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+      areg[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          ar, voffA[c], (int)(gbase4 + gstep4 * j), 0));  // row part: soffset
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      unsigned off = lpos4[c] + koff4[j];
+      if (PADDED) off |= ((bad[c] >> j) & 1u) << 31;
+      breg[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(br, off, 0, 0));
+    }
+  };
+  auto store = [&](int b) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) As[b][tl][rs + 8 * j] = areg[j];
+#pragma unroll
+    for (int j = 0; j < 16; j++) Bs[b][tl][rs + 8 * j] = breg[j];
+    if (do_bias) {
+#pragma unroll
+      for (int j = 0; j < 16; j++) bacc[j] += areg[j];
+    }
+  };
+
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[a][b][i] = 0.0f;
+
+  load(nbeg, 0);
+  store(0);
+  __syncthreads();
+  int cur = 0;
+  for (int n = nbeg; n < nend; n += fpc) {
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      const bool more = c + 1 < NCH || n + fpc < nend;
+      if (more) load(c + 1 < NCH ? n : n + fpc, c + 1 < NCH ? c + 1 : 0);
+#pragma unroll
+      for (int s = 0; s < 16; s++) {
+        const float a0 = As[cur][2 * s + h][wg * 64 + l];
+        const float a1 = As[cur][2 * s + h][wg * 64 + 32 + l];
+        const float b0 = Bs[cur][2 * s + h][wk * 64 + l];
+        const float b1 = Bs[cur][2 * s + h][wk * 64 + 32 + l];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+      }
+      if (more) store(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  // Partials of this split: weights (lanes along k: 128-B runs), bias.
+  const int64_t E = (int64_t)g.G * g.Kdim + g.G;
+  float *wsp = ws + (int64_t)split * E;
+#pragma unroll
+  for (int b = 0; b < 2; b++) {
+    const int kk = k0 + wk * 64 + 32 * b + l;
+    if (kk >= g.Kdim) continue;
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int gg = g0 + wg * 64 + 32 * a + kcnn::mfma32_row(r, lane);
+        wsp[(int64_t)gg * g.Kdim + kk] = acc[a][b][r];
+      }
+  }
+  if (do_bias) {
+    float *red = &As[0][0][0];  // [128][33]
+#pragma unroll
+    for (int j = 0; j < 16; j++) red[(rs + 8 * j) * 33 + tl] = bacc[j];
+    __syncthreads();
+    if (tid < W2_BG) {
+      float s = 0.0f;
+      for (int i = 0; i < 32; i++) s += red[tid * 33 + i];
+      wsp[(int64_t)g.G * g.Kdim + g0 + tid] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Host-side planning.
 struct IgemmPlan {
   int S, k_per_split;
@@ -520,6 +699,71 @@ WgradPlan plan_wgrad(const ConvGeom &g) {
   const size_t E = (size_t)g.G * g.Kdim + g.G;
   pl.ws_bytes = (size_t)S * E * sizeof(float) + kcnn_reduce_splits_ws((int)S, (int)E);
   return pl;
+}
+
+struct Wgrad2Plan {
+  int S, fps, fpc, nch, ktiles, nblocks;
+  size_t ws_bytes;
+};
+
+// conv_wgrad2_kernel eligibility and split.  Splits are whole frame ranges;
+// S keeps each accumulator chain <= ~8192 terms (fp32 chain error) and is
+// picked so that the blocks fill whole rounds of 512 (2 per CU).
+bool plan_wgrad2(const ConvGeom &g, int xs, int dys, Wgrad2Plan &pl) {
+  static const int enabled = [] {
+    const char *e = getenv("KCNN_WGRAD2");
+    return e && *e ? atoi(e) : 1;
+  }();
+  if (!enabled || g.R <= 0 || g.G % W2_BG != 0 || g.P > 96 || g.Kdim < 32)
+    return false;
+  const bool padded = g.pad_h > 0 || g.pad_w > 0;
+  pl.fpc = g.P <= 16 ? 32 / g.P : 1;
+  pl.nch = g.P <= 32 ? 1 : (g.P + 31) / 32;
+  if ((int64_t)pl.fpc * xs * 4 >= 0x3f000000 || (int64_t)pl.fpc * dys * 4 >= 0x7f000000 ||
+      (int64_t)g.G * g.P * 4 >= 0x7f000000)
+    return false;
+  pl.ktiles = (g.Kdim + W2_BK - 1) / W2_BK;
+  const int ntiles = pl.ktiles * (g.G / W2_BG);
+  const int64_t chain = (int64_t)g.R * g.P;
+  int s0 = (int)((chain + 8191) / 8192);
+  if (s0 < 1) s0 = 1;
+  if (s0 * ntiles < 512) s0 = (512 + ntiles - 1) / ntiles;
+  if (s0 > g.R) s0 = g.R;
+  int best_s = -1, best_fps = 0;
+  int64_t best_cost = 0;
+  for (int s = s0; s <= 2 * s0 && s <= g.R; s++) {
+    int fps = (g.R + s - 1) / s;
+    fps = (fps + pl.fpc - 1) / pl.fpc * pl.fpc;  // whole chunks per split
+    const int sa = (g.R + fps - 1) / fps;
+    const int64_t rounds = ((int64_t)sa * ntiles + 511) / 512;
+    const int64_t cost = rounds * ((fps + pl.fpc - 1) / pl.fpc);
+    if (best_s < 0 || cost < best_cost) { best_s = sa; best_fps = fps; best_cost = cost; }
+  }
+  pl.S = best_s;
+  pl.fps = best_fps;
+  pl.nblocks = pl.S * ntiles;
+  const size_t E = (size_t)g.G * g.Kdim + g.G;
+  pl.ws_bytes = (size_t)pl.S * E * sizeof(float) + kcnn_reduce_splits_ws(pl.S, (int)E);
+  return true;
+}
+
+int launch_wgrad2(const ConvGeom &g, const Wgrad2Plan &pl, const float *X, int xs,
+                  const float *dY, int dys, float *ws, hipStream_t st) {
+  const bool padded = g.pad_h > 0 || g.pad_w > 0;
+  const dim3 grid((unsigned)(8 * ((pl.nblocks + 7) / 8)));
+#define KCNN_W2(N_, P_)                                                                    \
+  hipLaunchKernelGGL((conv_wgrad2_kernel<N_, P_>), grid, dim3(256), 0, st, g, X, xs, dY, \
+                     dys, ws, pl.fps, pl.fpc, pl.ktiles, pl.nblocks)
+#define KCNN_W2P(N_) do { if (padded) KCNN_W2(N_, true); else KCNN_W2(N_, false); } while (0)
+  switch (pl.nch) {
+    case 1: KCNN_W2P(1); break;
+    case 2: KCNN_W2P(2); break;
+    case 3: KCNN_W2P(3); break;
+    default: KCNN_W2P(3); break;
+  }
+#undef KCNN_W2P
+#undef KCNN_W2
+  return kcnn::launch_status();
 }
 
 }  // namespace
@@ -688,6 +932,10 @@ size_t hipF_conv2d_wgrad_workspace_bytes(MatrixDim in_dim, int in_height,
   size_t a = kcnn_conv_wgrad_frame_ws(g);
   const size_t b = plan_wgrad(g).ws_bytes, c = kcnn_conv_bwd_frame_ws(g);
   if (b > a) a = b;
+  Wgrad2Plan p2;
+  if (plan_wgrad2(g, in_dim.stride > 0 ? in_dim.stride : g.HW * in_channel,
+                  g.P * group, p2) && p2.ws_bytes > a)
+    a = p2.ws_bytes;
   return c > a ? c : a;
 }
 
@@ -717,6 +965,18 @@ int hipF_conv2d_wgrad(const float *in, MatrixDim in_dim, int in_height,
                                        grad_W_dim.stride, grad_b, workspace,
                                        workspace_bytes, st) == 0)
     return 0;
+  Wgrad2Plan p2;
+  if (g.M > 0 && plan_wgrad2(g, in_dim.stride, out_deriv_dim.stride, p2) &&
+      workspace != nullptr && workspace_bytes >= p2.ws_bytes) {
+    const int E = g.G * g.Kdim + g.G;
+    float *part = static_cast<float *>(workspace);
+    int rc = launch_wgrad2(g, p2, in, in_dim.stride, out_deriv, out_deriv_dim.stride,
+                           part, st);
+    if (rc) return rc;
+    return kcnn_reduce_splits_wgrad(part, p2.S, E, part + (size_t)p2.S * E,
+                                    g.G * g.Kdim, g.Kdim, grad_W, grad_W_dim.stride,
+                                    grad_b, st);
+  }
   WgradPlan pl = plan_wgrad(g);
   if (workspace == nullptr || workspace_bytes < pl.ws_bytes)
     return (int)hipErrorInvalidValue;

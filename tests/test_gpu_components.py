@@ -28,6 +28,11 @@ CONVS = {
     "small_pad": (5, 6, 2, 3, 3, 5, 1, 2),
     "tiny": (3, 4, 1, 2, 2, 3, 0, 0),
     "c5_C1_G256": (40, 11, 3, 8, 1, 256, 0, 0),         # c5 C1: 128-filter chunks
+    # long-kernel weight gradient (conv_wgrad2_kernel): chunks of 32 positions
+    "c5_C3": (8, 9, 256, 3, 3, 256, 1, 1),              # P = 72: 3 chunks, padded
+    "c5_C2": (11, 11, 64, 4, 3, 256, 0, 0),             # P = 72, no padding
+    "nch2_pad": (7, 8, 16, 3, 3, 128, 1, 1),            # P = 56: 2 chunks; Kdim 144
+    "fpc2_pad": (4, 4, 32, 3, 3, 128, 1, 1),            # P = 16: 2 frames per chunk
 }
 
 
@@ -145,6 +150,28 @@ def test_conv_backprop_gradient(kc, name):
     scale_W = np.abs(W0) + np.abs(p0) + lr * gW_s + 1e-30
     assert_bound(host(comp.LinearParams()), oc.W, scale_W, what=f"{name} W'")
     assert_bound(host(comp.BiasParams()), oc.b, np.abs(b0) + lr * gb_s, what=f"{name} b'")
+
+
+@pytest.mark.parametrize("cfg,N", [
+    ((8, 9, 256, 3, 3, 256, 1, 1), 70),    # c5 C3: several frames per split
+    ((4, 9, 64, 4, 3, 256, 0, 0), 61),     # c5 C4: P = 7, 4 frames per chunk, ragged tail
+])
+def test_conv_wgrad_long(kc, cfg, N):
+    """Weight/bias gradient of long kernels (conv_wgrad2_kernel: frame-range
+    splits, fixed-order reduction) against the oracle's Update gradient
+    (nnet-component-nnet0.cc:738-765); deterministic across calls."""
+    H, W, C, kh, kw, G, ph, pw = cfg
+    comp, oc = make_pair(kc, cfg, seed=N)
+    r = rng(300 + N)
+    x = randn(r, (N, H * W * C))
+    oh, ow = H + 2 * ph - kh + 1, W + 2 * pw - kw + 1
+    dy = randn(r, (N, oh * ow * G))
+    _, (gW_t, gb_t), (gW_s, gb_s) = triple(lambda: oc.gradient(x, dy))
+    g = host(comp.ComputeGradient(dev(x), dev(dy)))
+    kd = kh * kw * C
+    assert_bound(g[:kd * G].reshape(kd, G), gW_t, gW_s, what=f"{cfg} gW")
+    assert_bound(g[kd * G:], gb_t, gb_s, what=f"{cfg} gb")
+    assert_same(host(comp.ComputeGradient(dev(x), dev(dy))), g, what="repeat")
 
 
 def test_conv_backprop_gradient_special_values(kc):

@@ -644,6 +644,51 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad2_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Data gradient, scatter form (maps much larger than the output: c5 C2/C4).
+// The flipped-kernel gather (the reference's flip branch) multiplies every
+// input position by every tap, valid or not: at c5 C2 only P*khkw of
+// HW*khkw pairs (59 %) are real, at C4 19 %.  Here the contraction over the
+// filters runs once per (output position, kernel row) -- a 1x1 convolution
+// of dY with W^T on the implicit-GEMM kernel, Z[n][k*P + p] -- and
+// conv_col2im_kernel adds the kh*kw taps of each input position:
+//   dX[n][c*HW + x*H + y] = sum_{kx,ky valid} Z[n][(c*khkw + kx*kh + ky)*P
+//                                                  + (x-kx+pad_w)*oh + (y-ky+pad_h)]
+// (Appendix A.11's sum, grouped by tap).
+__global__ __launch_bounds__(256) void conv_transpose_kernel(
+    const float *__restrict__ in, int rows, int cols, int is,
+    float *__restrict__ out, int os) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)rows * cols) return;
+  const int r = (int)(e / cols), c = (int)(e - (int64_t)r * cols);
+  out[(int64_t)c * os + r] = in[(int64_t)r * is + c];
+}
+
+__global__ __launch_bounds__(256) void conv_col2im_kernel(
+    ConvGeom g, const float *__restrict__ Z, int zs, float *__restrict__ dX,
+    int dxs) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t per = (int64_t)g.C * g.HW;
+  if (e >= (int64_t)g.R * per) return;
+  const int n = (int)(e / per);
+  const uint32_t rem = (uint32_t)(e - (int64_t)n * per);
+  uint32_t c, q, x, y;
+  g.div_HW.divmod(rem, c, q);
+  g.div_H.divmod(q, x, y);
+  const float *zr = Z + (int64_t)n * zs + (int64_t)c * g.kh * g.kw * g.P;
+  float sum = 0.0f;
+  for (int kx = 0; kx < g.kw; kx++) {
+    const int px = (int)x - kx + g.pad_w;
+    if ((unsigned)px >= (unsigned)g.ow) continue;
+    for (int ky = 0; ky < g.kh; ky++) {
+      const int py = (int)y - ky + g.pad_h;
+      if ((unsigned)py >= (unsigned)g.oh) continue;
+      sum += zr[(int64_t)(kx * g.kh + ky) * g.P + px * g.oh + py];
+    }
+  }
+  dX[(int64_t)n * dxs + rem] = sum;
+}
+
+// ---------------------------------------------------------------------------
 // Host-side planning.
 struct IgemmPlan {
   int S, k_per_split;
@@ -716,7 +761,6 @@ bool plan_wgrad2(const ConvGeom &g, int xs, int dys, Wgrad2Plan &pl) {
   }();
   if (!enabled || g.R <= 0 || g.G % W2_BG != 0 || g.P > 96 || g.Kdim < 32)
     return false;
-  const bool padded = g.pad_h > 0 || g.pad_w > 0;
   pl.fpc = g.P <= 16 ? 32 / g.P : 1;
   pl.nch = g.P <= 32 ? 1 : (g.P + 31) / 32;
   if ((int64_t)pl.fpc * xs * 4 >= 0x3f000000 || (int64_t)pl.fpc * dys * 4 >= 0x7f000000 ||
@@ -763,6 +807,71 @@ int launch_wgrad2(const ConvGeom &g, const Wgrad2Plan &pl, const float *X, int x
   }
 #undef KCNN_W2P
 #undef KCNN_W2
+  return kcnn::launch_status();
+}
+
+// Scatter-form data gradient: worth it when the map has many more
+// positions than the output (gather waste HW/P) and the 1x1 GEMM runs on the
+// implicit-GEMM v2 kernel (Kdim a multiple of 64).
+bool use_dgrad_scatter(const ConvGeom &g) {
+  static const int enabled = [] {
+    const char *e = getenv("KCNN_DGRAD_SCATTER");
+    return e && *e ? atoi(e) : 1;
+  }();
+  return enabled && g.Kdim >= 64 && g.Kdim % (g.Kdim > 64 ? 128 : 64) == 0 &&
+         4 * (int64_t)g.HW >= 5 * (int64_t)g.P && g.G >= 16;
+}
+
+size_t zbytes_pad(size_t b) { return (b + 255) & ~(size_t)255; }
+
+size_t dgrad_scatter_ws(const ConvGeom &g) {
+  if (!use_dgrad_scatter(g)) return 0;
+  const int wts = (g.Kdim + 3) & ~3;
+  const size_t wt = zbytes_pad((size_t)g.G * wts * 4);
+  const size_t z = zbytes_pad((size_t)g.R * g.Kdim * g.P * 4);
+  ConvGeom g1 = make_geom(g.R, g.oh, g.ow, g.G, 0, 0, 1, 1, g.Kdim);
+  return wt + z + plan_igemm(g1).ws_bytes;
+}
+
+}  // namespace
+
+extern "C" {
+int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
+                int in_channel, int pad_h, int pad_w, const float *kernel,
+                MatrixDim kernel_dim, int kernel_height, int kernel_width,
+                int group, const float *bias, float *out, MatrixDim out_dim,
+                int concat, void *workspace, size_t workspace_bytes,
+                kcnn_stream_t stream);
+}
+
+namespace {
+
+int dgrad_scatter(const ConvGeom &g, const float *dY, MatrixDim dyd,
+                  const float *W, MatrixDim wd, float *dX, MatrixDim dxd,
+                  void *ws, size_t ws_bytes, kcnn_stream_t stream) {
+  hipStream_t st = kcnn::as_stream(stream);
+  const int wts = (g.Kdim + 3) & ~3;
+  float *wt = static_cast<float *>(ws);
+  const size_t wt_b = zbytes_pad((size_t)g.G * wts * 4);
+  float *z = reinterpret_cast<float *>(static_cast<char *>(ws) + wt_b);
+  const size_t z_b = zbytes_pad((size_t)g.R * g.Kdim * g.P * 4);
+  const int64_t nt = (int64_t)g.Kdim * g.G;
+  hipLaunchKernelGGL(conv_transpose_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256),
+                     0, st, W, g.Kdim, g.G, wd.stride, wt, wts);
+  int rc = kcnn::launch_status();
+  if (rc) return rc;
+  MatrixDim wtd, zd;
+  wtd.rows = g.G; wtd.cols = g.Kdim; wtd.stride = wts;
+  zd.rows = g.R; zd.cols = g.Kdim * g.P; zd.stride = zd.cols;
+  // Z[n][k*P + p] = sum_g dY[n][g*P + p] W[k][g]: a 1x1 convolution of the
+  // (oh x ow x G) map dY into Kdim output maps.
+  rc = hipF_conv2d(dY, dyd, g.oh, g.ow, g.G, 0, 0, wt, wtd, 1, 1, g.Kdim, nullptr, z,
+                   zd, 1, static_cast<char *>(ws) + wt_b + z_b, ws_bytes - wt_b - z_b,
+                   stream);
+  if (rc) return rc;
+  const int64_t ne = (int64_t)g.R * g.C * g.HW;
+  hipLaunchKernelGGL(conv_col2im_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0,
+                     st, g, z, zd.stride, dX, dxd.stride);
   return kcnn::launch_status();
 }
 
@@ -1015,7 +1124,9 @@ size_t hipF_conv2d_dgrad_workspace_bytes(MatrixDim out_deriv_dim, int in_height,
   const size_t flip_bytes = (size_t)kernel_height * kernel_width * group *
                             in_channel * sizeof(float);
   const size_t flip_pad = (flip_bytes + 255) & ~(size_t)255;
-  return flip_pad + (use_direct(gt, 1) ? 0 : plan_igemm(gt).ws_bytes);
+  const size_t a = flip_pad + (use_direct(gt, 1) ? 0 : plan_igemm(gt).ws_bytes);
+  const size_t b = dgrad_scatter_ws(g);
+  return b > a ? b : a;
 }
 
 int hipF_conv2d_dgrad(const float *out_deriv, MatrixDim out_deriv_dim,
@@ -1043,6 +1154,10 @@ int hipF_conv2d_dgrad(const float *out_deriv, MatrixDim out_deriv_dim,
                             kernel_dim.stride, in_deriv, in_deriv_dim.stride,
                             st) == 0)
     return 0;
+  if (use_dgrad_scatter(g) && workspace != nullptr &&
+      workspace_bytes >= dgrad_scatter_ws(g))
+    return dgrad_scatter(g, out_deriv, out_deriv_dim, kernel, kernel_dim, in_deriv,
+                         in_deriv_dim, workspace, workspace_bytes, stream);
   // General shapes: dX = Conv2D(virtually padded dY, FlipMat(W)) -- the
   // reference's flip branch (nnet-component-nnet0.cc:529-540) in gather form.
   const size_t flip_bytes = (size_t)kernel_height * kernel_width * group *

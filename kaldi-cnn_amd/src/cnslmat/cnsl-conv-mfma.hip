@@ -469,9 +469,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(
 //   D[g][k] = sum_t dY[n][g*P + p] * B[t][k],   t = (n, p) over the block's
 //   frames, B = im2col(X) (Appendix A.12), block tile 128 (g) x 128 (k),
 //   each wave 64 x 64 (four 32x32 accumulators) as in conv_igemm2_kernel.
-// The reduction walks the block's frames in chunks of 32 positions, and lane
-// tl of every chunk always stands for the same position (p = 32c + tl, or
-// frame offset tl / P and p = tl % P when P <= 16).  Its map offset and its
+// The reduction walks the block's frames in chunks of bt <= 32 positions
+// (P split evenly, so no k-step multiplies padding), and lane tl of every
+// chunk always stands for the same position (p = bt*c + tl, or frame offset
+// tl / P and p = tl % P when P <= 16).  Its map offset and its
 // tap-validity mask are therefore computed once; per step only the frame
 // base moves, and that lives in the (scalar) buffer descriptors, whose range
 // also drops the frames past the split.  Per gathered X element: one add
@@ -485,7 +486,7 @@ constexpr int W2_BG = 128, W2_BK = 128, W2_LD = 129;
 template <int NCH, bool PADDED>
 __global__ __launch_bounds__(256, 2) void conv_wgrad2_kernel(
     ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ dY,
-    int dys, float *__restrict__ ws, int fps, int fpc, int ktiles, int nblocks) {
+    int dys, float *__restrict__ ws, int fps, int fpc, int bt, int ktiles, int nblocks) {
   __shared__ float As[2][32][W2_LD];  // dY tile [t][g]
   __shared__ float Bs[2][32][W2_LD];  // im2col tile [t][k]
   // XCD-aware order: hardware places block b on XCD b % 8; logical ids are
@@ -524,9 +525,9 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad2_kernel(
   unsigned voffA[NCH], lpos4[NCH], bad[NCH];
 #pragma unroll
   for (int c = 0; c < NCH; c++) {
-    int fo = 0, p = 32 * c + tl;
+    int fo = 0, p = bt * c + tl;
     if (fpc > 1) { fo = tl / g.P; p = tl - fo * g.P; }
-    const bool valid = fpc > 1 ? fo < fpc : p < g.P;
+    const bool valid = tl < bt && (fpc > 1 ? fo < fpc : p < g.P);
     uint32_t px = 0, py = 0;
     if (valid) g.div_oh.divmod((uint32_t)p, px, py);
     voffA[c] = valid ? (unsigned)((fo * dys + rs * g.P + p) * 4) : 0x80000000u;
@@ -600,6 +601,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad2_kernel(
       if (more) load(c + 1 < NCH ? n : n + fpc, c + 1 < NCH ? c + 1 : 0);
 #pragma unroll
       for (int s = 0; s < 16; s++) {
+        if (2 * s >= bt) break;  // chunk length bt (uniform): no padded k-steps
         const float a0 = As[cur][2 * s + h][wg * 64 + l];
         const float a1 = As[cur][2 * s + h][wg * 64 + 32 + l];
         const float b0 = Bs[cur][2 * s + h][wk * 64 + l];
@@ -747,7 +749,7 @@ WgradPlan plan_wgrad(const ConvGeom &g) {
 }
 
 struct Wgrad2Plan {
-  int S, fps, fpc, nch, ktiles, nblocks;
+  int S, fps, fpc, nch, bt, ktiles, nblocks;
   size_t ws_bytes;
 };
 
@@ -763,6 +765,10 @@ bool plan_wgrad2(const ConvGeom &g, int xs, int dys, Wgrad2Plan &pl) {
     return false;
   pl.fpc = g.P <= 16 ? 32 / g.P : 1;
   pl.nch = g.P <= 32 ? 1 : (g.P + 31) / 32;
+  // positions per chunk: P split evenly (c5 P = 72 -> 3 x 24), even for the
+  // MFMA's k-pairs; lanes past bt load nothing and feed no MFMA
+  pl.bt = g.P <= 16 ? pl.fpc * g.P : (g.P + pl.nch - 1) / pl.nch;
+  pl.bt = (pl.bt + 1) & ~1;
   if ((int64_t)pl.fpc * xs * 4 >= 0x3f000000 || (int64_t)pl.fpc * dys * 4 >= 0x7f000000 ||
       (int64_t)g.G * g.P * 4 >= 0x7f000000)
     return false;
@@ -797,7 +803,7 @@ int launch_wgrad2(const ConvGeom &g, const Wgrad2Plan &pl, const float *X, int x
   const dim3 grid((unsigned)(8 * ((pl.nblocks + 7) / 8)));
 #define KCNN_W2(N_, P_)                                                                    \
   hipLaunchKernelGGL((conv_wgrad2_kernel<N_, P_>), grid, dim3(256), 0, st, g, X, xs, dY, \
-                     dys, ws, pl.fps, pl.fpc, pl.ktiles, pl.nblocks)
+                     dys, ws, pl.fps, pl.fpc, pl.bt, pl.ktiles, pl.nblocks)
 #define KCNN_W2P(N_) do { if (padded) KCNN_W2(N_, true); else KCNN_W2(N_, false); } while (0)
   switch (pl.nch) {
     case 1: KCNN_W2P(1); break;

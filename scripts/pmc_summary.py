@@ -14,10 +14,9 @@ import os
 
 
 def short(name, n=48):
-    name = name.split("(")[0]
     for pre in ("void ", "(anonymous namespace)::"):
         name = name.replace(pre, "")
-    return name[:n]
+    return name.split("(")[0][:n]
 
 
 def main():

@@ -438,6 +438,57 @@ __global__ __launch_bounds__(256) void maxpool_direct_backprop_kernel(
   }
 }
 
+// Non-overlap backprop for general (ph x pw x pc) windows (c5's 3-D pools),
+// gather form with write_all semantics: a thread takes 4 consecutive inputs
+// (16-B load and store), finds each one's window j and writes
+// dP[j] if in == P[j], else 0 (A.9; the window's P/dP reads hit L1/L2).
+constexpr int kPoolWinVec = 2;  // float4 groups per thread in flight
+__global__ __launch_bounds__(256) void maxpool_window_backprop_kernel(
+    const float *__restrict__ x, int64_t xs, const float *__restrict__ y, int64_t ys,
+    const float *__restrict__ dy, int64_t dys, float *__restrict__ dx, int64_t dxs,
+    uint32_t total4, FastDiv div_cols4, FastDiv div_plane, FastDiv div_h, FastDiv div_ph,
+    FastDiv div_pw, FastDiv div_pc, int H, int W, int outplane, int outh) {
+  const uint32_t base = blockIdx.x * (256u * kPoolWinVec) + threadIdx.x;
+  float4 xv[kPoolWinVec];
+  float pv[kPoolWinVec][4], dv[kPoolWinVec][4];
+  int64_t off[kPoolWinVec];
+#pragma unroll
+  for (int t = 0; t < kPoolWinVec; t++) {
+    const uint32_t e0 = base + 256u * t;
+    const uint32_t e = e0 < total4 ? e0 : total4 - 1;
+    uint32_t row, q4, c, rem, w, h;
+    div_cols4.divmod(e, row, q4);
+    const uint32_t col = 4 * q4;
+    div_plane.divmod(col, c, rem);
+    div_h.divmod(rem, w, h);
+    xv[t] = *reinterpret_cast<const float4 *>(x + (int64_t)row * xs + col);
+    const float *yr = y + (int64_t)row * ys;
+    const float *dr = dy + (int64_t)row * dys;  // own stride (B14)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t j = div_pc.div(c) * (uint32_t)outplane +
+                         div_pw.div(w) * (uint32_t)outh + div_ph.div(h);
+      pv[t][k] = yr[j];
+      dv[t][k] = dr[j];
+      if (++h == (uint32_t)H) {
+        h = 0;
+        if (++w == (uint32_t)W) { w = 0; ++c; }
+      }
+    }
+    off[t] = (int64_t)row * dxs + col;
+  }
+#pragma unroll
+  for (int t = 0; t < kPoolWinVec; t++) {
+    if (base + 256u * t >= total4) continue;
+    float4 o;
+    o.x = xv[t].x == pv[t][0] ? dv[t][0] : 0.0f;
+    o.y = xv[t].y == pv[t][1] ? dv[t][1] : 0.0f;
+    o.z = xv[t].z == pv[t][2] ? dv[t][2] : 0.0f;
+    o.w = xv[t].w == pv[t][3] ? dv[t][3] : 0.0f;
+    *reinterpret_cast<float4 *>(dx + off[t]) = o;
+  }
+}
+
 // Backprop of the channel-only pool from the routing mask saved by the fused
 // forward (hipF_conv2d_maxpool): dX[(PC j + c) plane + q] = bit c of
 // mask[j plane + q] ? dP[j plane + q] : 0 -- the same values A.9 produces
@@ -788,6 +839,28 @@ int hipF_maxpool_backprop(const float *in_val, MatrixDim in_val_dim,
                        (int64_t)out_deriv_dim.stride, dest, (int64_t)dest_dim.stride,
                        (uint32_t)nout, FastDiv((uint32_t)out_val_dim.cols),
                        FastDiv((uint32_t)plane0), plane0);
+    return kcnn::launch_status();
+  }
+  if (write_all && mode == 0 && (pool_height_dim > 1 || pool_width_dim > 1) &&
+      in_val_dim.cols % 4 == 0 && in_val_dim.stride % 4 == 0 && dest_dim.stride % 4 == 0 &&
+      dest_dim.cols == in_val_dim.cols && (uintptr_t)in_val % 16 == 0 &&
+      (uintptr_t)dest % 16 == 0 && in_height % pool_height_dim == 0 &&
+      in_width % pool_width_dim == 0 &&
+      in_val_dim.cols == out_val_dim.cols * pool_height_dim * pool_width_dim * pool_channel_dim &&
+      (int64_t)in_val_dim.rows * in_val_dim.cols < ((int64_t)1 << 33) && env_pool_direct()) {
+    const uint32_t total4 = (uint32_t)((int64_t)in_val_dim.rows * in_val_dim.cols / 4);
+    if (total4 == 0) return 0;
+    const int outh = in_height / pool_height_dim;
+    const int outplane = outh * (in_width / pool_width_dim);
+    const unsigned blocks = (total4 + 256 * kPoolWinVec - 1) / (256 * kPoolWinVec);
+    hipLaunchKernelGGL(maxpool_window_backprop_kernel, dim3(blocks), dim3(256), 0, st,
+                       in_val, (int64_t)in_val_dim.stride, out_val,
+                       (int64_t)out_val_dim.stride, out_deriv, (int64_t)out_deriv_dim.stride,
+                       dest, (int64_t)dest_dim.stride, total4,
+                       FastDiv((uint32_t)(in_val_dim.cols / 4)), FastDiv((uint32_t)plane0),
+                       FastDiv((uint32_t)in_height), FastDiv((uint32_t)pool_height_dim),
+                       FastDiv((uint32_t)pool_width_dim), FastDiv((uint32_t)pool_channel_dim),
+                       in_height, in_width, outplane, outh);
     return kcnn::launch_status();
   }
   if (write_all &&

@@ -216,6 +216,9 @@ def test_conv_update_divides_by_local_rows(kc):
     (8, 9, 256, 2, 1, 4, False, False),
     (4, 3, 6, 1, 1, 3, True, False),
     (2, 3, 16, 1, 1, 2, False, True),
+    (33, 11, 256, 3, 1, 4, False, False),   # c5 P1 (3-D window, 16-B gather kernel)
+    (3, 2, 8, 3, 2, 2, False, False),       # 4-element groups wrap h -> w -> c
+    (6, 5, 3, 2, 5, 3, False, False),       # row length 90: not a multiple of 4
 ])
 def test_maxpool_component(kc, path, cfg):
     H, W, C, ph, pw, pc, ov, ov2 = cfg

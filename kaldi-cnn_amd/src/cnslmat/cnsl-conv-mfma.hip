@@ -148,7 +148,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(
 //     per-lane bitmask of the taps that fall inside the map (kh*kw <= 32)
 //     drops the others (buffer loads make any stray offset safe).
 //   * Operands per MFMA: one LDS read (A: W tile, B: im2col tile).
-template <int WGG, bool PADDED, int IG2_BK>
+constexpr int IG2_KTAB = 2304;  // im2col-row table entries (c5 C3: Kdim 2304)
+
+template <int WGG, bool PADDED, int IG2_BK, bool TAB>
 __global__ __launch_bounds__(256) void conv_igemm2_kernel(
     ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ Kmat,
     int ks, const float *__restrict__ bias, float *__restrict__ out, int os, int dbg) {
@@ -158,6 +160,11 @@ __global__ __launch_bounds__(256) void conv_igemm2_kernel(
   constexpr int BNF = IG2_BK * BM / 256;  // B floats per thread per K step (8 or 16)
   __shared__ __attribute__((aligned(16))) float As[2][IG2_BK][BG];
   __shared__ __attribute__((aligned(16))) float Bs[2][IG2_BK][BM];
+  // TAB: per im2col row k its map offset (bytes) and tap, stored per
+  // row-parity class [k % B_RSTEP][k / B_RSTEP] so that a thread's BNF rows
+  // of one K step are consecutive (16-B LDS reads, wave-uniform address).
+  __shared__ __attribute__((aligned(16))) unsigned ktab_off[TAB ? IG2_KTAB : 1];
+  __shared__ __attribute__((aligned(16))) unsigned ktab_tap[TAB && PADDED ? IG2_KTAB : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wg = wave % WGG, wm = wave / WGG;
@@ -197,13 +204,33 @@ __global__ __launch_bounds__(256) void conv_igemm2_kernel(
     if (!mvalid) tapmask = 0;
   }
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)X, (short)0, (int)((int64_t)g.R * xs * 4 < 0x7fffffff ? (int64_t)g.R * xs * 4 : 0x7fffffff),
-      0x00020000);
+      (void *)X, (short)0,
+      (dbg & 4) ? 0 : (int)((int64_t)g.R * xs * 4 < 0x7fffffff ? (int64_t)g.R * xs * 4 : 0x7fffffff),
+      0x00020000);  // dbg & 4: zero records (timing: same instructions, no traffic)
 
   // W rows through a descriptor too: rows past Kdim read 0 (range check)
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)Kmat, (short)0, g.Kdim * ks * 4, 0x00020000);
+      (void *)Kmat, (short)0, (dbg & 8) ? 0 : g.Kdim * ks * 4, 0x00020000);
   if (!PADDED) tapmask = mvalid ? 0xffffffffu : 0u;
+  // TAB: rows past Kdim have tap 31, which no lane's mask admits (kh*kw <= 31)
+  const unsigned nmask = PADDED ? ~(tapmask & 0x7fffffffu) : 0u;
+  const unsigned xoff4 = (unsigned)xoff * 4u;
+  const int kq = (nk * IG2_BK) / B_RSTEP;  // table entries per parity class
+  if (TAB) {
+    for (int k = tid; k < nk * IG2_BK; k += 256) {
+      uint32_t c = 0, r = 0, kx = 0, ky = 0;
+      if (k < g.Kdim) {
+        g.div_khkw.divmod((uint32_t)k, c, r);
+        g.div_kh.divmod(r, kx, ky);
+      }
+      const int slot = (k % B_RSTEP) * kq + k / B_RSTEP;
+      ktab_off[slot] = k < g.Kdim
+                           ? (unsigned)(((int)c * g.HW + (int)kx * g.H + (int)ky) * 4)
+                           : (PADDED ? 0u : 0x80000000u);
+      if (PADDED) ktab_tap[slot] = k < g.Kdim ? kx * (uint32_t)g.kh + ky : 31u;
+    }
+    __syncthreads();
+  }
   float4 areg[ANF / 4];
   float breg[BNF];
   unsigned bok = 0;  // bit j: element j of breg is inside the map
@@ -219,6 +246,27 @@ __global__ __launch_bounds__(256) void conv_igemm2_kernel(
           wr, (unsigned)(k * ks + g0 + ag) * 4u, 0, 0);
       areg[i] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]),
                             __uint_as_float(v[2]), __uint_as_float(v[3]));
+    }
+    if (TAB) {
+      // one add per element; padded maps: the tap's bit of this lane's
+      // outside-mask moves the offset out of range (the load returns 0)
+      const int t0 = br * kq + kb / B_RSTEP;
+#pragma unroll
+      for (int q = 0; q < BNF / 4; q++) {
+        const uint4 ko = *reinterpret_cast<const uint4 *>(&ktab_off[t0 + 4 * q]);
+        uint4 kt = make_uint4(0, 0, 0, 0);
+        if (PADDED) kt = *reinterpret_cast<const uint4 *>(&ktab_tap[t0 + 4 * q]);
+        const unsigned kov[4] = {ko.x, ko.y, ko.z, ko.w};
+        const unsigned ktv[4] = {kt.x, kt.y, kt.z, kt.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          unsigned off = xoff4 + kov[e];
+          if (PADDED) off |= ((nmask >> ktv[e]) & 1u) << 31;
+          breg[4 * q + e] = __uint_as_float(
+              __builtin_amdgcn_raw_buffer_load_b32(xr, off, 0, 0));
+        }
+      }
+      return;
     }
 #pragma unroll
     for (int j = 0; j < BNF; j++) {
@@ -242,7 +290,7 @@ __global__ __launch_bounds__(256) void conv_igemm2_kernel(
       *reinterpret_cast<float4 *>(&As[b][ar + A_RSTEP * i][ag]) = areg[i];
 #pragma unroll
     for (int j = 0; j < BNF; j++)
-      Bs[b][br + B_RSTEP * j][bm] = (bok >> j) & 1u ? breg[j] : 0.0f;
+      Bs[b][br + B_RSTEP * j][bm] = (TAB || ((bok >> j) & 1u)) ? breg[j] : 0.0f;
   };
 
   floatx16 acc[2][2];
@@ -983,14 +1031,26 @@ int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
     const char *e = getenv("KCNN_IGEMM2_BK");
     return e && *e ? atoi(e) : 16;
   }();
+  static const int ig2tab = [] {
+    const char *e = getenv("KCNN_IGEMM2_TAB");
+    return e && *e ? atoi(e) : 1;
+  }();
+  const bool tab = ig2tab && (g.Kdim + 15) / 16 * 16 <= IG2_KTAB &&
+                   (int64_t)g.HW * g.C < (1 << 28) && (!padded || g.kh * g.kw <= 31);
 #define KCNN_IG2(W_, P_)                                                                  \
   do {                                                                                    \
-    if (ig2bk == 32)                                                                      \
-      hipLaunchKernelGGL((conv_igemm2_kernel<W_, P_, 32>), grid2, dim3(256), 0, st, g, in, \
-                         in_dim.stride, kernel, kernel_dim.stride, bias, out, out_dim.stride, ig2dbg); \
+    if (tab)                                                                              \
+      hipLaunchKernelGGL((conv_igemm2_kernel<W_, P_, 16, true>), grid2, dim3(256), 0, st, g, \
+                         in, in_dim.stride, kernel, kernel_dim.stride, bias, out,          \
+                         out_dim.stride, ig2dbg);                                          \
+    else if (ig2bk == 32)                                                                 \
+      hipLaunchKernelGGL((conv_igemm2_kernel<W_, P_, 32, false>), grid2, dim3(256), 0, st, g, \
+                         in, in_dim.stride, kernel, kernel_dim.stride, bias, out,          \
+                         out_dim.stride, ig2dbg);                                          \
     else                                                                                  \
-      hipLaunchKernelGGL((conv_igemm2_kernel<W_, P_, 16>), grid2, dim3(256), 0, st, g, in, \
-                         in_dim.stride, kernel, kernel_dim.stride, bias, out, out_dim.stride, ig2dbg); \
+      hipLaunchKernelGGL((conv_igemm2_kernel<W_, P_, 16, false>), grid2, dim3(256), 0, st, g, \
+                         in, in_dim.stride, kernel, kernel_dim.stride, bias, out,          \
+                         out_dim.stride, ig2dbg);                                          \
   } while (0)
     if (wgg == 2) {
       if (padded) KCNN_IG2(2, true); else KCNN_IG2(2, false);

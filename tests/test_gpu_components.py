@@ -33,6 +33,9 @@ CONVS = {
     "c5_C2": (11, 11, 64, 4, 3, 256, 0, 0),             # P = 72, no padding
     "nch2_pad": (7, 8, 16, 3, 3, 128, 1, 1),            # P = 56: 2 chunks; Kdim 144
     "fpc2_pad": (4, 4, 32, 3, 3, 128, 1, 1),            # P = 16: 2 frames per chunk
+    # implicit-GEMM v2 with its im2col-row table: Kdim not a multiple of 16
+    "ig2_tail_g64": (6, 7, 9, 3, 3, 64, 1, 1),          # Kdim 81, one 64-filter tile
+    "ig2_tail_g128": (5, 6, 11, 3, 3, 128, 1, 0),       # Kdim 99, pad on one axis
 }
 
 

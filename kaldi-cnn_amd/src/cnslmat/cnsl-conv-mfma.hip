@@ -738,6 +738,47 @@ __global__ __launch_bounds__(256) void conv_col2im_kernel(
   dX[(int64_t)n * dxs + rem] = sum;
 }
 
+// col2im, one wave per (frame, input channel): the channel's kh*kw*P values
+// of Z are one contiguous run (16-B coalesced into LDS), its H*W outputs
+// another; the tap gathers happen in LDS.  Same sums, same order as
+// conv_col2im_kernel.
+__global__ __launch_bounds__(64) void conv_col2im_plane_kernel(
+    ConvGeom g, const float *__restrict__ Z, int zs, float *__restrict__ dX, int dxs,
+    int vec) {
+  extern __shared__ __attribute__((aligned(16))) float zp[];
+  const int lane = threadIdx.x;
+  const int U = g.kh * g.kw * g.P;
+  const int units = g.R * g.C;
+  for (int u = blockIdx.x; u < units; u += gridDim.x) {
+    const int n = u / g.C, c = u - n * g.C;
+    const float *src = Z + (int64_t)n * zs + (int64_t)c * U;
+    if (vec) {
+      for (int i = lane; i < U / 4; i += 64)
+        reinterpret_cast<float4 *>(zp)[i] = reinterpret_cast<const float4 *>(src)[i];
+    } else {
+      for (int i = lane; i < U; i += 64) zp[i] = src[i];
+    }
+    __syncthreads();
+    float *dst = dX + (int64_t)n * dxs + (int64_t)c * g.HW;
+    for (int qd = lane; qd < g.HW; qd += 64) {
+      uint32_t x, y;
+      g.div_H.divmod((uint32_t)qd, x, y);
+      float sum = 0.0f;
+      for (int kx = 0; kx < g.kw; kx++) {
+        const int px = (int)x - kx + g.pad_w;
+        if ((unsigned)px >= (unsigned)g.ow) continue;
+        for (int ky = 0; ky < g.kh; ky++) {
+          const int py = (int)y - ky + g.pad_h;
+          if ((unsigned)py >= (unsigned)g.oh) continue;
+          sum += zp[(kx * g.kh + ky) * g.P + px * g.oh + py];
+        }
+      }
+      dst[qd] = sum;
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Host-side planning.
 struct IgemmPlan {
@@ -923,6 +964,15 @@ int dgrad_scatter(const ConvGeom &g, const float *dY, MatrixDim dyd,
                    zd, 1, static_cast<char *>(ws) + wt_b + z_b, ws_bytes - wt_b - z_b,
                    stream);
   if (rc) return rc;
+  const size_t zlds = (size_t)g.kh * g.kw * g.P * 4;
+  if (zlds <= 32768) {
+    const int units = g.R * g.C;
+    const bool vec = (g.kh * g.kw * g.P) % 4 == 0 && zd.stride % 4 == 0;
+    hipLaunchKernelGGL(conv_col2im_plane_kernel,
+                       dim3((unsigned)(units < 256 * 24 ? units : 256 * 24)), dim3(64), zlds,
+                       st, g, z, zd.stride, dX, dxd.stride, vec ? 1 : 0);
+    return kcnn::launch_status();
+  }
   const int64_t ne = (int64_t)g.R * g.C * g.HW;
   hipLaunchKernelGGL(conv_col2im_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0,
                      st, g, z, zd.stride, dX, dxd.stride);

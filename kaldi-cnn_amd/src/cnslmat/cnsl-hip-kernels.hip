@@ -489,6 +489,85 @@ __global__ __launch_bounds__(256) void maxpool_window_backprop_kernel(
   }
 }
 
+// 3-D windows (ph x pw x pc, c5's P1/P2), one wave per (row, output
+// channel group): the group's pc input maps are one contiguous run of the
+// row (pc*H*W floats) and its outputs another (OP = H/ph * W/pw), so every
+// HBM access is a coalesced 16-B-per-lane run; the window gathers happen in
+// LDS.  Forward: A.8 (val = -1e20, `val < x`).  (A plane backprop measured
+// slower than maxpool_window_backprop_kernel's 16-B gather: 0.99 vs 0.85 ms
+// at c5.)
+struct PoolPlane {
+  int H, W, ph, pw, pc, HW, blk, OP, oh2, units, vec;
+  FastDiv div_groups, div_oh2;
+};
+
+__device__ __forceinline__ void plane_copy_in(float *dst, const float *src, int n, int vec,
+                                              int lane) {
+  if (vec) {
+    for (int i = lane; i < n / 4; i += 64)
+      reinterpret_cast<float4 *>(dst)[i] = reinterpret_cast<const float4 *>(src)[i];
+  } else {
+    for (int i = lane; i < n; i += 64) dst[i] = src[i];
+  }
+}
+
+__global__ __launch_bounds__(64) void maxpool_plane_prop_kernel(
+    const float *__restrict__ src, int64_t ss, float *__restrict__ pool, int64_t ps,
+    PoolPlane q) {
+  extern __shared__ __attribute__((aligned(16))) float blk[];
+  const int lane = threadIdx.x;
+  for (int u = blockIdx.x; u < q.units; u += gridDim.x) {
+    uint32_t n, oc;
+    q.div_groups.divmod((uint32_t)u, n, oc);
+    plane_copy_in(blk, src + (int64_t)n * ss + (int64_t)oc * q.blk, q.blk, q.vec, lane);
+    __syncthreads();
+    float *out = pool + (int64_t)n * ps + (int64_t)oc * q.OP;
+    for (int o = lane; o < q.OP; o += 64) {
+      uint32_t wi, hi;
+      q.div_oh2.divmod((uint32_t)o, wi, hi);
+      const float *b = blk + wi * q.pw * q.H + hi * q.ph;
+      float val = -1e20f;
+      for (int c = 0; c < q.pc; c++)
+        for (int w = 0; w < q.pw; w++)
+          for (int h = 0; h < q.ph; h++) {
+            const float x = b[c * q.HW + w * q.H + h];
+            if (val < x) val = x;
+          }
+      out[o] = val;
+    }
+    __syncthreads();
+  }
+}
+
+PoolPlane make_pool_plane(int64_t rows, int in_cols, int H, int W, int ph, int pw, int pc,
+                          bool vec) {
+  PoolPlane q;
+  q.H = H; q.W = W; q.ph = ph; q.pw = pw; q.pc = pc;
+  q.HW = H * W;
+  q.blk = pc * q.HW;
+  q.oh2 = H / ph;
+  q.OP = q.oh2 * (W / pw);
+  const int groups = in_cols / q.blk;
+  q.units = (int)(rows * groups);
+  q.vec = vec ? 1 : 0;
+  q.div_groups = FastDiv((uint32_t)groups);
+  q.div_oh2 = FastDiv((uint32_t)q.oh2);
+  return q;
+}
+
+bool env_pool_direct();
+
+// Plane kernels apply to non-overlap windows with ph*pw > 1 whose group of
+// pc maps fits the LDS budget; 16-B copies when the runs are aligned.
+bool pool_plane_ok(int in_cols, int H, int W, int ph, int pw, int pc, int mode,
+                   int64_t rows) {
+  return mode == 0 && (ph > 1 || pw > 1) && H % ph == 0 && W % pw == 0 &&
+         in_cols % (pc * H * W) == 0 && (size_t)(pc * H * W + 2 * (H / ph) * (W / pw)) * 4 <= 32768 &&
+         rows * (in_cols / (pc * H * W)) < ((int64_t)1 << 31) && env_pool_direct();
+}
+
+unsigned plane_grid(int units) { return (unsigned)(units < 256 * 24 ? units : 256 * 24); }
+
 // Backprop of the channel-only pool from the routing mask saved by the fused
 // forward (hipF_conv2d_maxpool): dX[(PC j + c) plane + q] = bit c of
 // mask[j plane + q] ? dP[j plane + q] : 0 -- the same values A.9 produces
@@ -791,6 +870,19 @@ int hipF_maxpool_prop(const float *src, MatrixDim src_dim, float *pool,
                        src, (int64_t)src_dim.stride, pool, (int64_t)pool_dim.stride,
                        (uint32_t)nout, FastDiv((uint32_t)pool_dim.cols),
                        FastDiv((uint32_t)plane), plane);
+    return kcnn::launch_status();
+  }
+  if (pool_plane_ok(src_dim.cols, in_height, in_width, pool_height_dim, pool_width_dim,
+                    pool_channel_dim, mode, src_dim.rows) &&
+      pool_dim.cols * pool_height_dim * pool_width_dim * pool_channel_dim == src_dim.cols) {
+    const bool vec = ((pool_channel_dim * plane) & 3) == 0 && (src_dim.stride & 3) == 0 &&
+                     ((uintptr_t)src & 15) == 0;
+    PoolPlane q = make_pool_plane(src_dim.rows, src_dim.cols, in_height, in_width,
+                                  pool_height_dim, pool_width_dim, pool_channel_dim, vec);
+    if (q.units == 0) return 0;
+    hipLaunchKernelGGL(maxpool_plane_prop_kernel, dim3(plane_grid(q.units)), dim3(64),
+                       (size_t)q.blk * 4, kcnn::as_stream(stream), src,
+                       (int64_t)src_dim.stride, pool, (int64_t)pool_dim.stride, q);
     return kcnn::launch_status();
   }
   if (pool_groups_ok(src, src_dim.stride, plane, pool_channel_dim,

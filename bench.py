@@ -156,6 +156,8 @@ def main():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--no-fusion", action="store_true",
                     help="run Conv and Maxpool as separate components")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (default); gloo = rehearsal on shared GPUs")
     ap.add_argument("--config", default="c2", choices=["c2", "c5"],
                     help="c2 (default, BASELINE's metric) or the c5 deep stack")
     args = ap.parse_args()
@@ -170,11 +172,18 @@ def main():
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     dist = None
+    # one process per GPU; --dist-backend gloo rehearses the N > 1 path with
+    # several ranks sharing the GPUs there are (RCCL needs one GPU per rank)
+    device = local_rank % max(1, torch.cuda.device_count()) \
+        if args.dist_backend == "gloo" else local_rank
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
-    kcnn.init(local_rank)
+        torch.cuda.set_device(device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{device}"))
+        else:
+            dist.init_process_group(args.dist_backend)
+    kcnn.init(device)
     kcnn.set_fusion(not args.no_fusion)
     kcnn.set_randn_seed(20261015)  # identical initial params on every replica
 

@@ -1,0 +1,41 @@
+"""Data-parallel training step on the GPU (bench.py --gpus N):
+two ranks (gloo, sharing the one GPU of the test box -- RCCL needs a GPU
+per rank) run kcnn_dp.dp_train_step through libkcnn.so on their shards of a
+global batch.  The replicas must stay bitwise identical, and must match one
+process that trained on the whole batch (the reference's update with the
+global frame count, nnet-component-nnet0.cc:767) to the fp32 reduction-order
+tolerance."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_dp_two_ranks_match_single_process(tmp_path):
+    steps, n_global = 2, 48
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(HERE, "dp_gpu_worker.py"), str(tmp_path), str(steps), str(n_global)]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    a, b = np.load(tmp_path / "rank0.npz"), np.load(tmp_path / "rank1.npz")
+    single = np.load(tmp_path / "single.npz")
+    assert sorted(a.files) == sorted(single.files) and len(a.files) == 6
+    for k in a.files:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=f"replicas differ: {k}")
+        ref = single[k]
+        err = np.abs(a[k] - ref).max() / max(np.abs(ref).max(), 1e-30)
+        assert err < 1e-5, f"{k}: DP vs single-process relative error {err:.2e}"

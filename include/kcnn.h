@@ -15,6 +15,10 @@
  *                     src/nnet2/nnet-component.h:157-348) and the factory
  *                     Component::NewFromString / ReadNew
  *                     (src/nnet2/nnet-component.cc:38-136)
+ *                     Also the upstream nnet2 components either side of
+ *                     the CNN path: SpliceComponent and
+ *                     RectifiedLinearComponent (src/nnet2/nnet-component.cc
+ *                     :799-827, :2524-2866), by the same entry points.
  *   kcnn_nnet_*       the propagate/backprop loop of upstream nnet2's
  *                     NnetUpdater (not vendored by the reference)
  *                     over a stack of these components.
@@ -111,6 +115,20 @@ int kcnn_component_type(const kcnn_component *c, char *buf, size_t len);
 int kcnn_component_info(const kcnn_component *c, char *buf, size_t len);
 int kcnn_component_input_dim(const kcnn_component *c);
 int kcnn_component_output_dim(const kcnn_component *c);
+/* Component::Context() (reference nnet-component.h:186-188): the frame
+ * offsets the component reads per output frame -- {0} except SpliceComponent
+ * (its left..right context).  Writes up to max_len offsets, returns the count
+ * (-1 on error).  For propagate/backprop the input chunk is the output chunk
+ * widened by this context: in_rows/num_chunks = out_rows/num_chunks +
+ * back - front. */
+int kcnn_component_context(const kcnn_component *c, int *offsets, int max_len);
+/* NonlinearComponent::ValueSum()/DerivSum()/Count() (reference
+ * nnet-component.h:377-379; accumulated by UpdateStats in Backprop when
+ * to_update is set): copies up to max_len fp64 values to HOST arrays, *len =
+ * their length (0 before the first update). */
+int kcnn_component_nonlinear_stats(const kcnn_component *c, double *value_sum,
+                                   double *deriv_sum, int max_len, int *len,
+                                   double *count);
 int kcnn_component_backprop_needs_input(const kcnn_component *c);
 int kcnn_component_backprop_needs_output(const kcnn_component *c);
 /* Component::Propagate(ChunkInfo(in_dim.cols, num_chunks, 0, rows/num_chunks-1),

@@ -344,18 +344,49 @@ class Component:
     def BackpropNeedsOutput(self) -> bool:
         return bool(lib().kcnn_component_backprop_needs_output(self._h))
 
+    def Context(self):
+        """Component::Context(): frame offsets read per output frame."""
+        buf = (ctypes.c_int * 256)()
+        n = lib().kcnn_component_context(self._h, buf, 256)
+        if n < 0:
+            check(1)
+        return list(buf[:n])
+
+    def _span(self):
+        ctx = self.Context()
+        return ctx[-1] - ctx[0]
+
     def Propagate(self, inp, out=None, num_chunks=None):
+        """num_chunks defaults to one output frame per chunk (the input chunk
+        is that frame widened by Context(): SpliceComponent)."""
+        span = self._span()
+        if num_chunks is None:
+            num_chunks = inp.shape[0] // (span + 1)
         if out is None:
-            out = empty(inp.shape[0], self.OutputDim())
+            out = empty(inp.shape[0] - num_chunks * span, self.OutputDim())
         check(lib().kcnn_component_propagate(self._h, ptr(inp), dim(inp),
-                                             ptr(out), dim(out),
-                                             num_chunks or inp.shape[0]))
+                                             ptr(out), dim(out), num_chunks))
         return out
+
+    def NonlinearStats(self):
+        """(value_sum, deriv_sum, count) of a NonlinearComponent (fp64)."""
+        import numpy as np
+        n = self.InputDim()
+        vs, ds = np.zeros(n, np.float64), np.zeros(n, np.float64)
+        cnt = ctypes.c_double()
+        k = ctypes.c_int()
+        check(lib().kcnn_component_nonlinear_stats(
+            self._h, vs.ctypes.data_as(ctypes.c_void_p), ds.ctypes.data_as(ctypes.c_void_p),
+            n, ctypes.byref(k), ctypes.byref(cnt)))
+        return vs[:k.value], ds[:k.value], cnt.value
 
     def Backprop(self, in_value, out_value, out_deriv, in_deriv=None,
                  update=True, num_chunks=None, need_in_deriv=True):
+        span = self._span()
+        if num_chunks is None:
+            num_chunks = out_deriv.shape[0]
         if in_deriv is None and need_in_deriv:
-            in_deriv = empty(out_deriv.shape[0], self.InputDim())
+            in_deriv = empty(out_deriv.shape[0] + num_chunks * span, self.InputDim())
         if out_value is None:
             out_value = out_deriv  # dummy when BackpropNeedsOutput() is false
         if in_value is None:
@@ -364,7 +395,7 @@ class Component:
         check(lib().kcnn_component_backprop(
             self._h, ptr(in_value), dim(in_value), ptr(out_value),
             dim(out_value), ptr(out_deriv), dim(out_deriv), ptr(in_deriv), idim,
-            num_chunks or out_deriv.shape[0], int(update)))
+            num_chunks, int(update)))
         return in_deriv
 
     # parameters

@@ -34,6 +34,10 @@ struct kcnn_nnet {
   std::vector<CuMatrix<BaseFloat>> fwd;    // fwd[0] borrowed input, fwd[i+1] = out_i
   std::vector<CuMatrix<BaseFloat>> deriv;  // deriv[i] = d input_i
   int num_chunks = 0;
+  // per component: first/last frame offset of its input and output chunk
+  // (upstream Nnet::ComputeChunkInfo for contiguous contexts: the last output
+  // is one frame per chunk; each component widens its input by Context())
+  std::vector<int> in_first, in_last, out_first, out_last;
   // Conv -> channel-only Maxpool pairs run fused: routing mask of pool i
   // ([rows x OutputDim] bytes), valid for the minibatch of the last Propagate
   std::vector<unsigned char *> mask;
@@ -85,6 +89,27 @@ ChunkInfo chunk_info(int cols, int rows, int num_chunks) {
   if (num_chunks <= 0) num_chunks = rows;
   KALDI_ASSERT(rows > 0 && rows % num_chunks == 0);
   return ChunkInfo(cols, num_chunks, 0, rows / num_chunks - 1);
+}
+
+// In/out ChunkInfos of one component call: the output chunk holds frames
+// [0, out_rows/num_chunks - 1]; the input chunk is widened by the component's
+// Context() (SpliceComponent; {0} for every other component).
+void component_chunks(const Component *c, MatrixDim in_dim, MatrixDim out_dim,
+                      int num_chunks, ChunkInfo *ii, ChunkInfo *oi) {
+  const std::vector<int32> ctx = c->Context();
+  if (num_chunks <= 0) num_chunks = out_dim.rows;
+  KALDI_ASSERT(out_dim.rows > 0 && out_dim.rows % num_chunks == 0 &&
+               in_dim.rows % num_chunks == 0);
+  const int ocs = out_dim.rows / num_chunks;
+  KALDI_ASSERT(in_dim.rows / num_chunks == ocs + ctx.back() - ctx.front());
+  *oi = ChunkInfo(out_dim.cols, num_chunks, 0, ocs - 1);
+  if (ctx.front() == 0 && ctx.back() == 0) {
+    *ii = ChunkInfo(in_dim.cols, num_chunks, 0, ocs - 1);
+  } else {
+    // ChunkInfo offsets are >= 0 (Check): shift both by -ctx.front()
+    *oi = ChunkInfo(out_dim.cols, num_chunks, -ctx.front(), ocs - 1 - ctx.front());
+    *ii = ChunkInfo(in_dim.cols, num_chunks, 0, ocs - 1 + ctx.back() - ctx.front());
+  }
 }
 
 void copy_out(std::string s, char *buf, size_t len) {
@@ -346,6 +371,32 @@ int kcnn_component_info(const kcnn_component *c, char *buf, size_t len) {
 }
 int kcnn_component_input_dim(const kcnn_component *c) { return c->c->InputDim(); }
 int kcnn_component_output_dim(const kcnn_component *c) { return c->c->OutputDim(); }
+int kcnn_component_context(const kcnn_component *c, int *offsets, int max_len) {
+  int n = -1;
+  guard([&] {
+    const std::vector<int32> ctx = c->c->Context();
+    n = (int)ctx.size();
+    for (int k = 0; k < n && k < max_len; k++) offsets[k] = ctx[k];
+  });
+  return n;
+}
+int kcnn_component_nonlinear_stats(const kcnn_component *c, double *value_sum,
+                                   double *deriv_sum, int max_len, int *len,
+                                   double *count) {
+  return guard([&] {
+    auto *nl = dynamic_cast<const kaldi::nnet2::NonlinearComponent *>(c->c);
+    if (!nl) KALDI_ERR << c->c->Type() << " is not a NonlinearComponent";
+    Vector<double> v, d;
+    nl->GetValueSum(&v);
+    nl->GetDerivSum(&d);
+    *len = v.Dim();
+    for (int k = 0; k < v.Dim() && k < max_len; k++) {
+      value_sum[k] = v(k);
+      deriv_sum[k] = d(k);
+    }
+    *count = nl->Count();
+  });
+}
 int kcnn_component_backprop_needs_input(const kcnn_component *c) {
   return c->c->BackpropNeedsInput();
 }
@@ -358,8 +409,8 @@ int kcnn_component_propagate(const kcnn_component *c, const float *in,
                              int num_chunks) {
   return guard([&] {
     auto x = view(in, in_dim), y = view(out, out_dim);
-    ChunkInfo ii = chunk_info(in_dim.cols, in_dim.rows, num_chunks);
-    ChunkInfo oi = chunk_info(out_dim.cols, out_dim.rows, num_chunks);
+    ChunkInfo ii, oi;
+    component_chunks(c->c, in_dim, out_dim, num_chunks, &ii, &oi);
     c->c->Propagate(ii, oi, x, &y);
   });
 }
@@ -372,12 +423,13 @@ int kcnn_component_backprop(kcnn_component *c, const float *in_value,
   return guard([&] {
     auto x = view(in_value, in_dim), y = view(out_value, ov_dim),
          dy = view(out_deriv, od_dim);
-    ChunkInfo ii = chunk_info(in_dim.cols, in_dim.rows, num_chunks);
-    ChunkInfo oi = chunk_info(od_dim.cols, od_dim.rows, num_chunks);
+    ChunkInfo ii, oi;
+    component_chunks(c->c, in_dim, od_dim, num_chunks, &ii, &oi);
     CuMatrix<BaseFloat> dx;
     if (in_deriv) borrow(&dx, in_deriv, id_dim);
-    Component *to_update =
-        update && dynamic_cast<UpdatableComponent *>(c->c) ? c->c : nullptr;
+    // the component itself, as NnetUpdater passes it: parameters for
+    // updatable components, diagnostic stats for NonlinearComponents
+    Component *to_update = update ? c->c : nullptr;
     c->c->Backprop(ii, oi, x, y, dy, to_update, in_deriv ? &dx : nullptr);
   });
 }
@@ -490,6 +542,26 @@ kcnn_nnet *kcnn_nnet_new(const char *config) {
         KALDI_ERR << "dimension mismatch between component " << i << " ("
                   << n->comps[i]->OutputDim() << ") and " << i + 1 << " ("
                   << n->comps[i + 1]->InputDim() << ")";
+    const size_t nc = n->comps.size();
+    n->in_first.assign(nc, 0); n->in_last.assign(nc, 0);
+    n->out_first.assign(nc, 0); n->out_last.assign(nc, 0);
+    int f = 0, l = 0;
+    for (size_t k = nc; k-- > 0;) {
+      const std::vector<int32> ctx = n->comps[k]->Context();
+      for (size_t j = 1; j < ctx.size(); j++)
+        if (ctx[j] != ctx[j - 1] + 1)
+          KALDI_ERR << "component " << k << " (" << n->comps[k]->Type()
+                    << "): only contiguous contexts are supported by the runtime";
+      n->out_first[k] = f; n->out_last[k] = l;
+      f += ctx.front(); l += ctx.back();
+      n->in_first[k] = f; n->in_last[k] = l;
+    }
+    // ChunkInfo offsets must be >= 0: shift everything by -first input offset
+    const int shift = -n->in_first[0];
+    for (size_t k = 0; k < nc; k++) {
+      n->in_first[k] += shift; n->in_last[k] += shift;
+      n->out_first[k] += shift; n->out_last[k] += shift;
+    }
     for (auto *c : n->comps) n->handles.push_back(kcnn_component{c});
     n->fwd.resize(n->comps.size() + 1);
     n->deriv.resize(n->comps.size());
@@ -504,6 +576,14 @@ int kcnn_nnet_num_components(const kcnn_nnet *n) { return (int)n->comps.size(); 
 kcnn_component *kcnn_nnet_component(kcnn_nnet *n, int i) {
   if (i < 0 || i >= (int)n->handles.size()) return nullptr;
   return &n->handles[i];
+}
+
+static ChunkInfo nnet_in_info(const kcnn_nnet *n, size_t i) {
+  return ChunkInfo(n->comps[i]->InputDim(), n->num_chunks, n->in_first[i], n->in_last[i]);
+}
+static ChunkInfo nnet_out_info(const kcnn_nnet *n, size_t i) {
+  return ChunkInfo(n->comps[i]->OutputDim(), n->num_chunks, n->out_first[i],
+                   n->out_last[i]);
 }
 
 // The non-virtual Component::Propagate's sizing (nnet-component.h:203-215):
@@ -540,13 +620,16 @@ static bool propagate_pair(kcnn_nnet *n, size_t i) {
 int kcnn_nnet_propagate(kcnn_nnet *n, const float *in, MatrixDim in_dim) {
   return guard([&] {
     KALDI_ASSERT(in_dim.cols == n->comps[0]->InputDim());
+    const int in_cs = n->in_last[0] - n->in_first[0] + 1;
+    if (in_dim.rows % in_cs != 0)
+      KALDI_ERR << "input rows " << in_dim.rows << " are not a multiple of the "
+                << in_cs << "-frame input chunk";
     borrow(&n->fwd[0], in, in_dim);
-    n->num_chunks = in_dim.rows;
+    n->num_chunks = in_dim.rows / in_cs;
     std::fill(n->mask_valid.begin(), n->mask_valid.end(), 0);
     for (size_t i = 0; i < n->comps.size(); i++) {
       if (propagate_pair(n, i)) { i++; continue; }
-      ChunkInfo ii(n->comps[i]->InputDim(), n->num_chunks, 0, 0);
-      ChunkInfo oi(n->comps[i]->OutputDim(), n->num_chunks, 0, 0);
+      ChunkInfo ii = nnet_in_info(n, i), oi = nnet_out_info(n, i);
       n->comps[i]->Propagate(ii, oi, n->fwd[i], &n->fwd[i + 1]);
     }
   });
@@ -583,8 +666,7 @@ int kcnn_nnet_backprop_component(kcnn_nnet *n, int i, const float *out_deriv,
         ? view(out_deriv, od_dim)
         : CuSubMatrix<BaseFloat>(n->deriv[i + 1].Data(), n->deriv[i + 1].NumRows(),
                                  n->deriv[i + 1].NumCols(), n->deriv[i + 1].Stride());
-    ChunkInfo ii(c->InputDim(), n->num_chunks, 0, 0);
-    ChunkInfo oi(c->OutputDim(), n->num_chunks, 0, 0);
+    ChunkInfo ii = nnet_in_info(n, i), oi = nnet_out_info(n, i);
     auto *u = dynamic_cast<UpdatableComponent *>(c);
     CuMatrix<BaseFloat> *dx = &n->deriv[i];
     if (i == 0 && skip_first_dx && u) dx = nullptr;
@@ -598,7 +680,9 @@ int kcnn_nnet_backprop_component(kcnn_nnet *n, int i, const float *out_deriv,
       pool->BackpropFromMask(n->mask[i], pool->OutputDim(), od, dx);
       return;
     }
-    Component *to_update = (mode == 0 && u) ? c : nullptr;
+    // NnetUpdater passes every component as to_update: updatable ones only
+    // update in mode 0; NonlinearComponent stats (per replica) always
+    Component *to_update = (mode == 0 || !u) ? c : nullptr;
     c->Backprop(ii, oi, n->fwd[i], n->fwd[i + 1], od, to_update, dx);
   });
 }

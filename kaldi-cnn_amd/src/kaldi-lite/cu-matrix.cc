@@ -170,8 +170,9 @@ void VectorBase<Real>::Read(std::istream &is, bool binary) {
   data_.clear();
   while (is >> tok) {
     if (tok == "]") return;
-    float v;
-    if (!ConvertStringToReal(tok, &v)) KALDI_ERR << "bad vector element " << tok;
+    char *end = nullptr;
+    const double v = strtod(tok.c_str(), &end);
+    if (tok.empty() || *end != '\0') KALDI_ERR << "bad vector element " << tok;
     data_.push_back((Real)v);
   }
   KALDI_ERR << "unterminated text vector";
@@ -612,6 +613,7 @@ Real VecVec(const CuVectorBase<Real> &a, const CuVectorBase<Real> &b) {
 }
 
 template class VectorBase<float>;
+template class VectorBase<double>;
 template class MatrixBase<float>;
 template class CuMatrixBase<float>;
 template class CuMatrix<float>;

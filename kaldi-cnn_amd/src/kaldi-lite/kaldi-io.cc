@@ -85,6 +85,62 @@ void ReadBasicType(std::istream &is, bool binary, float *t) {
       KALDI_ERR << "ReadBasicType<float> failed on '" << s << "'";
   }
 }
+void WriteBasicType(std::ostream &os, bool binary, double t) {
+  if (binary) write_raw(os, t);
+  else os << std::setprecision(std::numeric_limits<double>::max_digits10) << t << " ";
+}
+void ReadBasicType(std::istream &is, bool binary, double *t) {
+  if (binary) {
+    read_raw(is, t);
+  } else {
+    std::string s;
+    is >> s;
+    char *end = nullptr;
+    *t = strtod(s.c_str(), &end);
+    if (is.fail() || s.empty() || *end != '\0')
+      KALDI_ERR << "ReadBasicType<double> failed on '" << s << "'";
+  }
+}
+void WriteIntegerVector(std::ostream &os, bool binary, const std::vector<int32> &v) {
+  if (binary) {
+    const char sz = sizeof(int32);
+    os.write(&sz, 1);
+    const int32 n = (int32)v.size();
+    os.write(reinterpret_cast<const char *>(&n), sizeof(n));
+    if (n) os.write(reinterpret_cast<const char *>(v.data()), sizeof(int32) * n);
+  } else {
+    os << "[ ";
+    for (int32 x : v) os << x << " ";
+    os << "]\n";
+  }
+  if (os.fail()) KALDI_ERR << "WriteIntegerVector: write failure";
+}
+void ReadIntegerVector(std::istream &is, bool binary, std::vector<int32> *v) {
+  v->clear();
+  if (binary) {
+    char sz = 0;
+    is.read(&sz, 1);
+    if (sz != (char)sizeof(int32))
+      KALDI_ERR << "ReadIntegerVector: expected size byte 4, got " << (int)sz;
+    int32 n = 0;
+    is.read(reinterpret_cast<char *>(&n), sizeof(n));
+    if (is.fail() || n < 0) KALDI_ERR << "ReadIntegerVector: bad size";
+    v->resize(n);
+    if (n) is.read(reinterpret_cast<char *>(v->data()), sizeof(int32) * n);
+    if (is.fail()) KALDI_ERR << "ReadIntegerVector: read failure";
+    return;
+  }
+  std::string tok;
+  is >> tok;
+  if (tok != "[") KALDI_ERR << "ReadIntegerVector: expected '[', got " << tok;
+  while (is >> tok) {
+    if (tok == "]") { is >> std::ws; return; }
+    int32 x;
+    if (!ConvertStringToInteger(tok, &x)) KALDI_ERR << "ReadIntegerVector: bad value " << tok;
+    v->push_back(x);
+  }
+  KALDI_ERR << "ReadIntegerVector: unterminated vector";
+}
 void ReadBasicType(std::istream &is, bool binary, bool *t) {
   if (!binary) is >> std::ws;
   const char c = is.peek();

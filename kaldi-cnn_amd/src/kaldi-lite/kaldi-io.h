@@ -26,6 +26,12 @@ void WriteBasicType(std::ostream &os, bool binary, bool t);
 void ReadBasicType(std::istream &is, bool binary, int32 *t);
 void ReadBasicType(std::istream &is, bool binary, float *t);
 void ReadBasicType(std::istream &is, bool binary, bool *t);
+void WriteBasicType(std::ostream &os, bool binary, double t);
+void ReadBasicType(std::istream &is, bool binary, double *t);
+// upstream base/io-funcs-inl.h WriteIntegerVector / ReadIntegerVector (int32):
+// binary = size byte, int32 count, raw values; text = "[ v1 v2 ... ]".
+void WriteIntegerVector(std::ostream &os, bool binary, const std::vector<int32> &v);
+void ReadIntegerVector(std::istream &is, bool binary, std::vector<int32> *v);
 
 // Kaldi binary-mode header "\0B" (util/kaldi-io.cc InitKaldiInputStream).
 void InitKaldiOutputStream(std::ostream &os, bool binary);

@@ -9,6 +9,7 @@
 #include "../kaldi-lite/cu-device.h"
 #include "../kaldi-lite/kaldi-io.h"
 #include "../nnet0/nnet-component-nnet0.h"
+#include "nnet-kernels.h"
 #include "parse-from-string.h"
 
 namespace kaldi {
@@ -65,6 +66,10 @@ Component *Component::NewComponentOfType(const std::string &component_type) {
     ans = new cnsl::nnet0::MaxpoolComponent();
   } else if (component_type == "FullyConnectedComponent") {
     ans = new cnsl::nnet0::FullyConnectedComponent();
+  } else if (component_type == "RectifiedLinearComponent") {
+    ans = new RectifiedLinearComponent();
+  } else if (component_type == "SpliceComponent") {
+    ans = new SpliceComponent();
   }
   return ans;
 }
@@ -399,6 +404,351 @@ void AffineComponent::UnVectorize(const VectorBase<BaseFloat> &params) {
   std::copy(params.Data() + nw, params.Data() + nw + OutputDim(), b.Data());
   linear_params_.CopyFromMat(W);
   bias_params_.CopyFromVec(b);
+}
+
+
+// ---- NonlinearComponent (reference nnet-component.cc:329-426) ---------------
+namespace {
+kcnn_stream_t NS() {
+  return reinterpret_cast<kcnn_stream_t>(CuDevice::Instantiate().Stream());
+}
+double *NewDeviceDoubles(int32 n) {
+  void *p = CuDevice::Instantiate().Malloc(sizeof(double) * (size_t)n);
+  CU_SAFE_CALL(hipMemsetAsync(p, 0, sizeof(double) * (size_t)n,
+                              CuDevice::Instantiate().Stream()));
+  return static_cast<double *>(p);
+}
+void FreeDeviceDoubles(double **p) {
+  if (*p) CuDevice::Instantiate().Free(*p);
+  *p = nullptr;
+}
+void ReadDeviceDoubles(std::istream &is, bool binary, int32 *dim, double **p) {
+  Vector<double> v;
+  v.Read(is, binary);
+  FreeDeviceDoubles(p);
+  *dim = v.Dim();
+  if (v.Dim() == 0) return;
+  *p = NewDeviceDoubles(v.Dim());
+  CU_SAFE_CALL(hipMemcpyAsync(*p, v.Data(), sizeof(double) * v.Dim(), hipMemcpyHostToDevice,
+                              CuDevice::Instantiate().Stream()));
+  CU_SAFE_CALL(hipStreamSynchronize(CuDevice::Instantiate().Stream()));
+}
+void DownloadDoubles(const double *p, int32 dim, Vector<double> *v) {
+  v->Resize(dim);
+  if (dim == 0) return;
+  CU_SAFE_CALL(hipMemcpyAsync(v->Data(), p, sizeof(double) * dim, hipMemcpyDeviceToHost,
+                              CuDevice::Instantiate().Stream()));
+  CU_SAFE_CALL(hipStreamSynchronize(CuDevice::Instantiate().Stream()));
+}
+}  // namespace
+
+NonlinearComponent::NonlinearComponent(const NonlinearComponent &other)
+    : Component(), dim_(other.dim_), stats_dim_(0), value_sum_(nullptr),
+      deriv_sum_(nullptr), count_(other.count_) {
+  if (other.stats_dim_ > 0) {
+    stats_dim_ = other.stats_dim_;
+    value_sum_ = NewDeviceDoubles(stats_dim_);
+    deriv_sum_ = NewDeviceDoubles(stats_dim_);
+    hipStream_t st = CuDevice::Instantiate().Stream();
+    CU_SAFE_CALL(hipMemcpyAsync(value_sum_, other.value_sum_, sizeof(double) * stats_dim_,
+                                hipMemcpyDeviceToDevice, st));
+    CU_SAFE_CALL(hipMemcpyAsync(deriv_sum_, other.deriv_sum_, sizeof(double) * stats_dim_,
+                                hipMemcpyDeviceToDevice, st));
+  }
+}
+
+NonlinearComponent::~NonlinearComponent() {
+  FreeDeviceDoubles(&value_sum_);
+  FreeDeviceDoubles(&deriv_sum_);
+}
+
+void NonlinearComponent::SetDim(int32 dim) {
+  KALDI_ASSERT(dim > 0);
+  dim_ = dim;
+  FreeDeviceDoubles(&value_sum_);
+  FreeDeviceDoubles(&deriv_sum_);
+  stats_dim_ = 0;
+  EnsureStats();
+  count_ = 0.0;
+}
+
+void NonlinearComponent::EnsureStats() {
+  if (stats_dim_ == dim_ && value_sum_ && deriv_sum_) return;
+  FreeDeviceDoubles(&value_sum_);
+  FreeDeviceDoubles(&deriv_sum_);
+  value_sum_ = NewDeviceDoubles(dim_);
+  deriv_sum_ = NewDeviceDoubles(dim_);
+  stats_dim_ = dim_;
+  count_ = 0.0;  // :341-352: resizing the stats restarts the count
+}
+
+void NonlinearComponent::Scale(BaseFloat scale) {
+  if (stats_dim_ > 0) {
+    CNSL_SAFE_CALL(kn_dvec_update(value_sum_, nullptr, 0.0, scale, stats_dim_, NS()));
+    CNSL_SAFE_CALL(kn_dvec_update(deriv_sum_, nullptr, 0.0, scale, stats_dim_, NS()));
+  }
+  count_ *= scale;
+}
+
+void NonlinearComponent::Add(BaseFloat alpha, const NonlinearComponent &other) {
+  if (other.stats_dim_ > 0) {
+    if (stats_dim_ == 0) {
+      const double keep = count_;
+      EnsureStats();
+      count_ = keep;
+    }
+    KALDI_ASSERT(stats_dim_ == other.stats_dim_);
+    CNSL_SAFE_CALL(kn_dvec_update(value_sum_, other.value_sum_, alpha, 1.0, stats_dim_, NS()));
+    CNSL_SAFE_CALL(kn_dvec_update(deriv_sum_, other.deriv_sum_, alpha, 1.0, stats_dim_, NS()));
+  }
+  count_ += alpha * other.count_;
+}
+
+void NonlinearComponent::GetValueSum(Vector<double> *v) const {
+  DownloadDoubles(value_sum_, stats_dim_, v);
+}
+void NonlinearComponent::GetDerivSum(Vector<double> *v) const {
+  DownloadDoubles(deriv_sum_, stats_dim_, v);
+}
+
+void NonlinearComponent::Read(std::istream &is, bool binary) {
+  std::ostringstream ostr_beg, ostr_end;
+  ostr_beg << "<" << Type() << ">";
+  ostr_end << "</" << Type() << ">";
+  ExpectOneOrTwoTokens(is, binary, ostr_beg.str(), "<Dim>");
+  ReadBasicType(is, binary, &dim_);
+  ExpectToken(is, binary, "<ValueSum>");
+  int32 vd = 0, dd = 0;
+  ReadDeviceDoubles(is, binary, &vd, &value_sum_);
+  ExpectToken(is, binary, "<DerivSum>");
+  ReadDeviceDoubles(is, binary, &dd, &deriv_sum_);
+  if (vd != dd) KALDI_ERR << Type() << ": ValueSum/DerivSum sizes differ (" << vd << ", "
+                          << dd << ")";
+  stats_dim_ = vd;
+  ExpectToken(is, binary, "<Count>");
+  ReadBasicType(is, binary, &count_);
+  ExpectToken(is, binary, ostr_end.str());
+}
+
+void NonlinearComponent::Write(std::ostream &os, bool binary) const {
+  std::ostringstream ostr_beg, ostr_end;
+  ostr_beg << "<" << Type() << ">";
+  ostr_end << "</" << Type() << ">";
+  WriteToken(os, binary, ostr_beg.str());
+  WriteToken(os, binary, "<Dim>");
+  WriteBasicType(os, binary, dim_);
+  Vector<double> v;
+  WriteToken(os, binary, "<ValueSum>");
+  GetValueSum(&v);
+  v.Write(os, binary);
+  WriteToken(os, binary, "<DerivSum>");
+  GetDerivSum(&v);
+  v.Write(os, binary);
+  WriteToken(os, binary, "<Count>");
+  WriteBasicType(os, binary, count_);
+  WriteToken(os, binary, ostr_end.str());
+}
+
+void NonlinearComponent::InitFromString(std::string args) {
+  std::string orig_args(args);
+  int32 dim;
+  bool ok = ParseFromString("dim", &args, &dim);
+  if (!ok || !args.empty() || dim <= 0)
+    KALDI_ERR << "Invalid initializer for layer of type " << Type() << ": \""
+              << orig_args << "\"";
+  Init(dim);
+}
+
+// ---- RectifiedLinearComponent (reference nnet-component.cc:799-827) ---------
+void RectifiedLinearComponent::Propagate(const ChunkInfo &in_info,
+                                         const ChunkInfo &out_info,
+                                         const CuMatrixBase<BaseFloat> &in,
+                                         CuMatrixBase<BaseFloat> *out) const {
+  in_info.CheckSize(in);
+  out_info.CheckSize(*out);
+  // out->CopyFromMat(in); out->ApplyFloor(0.0) -- one pass
+  CNSL_SAFE_CALL(kn_relu_prop(in.Data(), in.Dim(), out->Data(), out->Dim(), NS()));
+}
+
+void RectifiedLinearComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
+                                        const CuMatrixBase<BaseFloat> &,
+                                        const CuMatrixBase<BaseFloat> &out_value,
+                                        const CuMatrixBase<BaseFloat> &out_deriv,
+                                        Component *to_update,
+                                        CuMatrix<BaseFloat> *in_deriv) const {
+  in_deriv->Resize(out_deriv.NumRows(), out_deriv.NumCols(), kUndefined);
+  // CopyFromMat(out_value); ApplyHeaviside(); UpdateStats(out_value, in_deriv)
+  // on to_update; MulElements(out_deriv) -- one pass plus the stat reduction.
+  NonlinearComponent *u = to_update ? dynamic_cast<NonlinearComponent *>(to_update) : nullptr;
+  double *vs = nullptr, *ds = nullptr;
+  size_t ws_bytes = 0;
+  if (u != nullptr) {
+    KALDI_ASSERT(out_value.NumCols() == u->InputDim());
+    u->EnsureStats();
+    u->count_ += out_value.NumRows();
+    vs = u->value_sum_;
+    ds = u->deriv_sum_;
+    ws_bytes = kn_relu_stats_ws(out_deriv.Dim());
+  }
+  void *ws = ws_bytes ? CuDevice::Instantiate().Malloc(ws_bytes) : nullptr;
+  const int rc = kn_relu_backprop(out_value.Data(), out_value.Dim(), out_deriv.Data(),
+                                  out_deriv.Dim(), in_deriv->Data(), in_deriv->Dim(), vs,
+                                  ds, ws, NS());
+  if (ws) CuDevice::Instantiate().Free(ws);
+  CNSL_SAFE_CALL(rc);
+}
+
+// ---- SpliceComponent (reference nnet-component.cc:2524-2866) ----------------
+std::string SpliceComponent::Info() const {
+  std::stringstream stream;
+  std::ostringstream os;
+  for (int32 c : context_) os << c << " ";
+  stream << Component::Info() << ", context=" << os.str();
+  if (const_component_dim_ != 0)
+    stream << ", const_component_dim=" << const_component_dim_;
+  return stream.str();
+}
+
+void SpliceComponent::Init(int32 input_dim, std::vector<int32> context,
+                           int32 const_component_dim) {
+  input_dim_ = input_dim;
+  const_component_dim_ = const_component_dim;
+  context_ = context;
+  KALDI_ASSERT(context_.size() > 0);
+  KALDI_ASSERT(input_dim_ > 0 && context_.front() <= 0 && context_.back() >= 0);
+  for (size_t i = 1; i < context_.size(); i++)  // IsSortedAndUniq
+    KALDI_ASSERT(context_[i - 1] < context_[i]);
+  KALDI_ASSERT(const_component_dim_ >= 0 && const_component_dim_ < input_dim_);
+  if ((int)context_.size() > KN_SPLICE_MAX_CONTEXT)
+    KALDI_ERR << "SpliceComponent: at most " << KN_SPLICE_MAX_CONTEXT
+              << " context offsets supported, got " << context_.size();
+}
+
+void SpliceComponent::InitFromString(std::string args) {
+  std::string orig_args(args);
+  int32 input_dim, left_context, right_context;
+  std::vector<int32> context;
+  bool in_dim_ok = ParseFromString("input-dim", &args, &input_dim);
+  bool context_ok = ParseFromString("context", &args, &context);
+  bool left_right_context_ok = ParseFromString("left-context", &args, &left_context) &&
+                               ParseFromString("right-context", &args, &right_context);
+  int32 const_component_dim = 0;
+  ParseFromString("const-component-dim", &args, &const_component_dim);
+  if (!(in_dim_ok && (context_ok || left_right_context_ok)) || !args.empty() ||
+      input_dim <= 0)
+    KALDI_ERR << "Invalid initializer for layer of type " << Type() << ": \""
+              << orig_args << "\"";
+  if (left_right_context_ok) {
+    KALDI_ASSERT(context.size() == 0);
+    for (int32 i = -left_context; i <= right_context; i++) context.push_back(i);
+  }
+  Init(input_dim, context, const_component_dim);
+}
+
+int32 SpliceComponent::OutputDim() const {
+  return (input_dim_ - const_component_dim_) * (int32)context_.size() +
+         const_component_dim_;
+}
+
+namespace {
+// The splice geometry for contiguous chunk offsets (what the nnet runtime
+// builds for a contiguous context); other ChunkInfos are rejected.
+kn_splice_geom SpliceGeom(const ChunkInfo &in_info, const ChunkInfo &out_info,
+                          const std::vector<int32> &context, int32 input_dim,
+                          int32 const_dim) {
+  in_info.Check();
+  out_info.Check();
+  KALDI_ASSERT(in_info.NumChunks() == out_info.NumChunks());
+  const int32 in_cs = in_info.ChunkSize(), out_cs = out_info.ChunkSize();
+  if (out_cs <= 0)
+    KALDI_ERR << "Splicing features: output will have zero dimension. "
+              << "Probably a code error.";
+  if (in_info.GetOffset(in_cs - 1) - in_info.GetOffset(0) + 1 != in_cs ||
+      out_info.GetOffset(out_cs - 1) - out_info.GetOffset(0) + 1 != out_cs)
+    KALDI_ERR << "SpliceComponent: non-contiguous chunk offsets are not supported";
+  kn_splice_geom g;
+  g.num_chunks = in_info.NumChunks();
+  g.in_cs = in_cs;
+  g.out_cs = out_cs;
+  g.in_first = in_info.GetOffset(0);
+  g.out_first = out_info.GetOffset(0);
+  g.const_dim = const_dim;
+  g.dim = input_dim - const_dim;
+  g.num_splice = (int)context.size();
+  for (int c = 0; c < g.num_splice; c++) {
+    g.context[c] = context[c];
+    // every spliced frame must exist in the input chunk (GetIndex asserts)
+    (void)in_info.GetIndex(g.out_first + context[c]);
+    (void)in_info.GetIndex(out_info.GetOffset(out_cs - 1) + context[c]);
+  }
+  return g;
+}
+}  // namespace
+
+void SpliceComponent::Propagate(const ChunkInfo &in_info, const ChunkInfo &out_info,
+                                const CuMatrixBase<BaseFloat> &in,
+                                CuMatrixBase<BaseFloat> *out) const {
+  in_info.CheckSize(in);
+  out_info.CheckSize(*out);
+  kn_splice_geom g = SpliceGeom(in_info, out_info, context_, input_dim_,
+                                const_component_dim_);
+  CNSL_SAFE_CALL(kn_splice_prop(in.Data(), in.Dim(), out->Data(), out->Dim(), g, NS()));
+}
+
+void SpliceComponent::Backprop(const ChunkInfo &in_info, const ChunkInfo &out_info,
+                               const CuMatrixBase<BaseFloat> &,
+                               const CuMatrixBase<BaseFloat> &,
+                               const CuMatrixBase<BaseFloat> &out_deriv, Component *,
+                               CuMatrix<BaseFloat> *in_deriv) const {
+  out_info.CheckSize(out_deriv);
+  in_deriv->Resize(in_info.NumRows(), in_info.NumCols(), kUndefined);
+  KALDI_ASSERT(OutputDim() == out_deriv.NumCols());
+  kn_splice_geom g = SpliceGeom(in_info, out_info, context_, input_dim_,
+                                const_component_dim_);
+  CNSL_SAFE_CALL(kn_splice_backprop(out_deriv.Data(), out_deriv.Dim(), in_deriv->Data(),
+                                    in_deriv->Dim(), g, NS()));
+}
+
+Component *SpliceComponent::Copy() const {
+  SpliceComponent *ans = new SpliceComponent();
+  ans->input_dim_ = input_dim_;
+  ans->context_ = context_;
+  ans->const_component_dim_ = const_component_dim_;
+  return ans;
+}
+
+void SpliceComponent::Read(std::istream &is, bool binary) {
+  ExpectOneOrTwoTokens(is, binary, "<SpliceComponent>", "<InputDim>");
+  ReadBasicType(is, binary, &input_dim_);
+  std::string token;
+  ReadToken(is, false, &token);
+  if (token == "<LeftContext>") {
+    int32 left_context = 0, right_context = 0;
+    std::vector<int32> context;
+    ReadBasicType(is, binary, &left_context);
+    ExpectToken(is, binary, "<RightContext>");
+    ReadBasicType(is, binary, &right_context);
+    for (int32 i = -1 * left_context; i <= right_context; i++) context.push_back(i);
+    context_ = context;
+  } else if (token == "<Context>") {
+    ReadIntegerVector(is, binary, &context_);
+  } else {
+    KALDI_ERR << "Unknown token" << token << ", the model might be corrupted";
+  }
+  ExpectToken(is, binary, "<ConstComponentDim>");
+  ReadBasicType(is, binary, &const_component_dim_);
+  ExpectToken(is, binary, "</SpliceComponent>");
+}
+
+void SpliceComponent::Write(std::ostream &os, bool binary) const {
+  WriteToken(os, binary, "<SpliceComponent>");
+  WriteToken(os, binary, "<InputDim>");
+  WriteBasicType(os, binary, input_dim_);
+  WriteToken(os, binary, "<Context>");
+  WriteIntegerVector(os, binary, context_);
+  WriteToken(os, binary, "<ConstComponentDim>");
+  WriteBasicType(os, binary, const_component_dim_);
+  WriteToken(os, binary, "</SpliceComponent>");
 }
 
 }  // namespace nnet2

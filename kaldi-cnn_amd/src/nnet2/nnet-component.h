@@ -219,6 +219,111 @@ class AffineComponent : public UpdatableComponent {
   bool is_gradient_;
 };
 
+// ---- the upstream nnet2 components either side of the CNN path -----------
+// (SpliceComponent feeds the first convolution,
+// RectifiedLinearComponent follows each one in egs/exp/nnet/nnet.config.)
+
+// reference nnet-component.h:351-409, nnet-component.cc:329-426.  The
+// diagnostic stats live on the device as fp64 vectors, as CuVector<double>
+// does upstream; they are allocated by the first UpdateStats (or Read).
+class NonlinearComponent : public Component {
+ public:
+  void Init(int32 dim) { dim_ = dim; count_ = 0.0; }
+  explicit NonlinearComponent(int32 dim) : value_sum_(nullptr), deriv_sum_(nullptr) {
+    Init(dim);
+  }
+  NonlinearComponent() : dim_(0), stats_dim_(0), value_sum_(nullptr),
+                         deriv_sum_(nullptr), count_(0.0) {}
+  explicit NonlinearComponent(const NonlinearComponent &other);
+  virtual ~NonlinearComponent();
+  virtual int32 InputDim() const { return dim_; }
+  virtual int32 OutputDim() const { return dim_; }
+  virtual void InitFromString(std::string args);
+  virtual void Read(std::istream &is, bool binary);
+  virtual void Write(std::ostream &os, bool binary) const;
+  void Scale(BaseFloat scale);
+  void Add(BaseFloat alpha, const NonlinearComponent &other);
+  // Host copies of the stats (ValueSum()/DerivSum() upstream return the
+  // CuVector<double>); empty until the first UpdateStats.
+  void GetValueSum(Vector<double> *v) const;
+  void GetDerivSum(Vector<double> *v) const;
+  double Count() const { return count_; }
+  void SetDim(int32 dim);
+
+ protected:
+  friend class RectifiedLinearComponent;  // UpdateStats on to_update (:821)
+  // Make the fp64 stat vectors dim_ long (zeroed) if they are not.
+  void EnsureStats();
+  int32 dim_;
+  int32 stats_dim_;     // length of value_sum_/deriv_sum_ (0 = empty)
+  double *value_sum_;   // device, stats of the output
+  double *deriv_sum_;   // device, stats of the nonlinearity's derivative
+  double count_;
+
+ private:
+  const NonlinearComponent &operator=(const NonlinearComponent &other);
+};
+
+// reference nnet-component.h:676-698, nnet-component.cc:799-827.
+class RectifiedLinearComponent : public NonlinearComponent {
+ public:
+  explicit RectifiedLinearComponent(int32 dim) : NonlinearComponent(dim) {}
+  explicit RectifiedLinearComponent(const RectifiedLinearComponent &other)
+      : NonlinearComponent(other) {}
+  RectifiedLinearComponent() {}
+  virtual std::string Type() const { return "RectifiedLinearComponent"; }
+  virtual Component *Copy() const { return new RectifiedLinearComponent(*this); }
+  virtual bool BackpropNeedsInput() const { return false; }
+  virtual bool BackpropNeedsOutput() const { return true; }
+  using Component::Propagate;
+  virtual void Propagate(const ChunkInfo &in_info, const ChunkInfo &out_info,
+                         const CuMatrixBase<BaseFloat> &in,
+                         CuMatrixBase<BaseFloat> *out) const;
+  virtual void Backprop(const ChunkInfo &in_info, const ChunkInfo &out_info,
+                        const CuMatrixBase<BaseFloat> &in_value,
+                        const CuMatrixBase<BaseFloat> &out_value,
+                        const CuMatrixBase<BaseFloat> &out_deriv,
+                        Component *to_update,
+                        CuMatrix<BaseFloat> *in_deriv) const;
+
+ private:
+  RectifiedLinearComponent &operator=(const RectifiedLinearComponent &other);
+};
+
+// reference nnet-component.h:1092-1129, nnet-component.cc:2524-2866.
+class SpliceComponent : public Component {
+ public:
+  SpliceComponent() : input_dim_(0), const_component_dim_(0) {}
+  void Init(int32 input_dim, std::vector<int32> context, int32 const_component_dim = 0);
+  virtual std::string Type() const { return "SpliceComponent"; }
+  virtual std::string Info() const;
+  virtual void InitFromString(std::string args);
+  virtual int32 InputDim() const { return input_dim_; }
+  virtual int32 OutputDim() const;
+  virtual std::vector<int32> Context() const { return context_; }
+  using Component::Propagate;
+  virtual void Propagate(const ChunkInfo &in_info, const ChunkInfo &out_info,
+                         const CuMatrixBase<BaseFloat> &in,
+                         CuMatrixBase<BaseFloat> *out) const;
+  virtual void Backprop(const ChunkInfo &in_info, const ChunkInfo &out_info,
+                        const CuMatrixBase<BaseFloat> &in_value,
+                        const CuMatrixBase<BaseFloat> &out_value,
+                        const CuMatrixBase<BaseFloat> &out_deriv,
+                        Component *to_update,
+                        CuMatrix<BaseFloat> *in_deriv) const;
+  virtual bool BackpropNeedsInput() const { return false; }
+  virtual bool BackpropNeedsOutput() const { return false; }
+  virtual Component *Copy() const;
+  virtual void Read(std::istream &is, bool binary);
+  virtual void Write(std::ostream &os, bool binary) const;
+
+ private:
+  KALDI_DISALLOW_COPY_AND_ASSIGN(SpliceComponent);
+  int32 input_dim_;
+  std::vector<int32> context_;
+  int32 const_component_dim_;
+};
+
 /// Shared by the components' Read functions (nnet-component-nnet0.cc:24-39).
 void ExpectOneOrTwoTokens(std::istream &is, bool binary,
                           const std::string &token1, const std::string &token2);

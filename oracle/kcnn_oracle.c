@@ -727,3 +727,121 @@ int orc_fc_apply(orc_fc *f, const orc_mat *grad_W, const float *grad_b,
     }
   return 0;
 }
+
+/* ===========================================================================
+ * RectifiedLinearComponent (nnet2/nnet-component.cc:799-827)
+ * ======================================================================== */
+int orc_relu_propagate(const orc_mat *in, orc_mat *out) {
+  CHECK(in->rows == out->rows && in->cols == out->cols);
+  for (int i = 0; i < in->rows; i++)
+    for (int j = 0; j < in->cols; j++) {
+      float v = AT(in, i, j);          /* CopyFromMat :804 */
+      if (v < 0.0f) v = 0.0f;          /* ApplyFloor(0.0) :805 */
+      AT(out, i, j) = v;
+    }
+  return 0;
+}
+
+int orc_relu_backprop(const orc_mat *out_value, const orc_mat *out_deriv,
+                      orc_mat *in_deriv, double *value_sum, double *deriv_sum,
+                      double *count) {
+  CHECK(out_value->rows == out_deriv->rows && out_value->cols == out_deriv->cols);
+  CHECK(in_deriv->rows == out_deriv->rows && in_deriv->cols == out_deriv->cols);
+  const int R = out_value->rows, C = out_value->cols;
+  for (int i = 0; i < R; i++)          /* CopyFromMat + ApplyHeaviside :817-818 */
+    for (int j = 0; j < C; j++)
+      AT(in_deriv, i, j) = AT(out_value, i, j) > 0.0f ? 1.0f : 0.0f;
+  if (value_sum) {                     /* UpdateStats :822 -> :337-363 */
+    *count += R;
+    for (int j = 0; j < C; j++) {
+      float tv = 0.0f, td = 0.0f;      /* CuVector<BaseFloat> temp; AddRowSumMat */
+      for (int i = 0; i < R; i++) {
+        tv += AT(out_value, i, j);
+        td += AT(in_deriv, i, j);
+      }
+      value_sum[j] += (double)tv;      /* value_sum_.AddVec(1.0, temp) */
+      deriv_sum[j] += (double)td;
+    }
+  }
+  for (int i = 0; i < R; i++)          /* MulElements(out_deriv) :826 */
+    for (int j = 0; j < C; j++) AT(in_deriv, i, j) *= AT(out_deriv, i, j);
+  return 0;
+}
+
+/* ===========================================================================
+ * SpliceComponent (nnet2/nnet-component.cc:2638-2819), contiguous chunks:
+ * GetOffset(i) = first + i, GetIndex(o) = o - first (asserted in range).
+ * ======================================================================== */
+static int splice_check(int in_first, int in_cs, int out_first, int out_cs,
+                        const int *context, int num_splice) {
+  for (int c = 0; c < num_splice; c++)
+    for (int oi = 0; oi < out_cs; oi++) {
+      const int ii = out_first + oi + context[c] - in_first;   /* GetIndex */
+      if (ii < 0 || ii >= in_cs) return -1;
+    }
+  return 0;
+}
+
+int orc_splice_propagate(const orc_mat *in, orc_mat *out, int num_chunks, int in_first,
+                         int in_cs, int out_first, int out_cs, const int *context,
+                         int num_splice, int const_dim) {
+  const int input_dim = in->cols, dim = input_dim - const_dim;
+  CHECK(in->rows == num_chunks * in_cs && out->rows == num_chunks * out_cs);
+  CHECK(out->cols == dim * num_splice + const_dim);
+  CHECK(splice_check(in_first, in_cs, out_first, out_cs, context, num_splice) == 0);
+  for (int c = 0; c < num_splice; c++)                     /* :2697-2705 */
+    for (int chunk = 0; chunk < num_chunks; chunk++)
+      for (int oi = 0; oi < out_cs; oi++) {
+        const int src = chunk * in_cs + (out_first + oi + context[c] - in_first);
+        for (int d = 0; d < dim; d++)
+          AT(out, chunk * out_cs + oi, c * dim + d) = AT(in, src, d);  /* CopyRows */
+      }
+  if (const_dim != 0)                                      /* :2706-2713 */
+    for (int chunk = 0; chunk < num_chunks; chunk++)
+      for (int oi = 0; oi < out_cs; oi++)
+        for (int d = 0; d < const_dim; d++)
+          AT(out, chunk * out_cs + oi, num_splice * dim + d) =
+              AT(in, chunk * in_cs + oi, dim + d);
+  return 0;
+}
+
+int orc_splice_backprop(const orc_mat *out_deriv, orc_mat *in_deriv, int num_chunks,
+                        int in_first, int in_cs, int out_first, int out_cs,
+                        const int *context, int num_splice, int const_dim) {
+  const int input_dim = in_deriv->cols, dim = input_dim - const_dim;
+  CHECK(in_deriv->rows == num_chunks * in_cs && out_deriv->rows == num_chunks * out_cs);
+  CHECK(out_deriv->cols == dim * num_splice + const_dim);
+  CHECK(splice_check(in_first, in_cs, out_first, out_cs, context, num_splice) == 0);
+  const int R = in_deriv->rows;
+  int *idx = (int *)malloc(sizeof(int) * (size_t)R);
+  float *temp = (float *)malloc(sizeof(float) * (size_t)R * (dim > 0 ? dim : 1));
+  if (!idx || !temp) { free(idx); free(temp); return -1; }
+  for (int c = 0; c < num_splice; c++) {
+    for (int r = 0; r < R; r++) idx[r] = -1;               /* :2760-2762 */
+    for (int chunk = 0; chunk < num_chunks; chunk++)
+      for (int oi = 0; oi < out_cs; oi++) {
+        const int ii = out_first + oi + context[c] - in_first;
+        idx[chunk * in_cs + ii] = chunk * out_cs + oi;     /* :2768-2775 */
+      }
+    for (int r = 0; r < R; r++)                            /* CopyRows :2804/2806 */
+      for (int d = 0; d < dim; d++)
+        temp[(size_t)r * dim + d] = idx[r] < 0 ? 0.0f : AT(out_deriv, idx[r], c * dim + d);
+    for (int r = 0; r < R; r++)
+      for (int d = 0; d < dim; d++) {
+        if (c == 0) AT(in_deriv, r, d) = temp[(size_t)r * dim + d];
+        else AT(in_deriv, r, d) += 1.0f * temp[(size_t)r * dim + d];  /* AddMat :2807 */
+      }
+  }
+  if (const_dim != 0) {                                    /* :2810-2818 */
+    for (int r = 0; r < R; r++) idx[r] = -1;
+    for (int chunk = 0; chunk < num_chunks; chunk++)
+      for (int oi = 0; oi < out_cs; oi++) idx[chunk * in_cs + oi] = chunk * out_cs + oi;
+    for (int r = 0; r < R; r++)
+      for (int d = 0; d < const_dim; d++)
+        AT(in_deriv, r, dim + d) =
+            idx[r] < 0 ? 0.0f : AT(out_deriv, idx[r], num_splice * dim + d);
+  }
+  free(idx);
+  free(temp);
+  return 0;
+}

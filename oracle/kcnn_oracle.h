@@ -155,6 +155,27 @@ int orc_fc_gradient(const orc_fc *f, const orc_mat *in_value,
 int orc_fc_apply(orc_fc *f, const orc_mat *grad_W, const float *grad_b,
                  int num_sample);
 
+/* ---- upstream nnet2 components either side of the path ---- */
+/* RectifiedLinearComponent::Propagate (nnet2/nnet-component.cc:799-806):
+ * CopyFromMat + ApplyFloor(0) (`if (x < 0) x = 0`). */
+int orc_relu_propagate(const orc_mat *in, orc_mat *out);
+/* ::Backprop (:808-827): in_deriv = Heaviside(out_value) (x > 0 ? 1 : 0),
+ * UpdateStats (:337-363) when value_sum != NULL -- fp32 column sums of
+ * out_value and of the Heaviside matrix (row order), added to the fp64
+ * stats, count += rows -- then MulElements(out_deriv). */
+int orc_relu_backprop(const orc_mat *out_value, const orc_mat *out_deriv,
+                      orc_mat *in_deriv, double *value_sum, double *deriv_sum,
+                      double *count);
+/* SpliceComponent::Propagate/Backprop (:2638-2819) for chunk offsets
+ * [in_first, in_first + in_cs) -> [out_first, out_first + out_cs): the
+ * reference's index vectors and CopyRows / AddMat sequence, literally. */
+int orc_splice_propagate(const orc_mat *in, orc_mat *out, int num_chunks, int in_first,
+                         int in_cs, int out_first, int out_cs, const int *context,
+                         int num_splice, int const_dim);
+int orc_splice_backprop(const orc_mat *out_deriv, orc_mat *in_deriv, int num_chunks,
+                        int in_first, int in_cs, int out_first, int out_cs,
+                        const int *context, int num_splice, int const_dim);
+
 #ifdef __cplusplus
 }
 #endif

@@ -349,3 +349,72 @@ class FC:
     def apply(self, gW, gb, num_sample):
         _chk(lib().orc_fc_apply(ctypes.byref(self._c()), ctypes.byref(mat(gW)),
                                 fptr(gb), int(num_sample)))
+
+
+# ---- upstream nnet2 components either side of the path --
+@dataclass
+class ReLU:
+    """RectifiedLinearComponent (nnet2/nnet-component.cc:799-827) with its
+    NonlinearComponent stats (fp64 value_sum / deriv_sum, count)."""
+    dim: int
+    value_sum: np.ndarray = None
+    deriv_sum: np.ndarray = None
+    count: float = 0.0
+
+    def propagate(self, x):
+        out = np.zeros_like(x)
+        _chk(lib().orc_relu_propagate(ctypes.byref(mat(x)), ctypes.byref(mat(out))))
+        return out
+
+    def backprop(self, y, dy, update=True):
+        dx = np.zeros_like(dy)
+        if update and self.value_sum is None:
+            self.value_sum = np.zeros(self.dim, np.float64)
+            self.deriv_sum = np.zeros(self.dim, np.float64)
+        cnt = ctypes.c_double(self.count)
+        dp = ctypes.POINTER(ctypes.c_double)
+        vs = self.value_sum.ctypes.data_as(dp) if update else None
+        ds = self.deriv_sum.ctypes.data_as(dp) if update else None
+        _chk(lib().orc_relu_backprop(ctypes.byref(mat(y)), ctypes.byref(mat(dy)),
+                                     ctypes.byref(mat(dx)), vs, ds, ctypes.byref(cnt)))
+        self.count = cnt.value
+        return dx
+
+
+@dataclass
+class Splice:
+    """SpliceComponent (nnet2/nnet-component.cc:2524-2866); one output frame
+    per chunk by default, i.e. chunks of len(context) input frames."""
+    input_dim: int
+    context: tuple
+    const_dim: int = 0
+
+    @property
+    def output_dim(self):
+        return (self.input_dim - self.const_dim) * len(self.context) + self.const_dim
+
+    def _geom(self, num_chunks, out_cs):
+        ctx = list(self.context)
+        in_cs = out_cs + ctx[-1] - ctx[0]
+        c = (ctypes.c_int * len(ctx))(*ctx)
+        # offsets as the runtime builds them: input chunk from 0, output chunk
+        # starting at -context[0]
+        return num_chunks, 0, in_cs, -ctx[0], out_cs, c, len(ctx), self.const_dim
+
+    def propagate(self, x, num_chunks=None, out_cs=1):
+        ctx = list(self.context)
+        in_cs = out_cs + ctx[-1] - ctx[0]
+        num_chunks = num_chunks or x.shape[0] // in_cs
+        out = np.zeros((num_chunks * out_cs, self.output_dim), np.float32)
+        _chk(lib().orc_splice_propagate(ctypes.byref(mat(x)), ctypes.byref(mat(out)),
+                                        *self._geom(num_chunks, out_cs)))
+        return out
+
+    def backprop(self, dy, num_chunks=None, out_cs=1):
+        ctx = list(self.context)
+        in_cs = out_cs + ctx[-1] - ctx[0]
+        num_chunks = num_chunks or dy.shape[0] // out_cs
+        dx = np.zeros((num_chunks * in_cs, self.input_dim), np.float32)
+        _chk(lib().orc_splice_backprop(ctypes.byref(mat(dy)), ctypes.byref(mat(dx)),
+                                       *self._geom(num_chunks, out_cs)))
+        return dx

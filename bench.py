@@ -99,6 +99,42 @@ def c5_config():
     return "\n".join(lines), flop, fin
 
 
+# The reference's own model, egs/exp/nnet/nnet.config, through its last
+# FullyConnectedComponent: Splice(40, +-10) -> 6 x (Conv -> ReLU) with a
+# 1x2x1 Maxpool -> FC 1024 -> 4096 -> 4096 -> 3454 with ReLUs.  The two
+# DropoutComponents and the SoftmaxComponent are not part of this build (the
+# output derivative is synthetic, as for c2/c5), and the last FC is
+# initialised like the others (param-stddev 0.01, bias-stddev 1) instead of
+# all-zero, so no layer trains on zeros.
+NNET_CONFIG = """SpliceComponent input-dim=40 left-context=10 right-context=10 const-component-dim=0
+ConvolutionComponent in-height=40 in-width=21 in-channel=1 kernel-height=40 kernel-width=4 stride=1 group=128 out-height=1 out-width=18 learning-rate=0.02 param-stddev=0.01 bias-stddev=0.5 weight-decay=0.0005 momentum=0.9
+RectifiedLinearComponent dim=2304
+ConvolutionComponent in-height=1 in-width=18 in-channel=128 kernel-height=1 kernel-width=3 stride=1 group=128 out-height=1 out-width=16 learning-rate=0.02 param-stddev=0.01 bias-stddev=0.5 weight-decay=0.0005 momentum=0.9
+RectifiedLinearComponent dim=2048
+ConvolutionComponent in-height=1 in-width=16 in-channel=128 kernel-height=1 kernel-width=3 stride=1 group=256 out-height=1 out-width=14 learning-rate=0.02 param-stddev=0.01 bias-stddev=0.5 weight-decay=0.0005 momentum=0.9
+RectifiedLinearComponent dim=3584
+ConvolutionComponent in-height=1 in-width=14 in-channel=256 kernel-height=1 kernel-width=3 stride=1 group=256 out-height=1 out-width=12 learning-rate=0.02 param-stddev=0.01 bias-stddev=0.5 weight-decay=0.0005 momentum=0.9
+MaxpoolComponent in-height=1 in-width=12 in-channel=256 pool-height-dim=1 pool-width-dim=2 pool-channel-dim=1
+RectifiedLinearComponent dim=1536
+ConvolutionComponent in-height=1 in-width=6 in-channel=256 kernel-height=1 kernel-width=3 stride=1 group=512 out-height=1 out-width=4 learning-rate=0.02 param-stddev=0.01 bias-stddev=0.5 weight-decay=0.0005 momentum=0.9
+RectifiedLinearComponent dim=2048
+ConvolutionComponent in-height=1 in-width=4 in-channel=512 kernel-height=1 kernel-width=3 stride=1 group=512 out-height=1 out-width=2 learning-rate=0.02 param-stddev=0.01 bias-stddev=0.5 weight-decay=0.0005 momentum=0.9
+RectifiedLinearComponent dim=1024
+FullyConnectedComponent input-dim=1024 output-dim=4096 learning-rate=0.02 param-stddev=0.01 bias-stddev=1 weight-decay=0.0005 momentum=0.9
+RectifiedLinearComponent dim=4096
+FullyConnectedComponent input-dim=4096 output-dim=4096 learning-rate=0.02 param-stddev=0.01  bias-stddev=1 weight-decay=0.0005 momentum=0.9
+RectifiedLinearComponent dim=4096
+FullyConnectedComponent input-dim=4096 output-dim=3454 learning-rate=0.02 param-stddev=0.01 bias-stddev=1 weight-decay=0.0005 momentum=0.9"""
+# (H, W, C, kh, kw, G) of its convolutions, for the flop count
+NNET_CONVS = [(40, 21, 1, 40, 4, 128), (1, 18, 128, 1, 3, 128), (1, 16, 128, 1, 3, 256),
+              (1, 14, 256, 1, 3, 256), (1, 6, 256, 1, 3, 512), (1, 4, 512, 1, 3, 512)]
+
+
+def nnet_conv_flop():
+    return sum(2 * (H - kh + 1) * (W - kw + 1) * G * kh * kw * C
+               for H, W, C, kh, kw, G in NNET_CONVS)
+
+
 def parse_profile(text):
     out = {}
     for line in text.strip().splitlines():
@@ -158,8 +194,9 @@ def main():
                     help="run Conv and Maxpool as separate components")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo = rehearsal on shared GPUs")
-    ap.add_argument("--config", default="c2", choices=["c2", "c5"],
-                    help="c2 (default, BASELINE's metric) or the c5 deep stack")
+    ap.add_argument("--config", default="c2", choices=["c2", "c5", "nnet"],
+                    help="c2 (default, BASELINE's metric), the c5 deep stack, or the "
+                         "reference's egs/exp/nnet/nnet.config model")
     args = ap.parse_args()
 
     import torch
@@ -188,15 +225,20 @@ def main():
     kcnn.set_randn_seed(20261015)  # identical initial params on every replica
 
     B = args.frames_per_gpu
+    in_rows, in_cols, out_cols = B, H * W * C, FC_OUT
     if args.config == "c5":
-        text, c5_flop, _ = c5_config()
+        text, stack_flop, _ = c5_config()
         net = kcnn.Nnet(text)
+    elif args.config == "nnet":
+        net = kcnn.Nnet(NNET_CONFIG)
+        stack_flop = nnet_conv_flop()
+        in_rows, in_cols, out_cols = 21 * B, 40, 3454  # 21 spliced frames per output frame
     else:
         net = kcnn.Nnet(stack_config())
     gen = torch.Generator(device="cuda")
     gen.manual_seed(20261015 + rank)  # each rank its own shard of frames
-    x = torch.randn((B, H * W * C), generator=gen, device="cuda")
-    dy = torch.randn((B, FC_OUT), generator=gen, device="cuda") * 1e-2
+    x = torch.randn((in_rows, in_cols), generator=gen, device="cuda")
+    dy = torch.randn((B, out_cols), generator=gen, device="cuda") * 1e-2
 
     grads = kcnn_dp.gradient_buffers(
         net, lambda n: torch.empty(n, device="cuda"))
@@ -235,22 +277,28 @@ def main():
     value = frames / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
-    if args.config == "c5":
+    if args.config in ("c5", "nnet"):
         # per-scope milliseconds per step (all layers of a kind together)
         scopes = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items())}
         conv_ms = sum(v for k, v in scopes.items() if k.startswith("ConvolutionComponent"))
-        conv_flop = 3 * c5_flop * B  # fwd + dgrad + wgrad per frame
+        conv_flop = 3 * stack_flop * B  # fwd + dgrad + wgrad per frame
+        if args.config == "nnet":
+            metric = "frames/sec fwd+bwd, reference egs/exp/nnet/nnet.config model"
+            workload = ("nnet.config: Splice(40,+-10) 6x(Conv+ReLU) Maxpool(1x2x1) "
+                        "FC 1024-4096-4096-3454 (+ReLU); no Dropout/Softmax")
+        else:
+            metric = "frames/sec fwd+bwd, c5 deep Conv/Maxpool stack (BASELINE configs[4])"
+            workload = ("c5: C1(40x11x3,8x1,256) P1(3x1x4) C2(11x11x64,4x3,256) "
+                        "C3(8x9x256,3x3,pad1,256) P2(2x1x4) C4(4x9x64,4x3,256) FC(1792->1024)")
         if rank == 0:
             result = {
-                "metric": "frames/sec fwd+bwd, c5 deep Conv/Maxpool stack (BASELINE configs[4])",
+                "metric": metric,
                 "value": round(value, 1), "unit": "frames/sec", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "f32",
                 "data": "synthetic N(0,1) frames",
-                "config": {"workload": "c5: C1(40x11x3,8x1,256) P1(3x1x4) C2(11x11x64,4x3,256) "
-                                       "C3(8x9x256,3x3,pad1,256) P2(2x1x4) C4(4x9x64,4x3,256) "
-                                       "FC(1792->1024)", "frames_per_gpu": B,
+                "config": {"workload": workload, "frames_per_gpu": B,
                            "parallelism": f"dp{world}"},
                 "conv": {"ms_per_step": round(conv_ms, 4),
                          "TFLOP/s": round(conv_flop / conv_ms / 1e9, 2) if conv_ms else None,

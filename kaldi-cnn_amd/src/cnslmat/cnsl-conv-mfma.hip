@@ -906,15 +906,14 @@ int launch_wgrad2(const ConvGeom &g, const Wgrad2Plan &pl, const float *X, int x
 }
 
 // Scatter-form data gradient: worth it when the map has many more
-// positions than the output (gather waste HW/P) and the 1x1 GEMM runs on the
-// implicit-GEMM v2 kernel (Kdim a multiple of 64).
+// positions than the output (gather waste HW/P; nnet.config layer 1: 840 vs
+// 18, a 47x waste for the flipped-kernel gather).
 bool use_dgrad_scatter(const ConvGeom &g) {
   static const int enabled = [] {
     const char *e = getenv("KCNN_DGRAD_SCATTER");
     return e && *e ? atoi(e) : 1;
   }();
-  return enabled && g.Kdim >= 64 && g.Kdim % (g.Kdim > 64 ? 128 : 64) == 0 &&
-         4 * (int64_t)g.HW >= 5 * (int64_t)g.P && g.G >= 16;
+  return enabled && g.Kdim >= 32 && 4 * (int64_t)g.HW >= 5 * (int64_t)g.P && g.G >= 16;
 }
 
 size_t zbytes_pad(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -964,8 +963,10 @@ int dgrad_scatter(const ConvGeom &g, const float *dY, MatrixDim dyd,
                    zd, 1, static_cast<char *>(ws) + wt_b + z_b, ws_bytes - wt_b - z_b,
                    stream);
   if (rc) return rc;
+  // one wave per (frame, channel) pays off for long runs only (c5 C2: 864
+  // floats); short ones (nnet.config C5/C6: 12) go element-wise
   const size_t zlds = (size_t)g.kh * g.kw * g.P * 4;
-  if (zlds <= 32768) {
+  if (zlds >= 1024 && zlds <= 32768) {
     const int units = g.R * g.C;
     const bool vec = (g.kh * g.kw * g.P) % 4 == 0 && zd.stride % 4 == 0;
     hipLaunchKernelGGL(conv_col2im_plane_kernel,
@@ -1069,7 +1070,7 @@ int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
   const int wgg = g.G > 64 ? 2 : 1;
   if (ig2 && concat && (int64_t)g.R * in_dim.stride * 4 < ((int64_t)1 << 31) &&
       (int64_t)g.Kdim * kernel_dim.stride * 4 < ((int64_t)1 << 31) &&
-      g.G % (64 * wgg) == 0 && kernel_dim.stride % 4 == 0 &&
+      g.G % 4 == 0 && kernel_dim.stride % 4 == 0 &&
       (uintptr_t)kernel % 16 == 0 && (!padded || g.kh * g.kw <= 32)) {
     const int bg = 64 * wgg, bm = 64 * (4 / wgg);
     dim3 grid2((unsigned)((g.M + bm - 1) / bm), (unsigned)((g.G + bg - 1) / bg));

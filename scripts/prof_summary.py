@@ -71,12 +71,13 @@ def main():
     ap.add_argument("--steps", type=int, default=25, help="bench steps profiled (warmup+timed)")
     ap.add_argument("--cmd", default="python bench.py --steps 20 --warmup 5 --no-cpu-baseline",
                     help="the profiled command, for the report header")
+    ap.add_argument("--label", default="c2, N=4096, 1x MI355X", help="workload, for the header")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     stats = os.path.join(a.run, "prof", "run_kernel_stats.csv")
     rows = list(csv.DictReader(open(stats)))
     shutil.copy(stats, os.path.join(a.out, f"{a.tag}_kernel_stats.csv"))
-    lines = [f"# {a.tag}: rocprofv3 --kernel-trace --stats, `{a.cmd}` (c2, N=4096, 1x MI355X)", "",
+    lines = [f"# {a.tag}: rocprofv3 --kernel-trace --stats, `{a.cmd}` ({a.label})", "",
              "| kernel | calls | avg us | total ms | % |", "|---|---:|---:|---:|---:|"]
     for r in rows:
         lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} "
@@ -86,6 +87,11 @@ def main():
     fetch = pmc_means(os.path.join(a.run, "pmc_FETCH_SIZE"), "FETCH_SIZE")
     write = pmc_means(os.path.join(a.run, "pmc_WRITE_SIZE"), "WRITE_SIZE")
     traffic = {}
+    if not fetch and not write:
+        with open(os.path.join(a.out, f"{a.tag}_kernel_stats.md"), "w") as fh:
+            fh.write("\n".join(lines) + "\n")
+        print("\n".join(lines))
+        return
     lines += ["", "## HBM traffic per launch (PMC, separate passes)", "",
               "FETCH_SIZE and WRITE_SIZE are in KB; on gfx950 FETCH_SIZE counts half the bytes "
               "of 16-B/lane streaming reads, so read bytes = 2 x FETCH_SIZE x 1024.", "",

@@ -367,7 +367,10 @@ def main():
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             try:
-                traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
+                ent = json.load(open(pmc)).get(dom, {})
+                # PMC bytes are per launch of the profiled run: only for that size
+                if ent.get("frames") == B:
+                    traffic = ent.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         if dk["bound"] == "mfma":

@@ -725,16 +725,15 @@ __global__ __launch_bounds__(256) void conv_col2im_kernel(
   g.div_HW.divmod(rem, c, q);
   g.div_H.divmod(q, x, y);
   const float *zr = Z + (int64_t)n * zs + (int64_t)c * g.kh * g.kw * g.P;
+  // only the taps whose output position exists: px = x + pad_w - kx in
+  // [0, ow), py = y + pad_h - ky in [0, oh)
+  const int tx = (int)x + g.pad_w, ty = (int)y + g.pad_h;
+  const int kx0 = max(0, tx - g.ow + 1), kx1 = min(g.kw - 1, tx);
+  const int ky0 = max(0, ty - g.oh + 1), ky1 = min(g.kh - 1, ty);
   float sum = 0.0f;
-  for (int kx = 0; kx < g.kw; kx++) {
-    const int px = (int)x - kx + g.pad_w;
-    if ((unsigned)px >= (unsigned)g.ow) continue;
-    for (int ky = 0; ky < g.kh; ky++) {
-      const int py = (int)y - ky + g.pad_h;
-      if ((unsigned)py >= (unsigned)g.oh) continue;
-      sum += zr[(int64_t)(kx * g.kh + ky) * g.P + px * g.oh + py];
-    }
-  }
+  for (int kx = kx0; kx <= kx1; kx++)
+    for (int ky = ky0; ky <= ky1; ky++)
+      sum += zr[(int64_t)(kx * g.kh + ky) * g.P + (tx - kx) * g.oh + (ty - ky)];
   dX[(int64_t)n * dxs + rem] = sum;
 }
 
@@ -763,16 +762,13 @@ __global__ __launch_bounds__(64) void conv_col2im_plane_kernel(
     for (int qd = lane; qd < g.HW; qd += 64) {
       uint32_t x, y;
       g.div_H.divmod((uint32_t)qd, x, y);
+      const int tx = (int)x + g.pad_w, ty = (int)y + g.pad_h;
+      const int kx0 = max(0, tx - g.ow + 1), kx1 = min(g.kw - 1, tx);
+      const int ky0 = max(0, ty - g.oh + 1), ky1 = min(g.kh - 1, ty);
       float sum = 0.0f;
-      for (int kx = 0; kx < g.kw; kx++) {
-        const int px = (int)x - kx + g.pad_w;
-        if ((unsigned)px >= (unsigned)g.ow) continue;
-        for (int ky = 0; ky < g.kh; ky++) {
-          const int py = (int)y - ky + g.pad_h;
-          if ((unsigned)py >= (unsigned)g.oh) continue;
-          sum += zp[(kx * g.kh + ky) * g.P + px * g.oh + py];
-        }
-      }
+      for (int kx = kx0; kx <= kx1; kx++)
+        for (int ky = ky0; ky <= ky1; ky++)
+          sum += zp[(kx * g.kh + ky) * g.P + (tx - kx) * g.oh + (ty - ky)];
       dst[qd] = sum;
     }
     __syncthreads();

@@ -561,7 +561,9 @@ bool env_pool_direct();
 // pc maps fits the LDS budget; 16-B copies when the runs are aligned.
 bool pool_plane_ok(int in_cols, int H, int W, int ph, int pw, int pc, int mode,
                    int64_t rows) {
-  return mode == 0 && (ph > 1 || pw > 1) && H % ph == 0 && W % pw == 0 &&
+  // a wave per run pays off for runs of >= 256 floats (c5 P1: 1452, P2: 288;
+  // nnet.config's 1x2x1 pool has 12-float runs and goes element-wise)
+  return mode == 0 && (ph > 1 || pw > 1) && H % ph == 0 && W % pw == 0 && pc * H * W >= 256 &&
          in_cols % (pc * H * W) == 0 && (size_t)(pc * H * W + 2 * (H / ph) * (W / pw)) * 4 <= 32768 &&
          rows * (in_cols / (pc * H * W)) < ((int64_t)1 << 31) && env_pool_direct();
 }

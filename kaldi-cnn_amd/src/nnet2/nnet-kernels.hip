@@ -56,6 +56,7 @@ __global__ __launch_bounds__(256) void relu_stats_final_kernel(
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= cols) return;
   float sv = 0.0f, sh = 0.0f;  // CuVector<BaseFloat> temp (:355-361)
+#pragma unroll 16
   for (int p = 0; p < nparts; p++) {
     sv += part_v[(int64_t)p * cols + c];
     sh += part_h[(int64_t)p * cols + c];

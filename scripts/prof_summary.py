@@ -72,6 +72,7 @@ def main():
     ap.add_argument("--cmd", default="python bench.py --steps 20 --warmup 5 --no-cpu-baseline",
                     help="the profiled command, for the report header")
     ap.add_argument("--label", default="c2, N=4096, 1x MI355X", help="workload, for the header")
+    ap.add_argument("--frames", type=int, default=4096, help="frames per launch of the run")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     stats = os.path.join(a.run, "prof", "run_kernel_stats.csv")
@@ -112,6 +113,7 @@ def main():
         for v in traffic.values():
             v["hbm_bytes_per_launch"] = round(v["hbm_bytes_per_launch"])
             v["run"] = a.tag
+            v["frames"] = a.frames
         path = os.path.join(a.out, "pmc_traffic.json")
         merged = json.load(open(path)) if os.path.exists(path) else {}
         merged.update(traffic)  # kernels of several runs (fused / unfused)

@@ -36,6 +36,8 @@ CONVS = {
     # implicit-GEMM v2 with its im2col-row table: Kdim not a multiple of 16
     "ig2_tail_g64": (6, 7, 9, 3, 3, 64, 1, 1),          # Kdim 81, one 64-filter tile
     "ig2_tail_g128": (5, 6, 11, 3, 3, 128, 1, 0),       # Kdim 99, pad on one axis
+    # scatter-form data gradient (HW >= 1.25 P) on a padded map
+    "scatter_pad": (12, 10, 4, 5, 5, 32, 1, 1),          # HW 120, P 80, Kdim 100
 }
 
 
@@ -222,6 +224,7 @@ def test_conv_update_divides_by_local_rows(kc):
     (33, 11, 256, 3, 1, 4, False, False),   # c5 P1 (3-D window, 16-B gather kernel)
     (3, 2, 8, 3, 2, 2, False, False),       # 4-element groups wrap h -> w -> c
     (6, 5, 3, 2, 5, 3, False, False),       # row length 90: not a multiple of 4
+    (9, 5, 12, 3, 5, 6, False, False),      # plane kernel, 270-float runs (no 16-B)
 ])
 def test_maxpool_component(kc, path, cfg):
     H, W, C, ph, pw, pc, ov, ov2 = cfg

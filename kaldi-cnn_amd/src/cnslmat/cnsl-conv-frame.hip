@@ -1143,8 +1143,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_frame_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Deterministic reduction of S partial rows: pass 1 sums groups of 32 rows,
-// pass 2 sums the groups in order.
+// Pass 1 of the implicit-GEMM v1 split-K reduction: sums groups of 32
+// partial rows (conv_splitk_reduce_kernel adds the groups in order).
 __global__ __launch_bounds__(256) void reduce_pass1(const float *__restrict__ in,
                                                     int S, int E,
                                                     float *__restrict__ tmp) {
@@ -1156,24 +1156,40 @@ __global__ __launch_bounds__(256) void reduce_pass1(const float *__restrict__ in
   tmp[(int64_t)blockIdx.y * E + e] = acc;
 }
 
-// out mapping: e < nw -> gW[row][col] with (row, col) = gk_layout ?
+// One-pass deterministic reduction of S partial rows [S][E]: a block takes 64
+// columns; its 4 waves sum interleaved rows (s = w, w + 4, ...) with the loads
+// of 16 rows in flight, then add the 4 wave sums in order through LDS.  Same
+// output mapping: e < nw -> gW[row][col] with (row, col) = gk_layout ?
 // (e % inner, e / inner) : (e / inner, e % inner); e >= nw -> gb[e - nw].
-__global__ __launch_bounds__(256) void reduce_pass2(const float *__restrict__ tmp,
-                                                    int Q, int E, int nw,
-                                                    int inner, int gk_layout,
-                                                    float *__restrict__ gW,
-                                                    int gws,
-                                                    float *__restrict__ gb) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= E) return;
+// (Two passes of 32-row groups spent ~14 us of latency at c2, for 3.3 MB.)
+__global__ __launch_bounds__(256) void reduce_splits_kernel(
+    const float *__restrict__ in, int S, int E, int nw, int inner, int gk_layout,
+    float *__restrict__ gW, int gws, float *__restrict__ gb) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + c;
   float acc = 0.0f;
-  for (int q = 0; q < Q; q++) acc += tmp[(int64_t)q * E + e];
+  if (e < E) {
+    int s = w;
+    for (; s + 4 * 15 < S; s += 64) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++) v[u] = in[(int64_t)(s + 4 * u) * E + e];
+#pragma unroll
+      for (int u = 0; u < 16; u++) acc += v[u];
+    }
+    for (; s < S; s += 4) acc += in[(int64_t)s * E + e];
+  }
+  red[w][c] = acc;
+  __syncthreads();
+  if (w != 0 || e >= E) return;
+  const float sum = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
   if (e < nw) {
     const int a = e / inner, b = e - a * inner;
     const int row = gk_layout ? b : a, col = gk_layout ? a : b;
-    gW[(int64_t)row * gws + col] = acc;
+    gW[(int64_t)row * gws + col] = sum;
   } else if (gb) {
-    gb[e - nw] = acc;
+    gb[e - nw] = sum;
   }
 }
 
@@ -1354,11 +1370,9 @@ int kcnn_conv_wgrad_frame(const ConvGeom &g, const float *X, int xs,
                        g, X, xs, dY, dys, part);
   int rc = (int)hipGetLastError();
   if (rc) return rc;
-  const int Q = (S + 31) / 32;
-  hipLaunchKernelGGL(reduce_pass1, dim3((E + 255) / 256, Q), dim3(256), 0, st,
-                     part, S, E, tmp);
-  hipLaunchKernelGGL(reduce_pass2, dim3((E + 255) / 256), dim3(256), 0, st, tmp,
-                     Q, E, g.Kdim * g.G, g.G, 0, gW, gws, gb);
+  (void)tmp;
+  hipLaunchKernelGGL(reduce_splits_kernel, dim3((E + 63) / 64), dim3(256), 0, st, part, S,
+                     E, g.Kdim * g.G, g.G, 0, gW, gws, gb);
   return (int)hipGetLastError();
 }
 
@@ -1483,11 +1497,9 @@ static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
   int rc = (int)hipGetLastError();
   if (rc || gW == nullptr) return rc;
   float *tmp = part + (size_t)S * E;
-  const int Q = (S + 31) / 32;
-  hipLaunchKernelGGL(reduce_pass1, dim3((E + 255) / 256, Q), dim3(256), 0, st,
-                     part, S, E, tmp);
-  hipLaunchKernelGGL(reduce_pass2, dim3((E + 255) / 256), dim3(256), 0, st, tmp,
-                     Q, E, g.Kdim * g.G, g.G, 0, gW, gws, gb);
+  (void)tmp;
+  hipLaunchKernelGGL(reduce_splits_kernel, dim3((E + 63) / 64), dim3(256), 0, st, part, S,
+                     E, g.Kdim * g.G, g.G, 0, gW, gws, gb);
   return (int)hipGetLastError();
 }
 
@@ -1525,16 +1537,14 @@ size_t kcnn_reduce_splits_ws(int S, int E) {
   return (size_t)((S + 31) / 32) * (size_t)E * 4;
 }
 
-// Generic: in [S][E] -> tmp [Q][E] -> out (with the gW/gb mapping of the
-// implicit-GEMM wgrad: e = g*Kdim + k for e < G*Kdim).
+// Generic: in [S][E] -> out (with the gW/gb mapping of the implicit-GEMM
+// wgrad: e = g*Kdim + k for e < G*Kdim); tmp is unused (one pass).
 int kcnn_reduce_splits_wgrad(const float *in, int S, int E, float *tmp, int nw,
                              int inner, float *gW, int gws, float *gb,
                              hipStream_t st) {
-  const int Q = (S + 31) / 32;
-  hipLaunchKernelGGL(reduce_pass1, dim3((E + 255) / 256, Q), dim3(256), 0, st,
-                     in, S, E, tmp);
-  hipLaunchKernelGGL(reduce_pass2, dim3((E + 255) / 256), dim3(256), 0, st, tmp,
-                     Q, E, nw, inner, 1, gW, gws, gb);
+  (void)tmp;
+  hipLaunchKernelGGL(reduce_splits_kernel, dim3((E + 63) / 64), dim3(256), 0, st, in, S, E,
+                     nw, inner, 1, gW, gws, gb);
   return (int)hipGetLastError();
 }
 
@@ -1548,10 +1558,8 @@ int kcnn_reduce_splits_pass1(const float *in, int S, int E, float *tmp,
 
 int kcnn_reduce_splits(const float *in, int S, int E, float *tmp, float *out,
                        hipStream_t st) {
-  const int Q = (S + 31) / 32;
-  hipLaunchKernelGGL(reduce_pass1, dim3((E + 255) / 256, Q), dim3(256), 0, st,
-                     in, S, E, tmp);
-  hipLaunchKernelGGL(reduce_pass2, dim3((E + 255) / 256), dim3(256), 0, st, tmp,
-                     Q, E, E, E, 0, out, 0, nullptr);
+  (void)tmp;
+  hipLaunchKernelGGL(reduce_splits_kernel, dim3((E + 63) / 64), dim3(256), 0, st, in, S, E,
+                     E, E, 0, out, 0, nullptr);
   return (int)hipGetLastError();
 }

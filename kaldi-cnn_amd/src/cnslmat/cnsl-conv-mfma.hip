@@ -527,6 +527,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(
 // for the offset and two ops for the tap mask (padded maps only); per dY
 // element one add.  Steps are double-buffered in LDS, one barrier each.
 // Bias gradient: the k-tile-0 blocks also sum their dY values (fixed order).
+// A last, partial filter tile reads rows past G (the next frame's values, or
+// zeros past the descriptor's range): they only reach accumulator rows that
+// are never stored.
 // Partials go to ws[split][e] (e = g*Kdim + k, then G bias entries) and are
 // reduced in a fixed order (kcnn_reduce_splits_wgrad): deterministic.
 constexpr int W2_BG = 128, W2_BK = 128, W2_LD = 129;
@@ -542,7 +545,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad2_kernel(
   const int nb8 = (nblocks + 7) >> 3;
   const int bid = (int)(blockIdx.x & 7) * nb8 + (int)(blockIdx.x >> 3);
   if (bid >= nblocks) return;
-  const int ntiles = ktiles * (g.G / W2_BG);
+  const int ntiles = ktiles * ((g.G + W2_BG - 1) / W2_BG);
   const int split = bid / ntiles, tile = bid - split * ntiles;
   const int k0 = (tile % ktiles) * W2_BK, g0 = (tile / ktiles) * W2_BG;
   const int nbeg = split * fps;
@@ -677,7 +680,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad2_kernel(
 #pragma unroll
       for (int r = 0; r < 16; r++) {
         const int gg = g0 + wg * 64 + 32 * a + kcnn::mfma32_row(r, lane);
-        wsp[(int64_t)gg * g.Kdim + kk] = acc[a][b][r];
+        if (gg < g.G) wsp[(int64_t)gg * g.Kdim + kk] = acc[a][b][r];
       }
   }
   if (do_bias) {
@@ -688,7 +691,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad2_kernel(
     if (tid < W2_BG) {
       float s = 0.0f;
       for (int i = 0; i < 32; i++) s += red[tid * 33 + i];
-      wsp[(int64_t)g.G * g.Kdim + g0 + tid] = s;
+      if (g0 + tid < g.G) wsp[(int64_t)g.G * g.Kdim + g0 + tid] = s;
     }
   }
 }
@@ -846,7 +849,7 @@ bool plan_wgrad2(const ConvGeom &g, int xs, int dys, Wgrad2Plan &pl) {
     const char *e = getenv("KCNN_WGRAD2");
     return e && *e ? atoi(e) : 1;
   }();
-  if (!enabled || g.R <= 0 || g.G % W2_BG != 0 || g.P > 96 || g.Kdim < 32)
+  if (!enabled || g.R <= 0 || g.G < 32 || g.P > 96 || g.Kdim < 32)
     return false;
   pl.fpc = g.P <= 16 ? 32 / g.P : 1;
   pl.nch = g.P <= 32 ? 1 : (g.P + 31) / 32;
@@ -858,7 +861,7 @@ bool plan_wgrad2(const ConvGeom &g, int xs, int dys, Wgrad2Plan &pl) {
       (int64_t)g.G * g.P * 4 >= 0x7f000000)
     return false;
   pl.ktiles = (g.Kdim + W2_BK - 1) / W2_BK;
-  const int ntiles = pl.ktiles * (g.G / W2_BG);
+  const int ntiles = pl.ktiles * ((g.G + W2_BG - 1) / W2_BG);
   const int64_t chain = (int64_t)g.R * g.P;
   int s0 = (int)((chain + 8191) / 8192);
   if (s0 < 1) s0 = 1;

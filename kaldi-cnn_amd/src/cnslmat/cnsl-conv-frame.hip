@@ -21,6 +21,8 @@
 //            falls out of the same MFMAs.  Per-workgroup partials are reduced
 //            in a fixed order (deterministic).
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -1197,6 +1199,14 @@ size_t fwd_lds(const ConvGeom &g, int Kpad, int Gp) {
   return (size_t)align16(Kpad * 8) + (size_t)Kpad * Gp * 4 + (size_t)g.C * g.HW * 4;
 }
 
+// conv_fwd_regs_kernel: 3 resident blocks per CU when their LDS fits (c2:
+// 52 KB each; VGPRs allow 3).  The third block overlaps the others' store
+// and barrier phases: c2 forward+pool 224 -> 200 us, although 4096 frames
+// then split 5/6 per block instead of 8.
+int fwd_regs_blocks_per_cu(size_t lds) {
+  return lds * 3 <= 160 * 1024 ? 3 : 2;
+}
+
 unsigned frame_grid(const ConvGeom &g, int blocks_per_cu) {
   int64_t b = 256LL * blocks_per_cu;
   if (b > g.R) b = g.R;
@@ -1234,7 +1244,7 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
     if (lds <= (size_t)kFrameLdsMax) {
       const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0);
       const int ksn = (g.Kdim + 1) / 2;
-      const unsigned grid = frame_grid(g, 2);
+      const unsigned grid = frame_grid(g, fwd_regs_blocks_per_cu(lds));
 #define KCNN_FWD_REGS(KS_)                                                         \
   hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, 0>), dim3(grid), dim3(256), lds, st, \
                      g, X, xs, K, ks, bias, out, os, vec_ok, dbg, nullptr, 0, nullptr, 0)
@@ -1305,7 +1315,9 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
   if (lds > (size_t)kFrameLdsMax) return -1;
   const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0);
   const int ksn = (g.Kdim + 1) / 2;
-  const unsigned grid = frame_grid(g, 2);
+  static const int grid_env = env_int("KCNN_FWD_GRID", 0);  // timing experiments
+  const unsigned grid = grid_env > 0 ? (unsigned)std::min<int64_t>(grid_env, g.R)
+                                     : frame_grid(g, fwd_regs_blocks_per_cu(lds));
 #define KCNN_FWD_POOL(KS_, PC_)                                                       \
   hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_>), dim3(grid), dim3(256), lds, \
                      st, g, X, xs, K, ks, bias, out, os, vec_ok, 0, pool, ps, mask, ms)

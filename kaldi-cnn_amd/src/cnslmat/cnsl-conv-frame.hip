@@ -1244,7 +1244,8 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
     if (lds <= (size_t)kFrameLdsMax) {
       const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0);
       const int ksn = (g.Kdim + 1) / 2;
-      const unsigned grid = frame_grid(g, fwd_regs_blocks_per_cu(lds));
+      static const int bpc_env = env_int("KCNN_FWD_BPC", 0);  // timing experiments
+      const unsigned grid = frame_grid(g, bpc_env > 0 ? bpc_env : fwd_regs_blocks_per_cu(lds));
 #define KCNN_FWD_REGS(KS_)                                                         \
   hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, 0>), dim3(grid), dim3(256), lds, st, \
                      g, X, xs, K, ks, bias, out, os, vec_ok, dbg, nullptr, 0, nullptr, 0)

@@ -570,6 +570,173 @@ bool pool_plane_ok(int in_cols, int H, int W, int ph, int pw, int pc, int mode,
 
 unsigned plane_grid(int units) { return (unsigned)(units < 256 * 24 ? units : 256 * 24); }
 
+// Intermap pooling (reference cnsl-cu-kernels.cu:310-503)
+// as channel streams: a thread owns one (row, map position) -- lanes along
+// the position, so every access is a coalesced row segment -- and walks the
+// channels in order with the last PC values in registers.  Each input, pool
+// value and derivative is read once (overlap2D: once per output-grid row
+// that uses it, from L2).  Same comparisons, start value and summation
+// order as the element-wise forms (A.10; backprop in the gather form of B2,
+// increasing output channel, from 0).
+template <int PC>
+__global__ __launch_bounds__(256) void maxpool_overlap_prop_kernel(
+    const float *__restrict__ x, int64_t xs, float *__restrict__ y, int64_t ys, int rows,
+    int plane, int C) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)rows * plane) return;
+  const int r = (int)(t / plane), pos = (int)(t - (int64_t)r * plane);
+  const float *xr = x + (int64_t)r * xs + pos;
+  float *yr = y + (int64_t)r * ys + pos;
+  float ring[PC];
+#pragma unroll
+  for (int k = 0; k < PC - 1; k++) ring[k + 1] = xr[(int64_t)k * plane];
+#pragma unroll 4
+  for (int oc = 0; oc + PC - 1 < C; oc++) {
+#pragma unroll
+    for (int k = 0; k < PC - 1; k++) ring[k] = ring[k + 1];
+    ring[PC - 1] = xr[(int64_t)(oc + PC - 1) * plane];
+    float val = -1e20f;
+#pragma unroll
+    for (int k = 0; k < PC; k++)
+      if (val < ring[k]) val = ring[k];
+    yr[(int64_t)oc * plane] = val;
+  }
+}
+
+template <int PC>
+__global__ __launch_bounds__(256) void maxpool_overlap_backprop_kernel(
+    const float *__restrict__ x, int64_t xs, const float *__restrict__ y, int64_t ys,
+    const float *__restrict__ dy, int64_t dys, float *__restrict__ dx, int64_t dxs,
+    int rows, int plane, int C, int write_all) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)rows * plane) return;
+  const int r = (int)(t / plane), pos = (int)(t - (int64_t)r * plane);
+  const int OC = C - PC + 1;
+  const float *xr = x + (int64_t)r * xs + pos;
+  const float *yr = y + (int64_t)r * ys + pos;
+  const float *er = dy + (int64_t)r * dys + pos;  // own stride (B14)
+  float *dr = dx + (int64_t)r * dxs + pos;
+  // ring slot k holds output channel c - (PC-1) + k (invalid: NaN never matches)
+  float ov[PC], ev[PC];
+#pragma unroll
+  for (int k = 0; k < PC; k++) { ov[k] = __builtin_nanf(""); ev[k] = 0.0f; }
+#pragma unroll 4
+  for (int c = 0; c < C; c++) {
+#pragma unroll
+    for (int k = 0; k < PC - 1; k++) { ov[k] = ov[k + 1]; ev[k] = ev[k + 1]; }
+    if (c < OC) {
+      ov[PC - 1] = yr[(int64_t)c * plane];
+      ev[PC - 1] = er[(int64_t)c * plane];
+    } else {
+      ov[PC - 1] = __builtin_nanf("");
+      ev[PC - 1] = 0.0f;
+    }
+    const float xv = xr[(int64_t)c * plane];
+    float acc = 0.0f;
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < PC; k++)
+      if (xv == ov[k]) { acc += ev[k]; any = true; }
+    if (write_all) dr[(int64_t)c * plane] = acc;
+    else if (any) dr[(int64_t)c * plane] += acc;
+  }
+}
+
+// overlap2D: channels form an in2 x in2 grid, outputs an o2 x o2 grid
+// (o2 = in2 - PC + 1); output (ox, oy) = max over input (ox+cx, oy+cy).
+// A thread owns (row, position, output-grid row ox).
+template <int PC>
+__global__ __launch_bounds__(256) void maxpool_overlap2d_prop_kernel(
+    const float *__restrict__ x, int64_t xs, float *__restrict__ y, int64_t ys, int rows,
+    int plane, int o2) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t per = (int64_t)plane * o2;
+  if (t >= (int64_t)rows * per) return;
+  const int r = (int)(t / per);
+  const int rem = (int)(t - (int64_t)r * per);
+  const int ox = rem / plane, pos = rem - ox * plane;
+  const int in2 = o2 + PC - 1;
+  const float *xr = x + (int64_t)r * xs + pos;
+  float *yr = y + (int64_t)r * ys + pos;
+  // col[cy][cx] = input (ox + cx, oy + cy): a ring of PC grid columns, one
+  // new column per output (each input read once by this thread)
+  float col[PC][PC];
+#pragma unroll
+  for (int cy = 1; cy < PC; cy++)
+#pragma unroll
+    for (int cx = 0; cx < PC; cx++)
+      col[cy][cx] = xr[(int64_t)((ox + cx) * in2 + cy - 1) * plane];
+  for (int oy = 0; oy < o2; oy++) {
+#pragma unroll
+    for (int cy = 0; cy < PC - 1; cy++)
+#pragma unroll
+      for (int cx = 0; cx < PC; cx++) col[cy][cx] = col[cy + 1][cx];
+#pragma unroll
+    for (int cx = 0; cx < PC; cx++)
+      col[PC - 1][cx] = xr[(int64_t)((ox + cx) * in2 + oy + PC - 1) * plane];
+    float val = -1e20f;
+#pragma unroll
+    for (int cx = 0; cx < PC; cx++)
+#pragma unroll
+      for (int cy = 0; cy < PC; cy++)
+        if (val < col[cy][cx]) val = col[cy][cx];
+    yr[(int64_t)(ox * o2 + oy) * plane] = val;
+  }
+}
+
+// A thread owns (row, position, input-grid row X) and sums, for each input
+// (X, Y), the outputs (xo, yo) whose window holds it, xo then yo increasing.
+template <int PC>
+__global__ __launch_bounds__(256) void maxpool_overlap2d_backprop_kernel(
+    const float *__restrict__ x, int64_t xs, const float *__restrict__ y, int64_t ys,
+    const float *__restrict__ dy, int64_t dys, float *__restrict__ dx, int64_t dxs,
+    int rows, int plane, int o2, int write_all) {
+  const int in2 = o2 + PC - 1;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t per = (int64_t)plane * in2;
+  if (t >= (int64_t)rows * per) return;
+  const int r = (int)(t / per);
+  const int rem = (int)(t - (int64_t)r * per);
+  const int X = rem / plane, pos = rem - X * plane;
+  const float *xr = x + (int64_t)r * xs + pos;
+  const float *yr = y + (int64_t)r * ys + pos;
+  const float *er = dy + (int64_t)r * dys + pos;
+  float *dr = dx + (int64_t)r * dxs + pos;
+  // ring [a][b]: output (X - a, Y - b); a new column yo = Y enters per step
+  // (NaN: no such output, never equal)
+  float ov[PC][PC], ev[PC][PC];
+#pragma unroll
+  for (int a = 0; a < PC; a++)
+#pragma unroll
+    for (int b = 0; b < PC; b++) { ov[a][b] = __builtin_nanf(""); ev[a][b] = 0.0f; }
+  for (int Y = 0; Y < in2; Y++) {
+#pragma unroll
+    for (int a = 0; a < PC; a++) {
+#pragma unroll
+      for (int b = PC - 1; b > 0; b--) { ov[a][b] = ov[a][b - 1]; ev[a][b] = ev[a][b - 1]; }
+      const int xo = X - a;
+      if (xo >= 0 && xo < o2 && Y < o2) {
+        const int64_t j = (int64_t)(xo * o2 + Y) * plane;
+        ov[a][0] = yr[j];
+        ev[a][0] = er[j];
+      } else {
+        ov[a][0] = __builtin_nanf("");
+        ev[a][0] = 0.0f;
+      }
+    }
+    const float xv = xr[(int64_t)(X * in2 + Y) * plane];
+    float acc = 0.0f;
+    bool any = false;
+#pragma unroll
+    for (int a = PC - 1; a >= 0; a--)      // xo = X - a, increasing
+#pragma unroll
+      for (int b = PC - 1; b >= 0; b--)    // yo = Y - b, increasing
+        if (xv == ov[a][b]) { acc += ev[a][b]; any = true; }
+    if (write_all) dr[(int64_t)(X * in2 + Y) * plane] = acc;
+    else if (any) dr[(int64_t)(X * in2 + Y) * plane] += acc;
+  }
+}
+
 // Backprop of the channel-only pool from the routing mask saved by the fused
 // forward (hipF_conv2d_maxpool): dX[(PC j + c) plane + q] = bit c of
 // mask[j plane + q] ? dP[j plane + q] : 0 -- the same values A.9 produces
@@ -901,6 +1068,36 @@ int hipF_maxpool_prop(const float *src, MatrixDim src_dim, float *pool,
                        (int64_t)pool_dim.stride, pg);
     return kcnn::launch_status();
   }
+  if (mode != 0 && pool_channel_dim >= 2 && pool_channel_dim <= 4 && env_pool_direct()) {
+    if (pool_dim.rows == 0 || plane == 0) return 0;
+    const int C = src_dim.cols / plane;
+    hipStream_t st = kcnn::as_stream(stream);
+    if (mode == 1 && pool_dim.cols == (C - pool_channel_dim + 1) * plane) {
+      const int64_t n = (int64_t)pool_dim.rows * plane;
+      const unsigned blocks = (unsigned)((n + 255) / 256);
+#define KCNN_OVP(PC_)                                                                       \
+  hipLaunchKernelGGL(maxpool_overlap_prop_kernel<PC_>, dim3(blocks), dim3(256), 0, st, src, \
+                     (int64_t)src_dim.stride, pool, (int64_t)pool_dim.stride, pool_dim.rows, \
+                     plane, C)
+      if (pool_channel_dim == 2) KCNN_OVP(2); else if (pool_channel_dim == 3) KCNN_OVP(3); else KCNN_OVP(4);
+#undef KCNN_OVP
+      return kcnn::launch_status();
+    }
+    PoolGeom g2 = make_pool_geom(in_height, in_width, 1, 1, pool_channel_dim, mode,
+                                 pool_dim.cols);
+    if (mode == 2 && g2.in_2d * g2.in_2d * plane <= src_dim.cols &&
+        pool_dim.cols == g2.out_2d * g2.out_2d * plane) {
+      const int64_t n = (int64_t)pool_dim.rows * plane * g2.out_2d;
+      const unsigned blocks = (unsigned)((n + 255) / 256);
+#define KCNN_OV2P(PC_)                                                                        \
+  hipLaunchKernelGGL(maxpool_overlap2d_prop_kernel<PC_>, dim3(blocks), dim3(256), 0, st, src, \
+                     (int64_t)src_dim.stride, pool, (int64_t)pool_dim.stride, pool_dim.rows,   \
+                     plane, g2.out_2d)
+      if (pool_channel_dim == 2) KCNN_OV2P(2); else if (pool_channel_dim == 3) KCNN_OV2P(3); else KCNN_OV2P(4);
+#undef KCNN_OV2P
+      return kcnn::launch_status();
+    }
+  }
   PoolGeom g = make_pool_geom(in_height, in_width, pool_height_dim,
                               pool_width_dim, pool_channel_dim, mode,
                               pool_dim.cols);
@@ -989,6 +1186,36 @@ int hipF_maxpool_backprop(const float *in_val, MatrixDim in_val_dim,
   PoolGeom g = make_pool_geom(in_height, in_width, 1, 1, pool_channel_dim,
                               mode, out_val_dim.cols);
   const int plane = in_height * in_width;
+  if (pool_channel_dim >= 2 && pool_channel_dim <= 4 && plane > 0 && env_pool_direct()) {
+    const int C = in_val_dim.cols / plane;
+    if (in_val_dim.rows == 0) return 0;
+    if (mode == 1 && out_val_dim.cols == (C - pool_channel_dim + 1) * plane &&
+        in_val_dim.cols == C * plane) {
+      const int64_t n = (int64_t)in_val_dim.rows * plane;
+      const unsigned blocks = (unsigned)((n + 255) / 256);
+#define KCNN_OVB(PC_)                                                                         \
+  hipLaunchKernelGGL(maxpool_overlap_backprop_kernel<PC_>, dim3(blocks), dim3(256), 0, st,    \
+                     in_val, (int64_t)in_val_dim.stride, out_val, (int64_t)out_val_dim.stride, \
+                     out_deriv, (int64_t)out_deriv_dim.stride, dest, (int64_t)dest_dim.stride, \
+                     in_val_dim.rows, plane, C, write_all)
+      if (pool_channel_dim == 2) KCNN_OVB(2); else if (pool_channel_dim == 3) KCNN_OVB(3); else KCNN_OVB(4);
+#undef KCNN_OVB
+      return kcnn::launch_status();
+    }
+    if (mode == 2 && in_val_dim.cols == g.in_2d * g.in_2d * plane &&
+        out_val_dim.cols == g.out_2d * g.out_2d * plane) {
+      const int64_t n = (int64_t)in_val_dim.rows * plane * g.in_2d;
+      const unsigned blocks = (unsigned)((n + 255) / 256);
+#define KCNN_OV2B(PC_)                                                                        \
+  hipLaunchKernelGGL(maxpool_overlap2d_backprop_kernel<PC_>, dim3(blocks), dim3(256), 0, st,  \
+                     in_val, (int64_t)in_val_dim.stride, out_val, (int64_t)out_val_dim.stride, \
+                     out_deriv, (int64_t)out_deriv_dim.stride, dest, (int64_t)dest_dim.stride, \
+                     in_val_dim.rows, plane, g.out_2d, write_all)
+      if (pool_channel_dim == 2) KCNN_OV2B(2); else if (pool_channel_dim == 3) KCNN_OV2B(3); else KCNN_OV2B(4);
+#undef KCNN_OV2B
+      return kcnn::launch_status();
+    }
+  }
   MaxpoolBackpropGather f{in_val, in_val_dim, out_val, out_val_dim, out_deriv,
                           out_deriv_dim, dest, dest_dim, g,
                           out_val_dim.cols / plane, write_all,

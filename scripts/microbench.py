@@ -51,6 +51,18 @@ def main():
     dx = torch.empty_like(x)
     dyp = torch.empty_like(y)
     grad = torch.empty(conv.NumGradientParams(), device="cuda")
+    pool_ov = kcnn.Component.NewFromString(
+        f"MaxpoolComponent in-height={bench.OH} in-width={bench.OW} in-channel={bench.G} "
+        f"pool-height-dim=1 pool-width-dim=1 pool-channel-dim={bench.PC} overlap=true")
+    p_ov = pool_ov.Propagate(y)
+    dp_ov = torch.randn_like(p_ov)
+    pool_2d = kcnn.Component.NewFromString(
+        f"MaxpoolComponent in-height={bench.OH} in-width={bench.OW} in-channel=256 "
+        f"pool-height-dim=1 pool-width-dim=1 pool-channel-dim=2 overlap2D=true")
+    y2 = torch.randn(B, bench.OH * bench.OW * 256, device="cuda")
+    p_2d = pool_2d.Propagate(y2)
+    dp_2d = torch.randn_like(p_2d)
+    dy2 = torch.empty_like(y2)
     conv_b = bench.CONV_BYTES_PER_PASS * B
     tests = {
         "fwd": (lambda: conv.Propagate(x, y), conv_b),
@@ -61,6 +73,14 @@ def main():
                            conv_b),
         "pool_fwd": (lambda: pool.Propagate(y, p), bench.POOL_FWD_BYTES * B),
         "pool_bwd": (lambda: pool.Backprop(y, p, dp, dyp), bench.POOL_BWD_BYTES * B),
+        # intermap pooling variants: overlapping channel
+        # windows on Y, and overlap2D on a 16 x 16 map grid (256 channels)
+        "pool_ov_fwd": (lambda: pool_ov.Propagate(y, p_ov), (y.numel() + p_ov.numel()) * 4),
+        "pool_ov_bwd": (lambda: pool_ov.Backprop(y, p_ov, dp_ov, dyp),
+                        (2 * y.numel() + 2 * p_ov.numel()) * 4),
+        "pool_ov2d_fwd": (lambda: pool_2d.Propagate(y2, p_2d), (y2.numel() + p_2d.numel()) * 4),
+        "pool_ov2d_bwd": (lambda: pool_2d.Backprop(y2, p_2d, dp_2d, dy2),
+                          (2 * y2.numel() + 2 * p_2d.numel()) * 4),
         # HBM reference points of the same size (torch kernels)
         "fill_y": (lambda: dyp.fill_(1.0), dyp.numel() * 4),
         "copy_y": (lambda: dyp.copy_(y), 2 * dyp.numel() * 4),

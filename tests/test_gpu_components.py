@@ -225,6 +225,10 @@ def test_conv_update_divides_by_local_rows(kc):
     (3, 2, 8, 3, 2, 2, False, False),       # 4-element groups wrap h -> w -> c
     (6, 5, 3, 2, 5, 3, False, False),       # row length 90: not a multiple of 4
     (9, 5, 12, 3, 5, 6, False, False),      # plane kernel, 270-float runs (no 16-B)
+    (33, 11, 128, 1, 1, 4, True, False),    # intermap overlap on c2's maps (channel streams)
+    (33, 11, 256, 1, 1, 2, False, True),    # overlap2D, 16 x 16 channel grid
+    (3, 5, 49, 1, 1, 4, False, True),       # overlap2D pc 4, 7 x 7 grid
+    (4, 4, 9, 1, 1, 2, True, False),        # overlap pc 2
 ])
 def test_maxpool_component(kc, path, cfg):
     H, W, C, ph, pw, pc, ov, ov2 = cfg

@@ -590,7 +590,7 @@ __global__ __launch_bounds__(256) void maxpool_overlap_prop_kernel(
   float ring[PC];
 #pragma unroll
   for (int k = 0; k < PC - 1; k++) ring[k + 1] = xr[(int64_t)k * plane];
-#pragma unroll 4
+#pragma unroll 16
   for (int oc = 0; oc + PC - 1 < C; oc++) {
 #pragma unroll
     for (int k = 0; k < PC - 1; k++) ring[k] = ring[k + 1];
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(256) void maxpool_overlap_backprop_kernel(
   float ov[PC], ev[PC];
 #pragma unroll
   for (int k = 0; k < PC; k++) { ov[k] = __builtin_nanf(""); ev[k] = 0.0f; }
-#pragma unroll 4
+#pragma unroll 16
   for (int c = 0; c < C; c++) {
 #pragma unroll
     for (int k = 0; k < PC - 1; k++) { ov[k] = ov[k + 1]; ev[k] = ev[k + 1]; }
@@ -666,6 +666,7 @@ __global__ __launch_bounds__(256) void maxpool_overlap2d_prop_kernel(
 #pragma unroll
     for (int cx = 0; cx < PC; cx++)
       col[cy][cx] = xr[(int64_t)((ox + cx) * in2 + cy - 1) * plane];
+#pragma unroll 4
   for (int oy = 0; oy < o2; oy++) {
 #pragma unroll
     for (int cy = 0; cy < PC - 1; cy++)
@@ -709,6 +710,7 @@ __global__ __launch_bounds__(256) void maxpool_overlap2d_backprop_kernel(
   for (int a = 0; a < PC; a++)
 #pragma unroll
     for (int b = 0; b < PC; b++) { ov[a][b] = __builtin_nanf(""); ev[a][b] = 0.0f; }
+#pragma unroll 4
   for (int Y = 0; Y < in2; Y++) {
 #pragma unroll
     for (int a = 0; a < PC; a++) {

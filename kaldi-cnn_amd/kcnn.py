@@ -23,7 +23,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkcnn.so")
+# KCNN_LIB: an alternative build of the same library (e.g. the phase-timing
+# build, `make -C kaldi-cnn_amd timing`)
+LIB_PATH = os.environ.get("KCNN_LIB") or os.path.join(_HERE, "libkcnn.so")
 INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
 
 

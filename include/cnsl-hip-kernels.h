@@ -116,6 +116,16 @@ int hipF_maxpool_backprop_mask(const unsigned char *mask, int mask_stride,
                                int in_height, int in_width,
                                int pool_channel_dim, kcnn_stream_t stream);
 
+/* MaxpoolComponent::Backprop of a 3-D window from hipF_conv2d_maxpool3d's
+ * 16-bit mask: every input written, dP of its window where its bit is set,
+ * else 0 (A.9). */
+int hipF_maxpool_backprop_mask3d(const unsigned short *mask, int mask_stride,
+                                 const float *out_deriv, MatrixDim out_deriv_dim,
+                                 float *in_deriv, MatrixDim in_deriv_dim,
+                                 int in_height, int in_width, int pool_height_dim,
+                                 int pool_width_dim, int pool_channel_dim,
+                                 kcnn_stream_t stream);
+
 /* ModPermuteChannel (conv2D.cc:685-727, kernel cnsl-cu-kernels.cu:505-528,
  * launcher cnsl-cu-kernels.h:45 cudaF_mod_permute_channels): moves the
  * in_height x in_width maps of `comp` into channel slot
@@ -164,6 +174,19 @@ int hipF_conv2d_maxpool(const float *in, MatrixDim in_dim, int in_height,
                         float *pool, MatrixDim pool_dim, unsigned char *mask,
                         int mask_stride, int pool_channel_dim,
                         kcnn_stream_t stream);
+
+/* The same fusion for a 3-D pooling window (ph x pw x pc, non-overlapping,
+ * pc dividing 32, ph*pw*pc <= 16; c5's 3 x 1 x 4): pool as A.8 and a 16-bit
+ * mask per pooled value, bit c*pw*ph + w*ph + h = "input (c, w, h) of the
+ * window equals the max" (mask_stride in elements).  -1 = not covered. */
+int hipF_conv2d_maxpool3d(const float *in, MatrixDim in_dim, int in_height,
+                          int in_width, int in_channel, int pad_h, int pad_w,
+                          const float *kernel, MatrixDim kernel_dim,
+                          int kernel_height, int kernel_width, int group,
+                          const float *bias, float *out, MatrixDim out_dim,
+                          float *pool, MatrixDim pool_dim, unsigned short *mask,
+                          int mask_stride, int pool_height_dim, int pool_width_dim,
+                          int pool_channel_dim, kcnn_stream_t stream);
 
 /* Weight gradient of ConvolutionComponent::Update (nnet-component-nnet0.cc:
  * 738-765 + :775): grad_W[c*kh*kw + kx*kh + ky][g] = sum_{n,p} X[n][..] *

@@ -600,9 +600,11 @@ static bool propagate_pair(kcnn_nnet *n, size_t i) {
   if (!g_fusion || i + 1 >= n->comps.size()) return false;
   auto *conv = dynamic_cast<ConvolutionComponent *>(n->comps[i]);
   auto *pool = dynamic_cast<MaxpoolComponent *>(n->comps[i + 1]);
-  if (!conv || !pool || pool->FusableChannelPool() == 0) return false;
+  if (!conv || !pool) return false;
+  const int mask_bytes = pool->FusedMaskBytes();  // 1: channel-only, 2: 3-D window
+  if (mask_bytes == 0) return false;
   const int rows = n->fwd[i].NumRows();
-  const size_t need = (size_t)rows * pool->OutputDim();
+  const size_t need = (size_t)rows * pool->OutputDim() * mask_bytes;
   if (n->mask_bytes[i + 1] < need) {
     if (n->mask[i + 1]) CuDevice::Instantiate().Free(n->mask[i + 1]);
     n->mask[i + 1] = static_cast<unsigned char *>(CuDevice::Instantiate().Malloc(need));

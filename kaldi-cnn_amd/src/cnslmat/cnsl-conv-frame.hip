@@ -222,12 +222,20 @@ __global__ __launch_bounds__(256) void conv_fwd_slab_kernel(
 // (same start value and comparison as A.8), plus the routing mask
 // mask[n][j*P + q] bit c = (Y[PC*j + c][q] == pool value) that the pool's
 // Backprop (A.9) would recompute from Y.
+// PC == -1: a 3-D window (ph x pw x pc, runtime; pc divides 32) pooled from
+// the same slab, with a 16-bit mask (bit c*pw*ph + w*ph + h).
+struct PoolWin {
+  int ph, pw, pc, oh2, OP;
+  FastDiv div_OP, div_oh2;
+};
+
 template <int KS, int FT, int PC>
 __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
     ConvGeom g, const float *__restrict__ X, int xs,
     const float *__restrict__ K, int ks, const float *__restrict__ bias,
     float *__restrict__ out, int os, int vec_ok, int dbg,
-    float *__restrict__ pool, int ps, unsigned char *__restrict__ mask, int ms) {
+    float *__restrict__ pool, int ps, unsigned char *__restrict__ mask, int ms,
+    PoolWin pw3) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float *T = reinterpret_cast<float *>(smem);                 // [32][P]
   float *Bs = T + ((32 * g.P + 3) & ~3);                      // [128] bias
@@ -346,6 +354,33 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
         for (int e = (cnt & ~3) + tid_f; e < cnt; e += 256) dst[e] = T[e];
       } else {
         for (int e = tid_f; e < cnt; e += 256) dst[e] = T[e];
+      }
+      if constexpr (PC < 0) {  // 3-D window; rows % pc == 0 (host check)
+        const int cnt_p = rows / pw3.pc * pw3.OP;
+        const int64_t pb = (int64_t)(gb * 32 / pw3.pc) * pw3.OP;
+        float *pd = pool + (int64_t)n * ps + pb;
+        unsigned short *md = reinterpret_cast<unsigned short *>(mask) + (int64_t)n * ms + pb;
+        for (int e = tid_f; e < cnt_p; e += 256) {
+          uint32_t j, q, wi, hi;
+          pw3.div_OP.divmod((uint32_t)e, j, q);
+          pw3.div_oh2.divmod(q, wi, hi);
+          const float *t = T + (int)j * pw3.pc * g.P + (int)wi * pw3.pw * g.oh + (int)hi * pw3.ph;
+          float val = -1e20f;  // A.8: c, then w, then h
+          for (int c = 0; c < pw3.pc; c++)
+            for (int w = 0; w < pw3.pw; w++)
+              for (int h = 0; h < pw3.ph; h++) {
+                const float v = t[c * g.P + w * g.oh + h];
+                if (val < v) val = v;
+              }
+          unsigned m = 0;
+          int bit = 0;
+          for (int c = 0; c < pw3.pc; c++)
+            for (int w = 0; w < pw3.pw; w++)
+              for (int h = 0; h < pw3.ph; h++, bit++)
+                m |= (t[c * g.P + w * g.oh + h] == val ? 1u : 0u) << bit;
+          pd[e] = val;
+          md[e] = (unsigned short)m;
+        }
       }
       if constexpr (PC > 0) {  // rows % PC == 0 (host check)
         const int cnt_p = rows / PC * g.P;
@@ -1248,7 +1283,8 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
       const unsigned grid = frame_grid(g, bpc_env > 0 ? bpc_env : fwd_regs_blocks_per_cu(lds));
 #define KCNN_FWD_REGS(KS_)                                                         \
   hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, 0>), dim3(grid), dim3(256), lds, st, \
-                     g, X, xs, K, ks, bias, out, os, vec_ok, dbg, nullptr, 0, nullptr, 0)
+                     g, X, xs, K, ks, bias, out, os, vec_ok, dbg, nullptr, 0, nullptr, 0, \
+                     PoolWin{})
       static const int dbg = env_int("KCNN_FWD_DEBUG", 0);
       if (ksn <= 4) KCNN_FWD_REGS(4);
       else if (ksn <= 8) KCNN_FWD_REGS(8);
@@ -1294,19 +1330,38 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
                              const float *K, int ks, const float *bias,
                              float *out, int os, float *pool, int ps,
                              unsigned char *mask, int ms, int pc,
-                             hipStream_t st) {
-  if (!(pc == 2 || pc == 4 || pc == 8) || g.G % pc != 0) return -1;
+                             hipStream_t st, int ph, int pw) {
+  const bool win3 = ph > 1 || pw > 1;  // 16-bit mask; ms in mask elements
+  if (win3) {
+    if (pc < 1 || 32 % pc != 0 || ph * pw * pc > 16 || g.oh % ph != 0 || g.ow % pw != 0)
+      return -1;
+  } else if (!(pc == 2 || pc == 4 || pc == 8)) {
+    return -1;
+  }
+  if (g.G % pc != 0) return -1;
+  const int OP = win3 ? (g.oh / ph) * (g.ow / pw) : g.P;  // pooled positions per map
   if (g.G > 128 && g.G % 32 == 0) {  // filter chunks of 128 (pool groups never straddle)
     for (int g0 = 0; g0 < g.G; g0 += 128) {
       ConvGeom gc = g;
       gc.G = g.G - g0 < 128 ? g.G - g0 : 128;
-      const int64_t pofs = (int64_t)(g0 / pc) * g.P;
+      const int64_t pofs = (int64_t)(g0 / pc) * OP;
+      unsigned char *mc = win3 ? reinterpret_cast<unsigned char *>(
+                                     reinterpret_cast<unsigned short *>(mask) + pofs)
+                               : mask + pofs;
       const int rc = kcnn_conv_fwd_frame_pool(gc, X, xs, K + g0, ks, bias ? bias + g0 : nullptr,
                                               out + (int64_t)g0 * g.P, os, pool + pofs, ps,
-                                              mask + pofs, ms, pc, st);
+                                              mc, ms, pc, st, ph, pw);
       if (rc) return g0 == 0 ? rc : (rc < 0 ? (int)hipErrorLaunchFailure : rc);
     }
     return 0;
+  }
+  PoolWin pw3{};
+  if (win3) {
+    pw3.ph = ph; pw3.pw = pw; pw3.pc = pc;
+    pw3.oh2 = g.oh / ph;
+    pw3.OP = OP;
+    pw3.div_OP = FastDiv((uint32_t)OP);
+    pw3.div_oh2 = FastDiv((uint32_t)pw3.oh2);
   }
   if (g.Kdim > 32 || g.G > 128 || g.P < 16 || g.P > 4 * 32 * 3 ||
       g.C * g.HW > 256 * 8)
@@ -1321,7 +1376,7 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
                                      : frame_grid(g, fwd_regs_blocks_per_cu(lds));
 #define KCNN_FWD_POOL(KS_, PC_)                                                       \
   hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_>), dim3(grid), dim3(256), lds, \
-                     st, g, X, xs, K, ks, bias, out, os, vec_ok, 0, pool, ps, mask, ms)
+                     st, g, X, xs, K, ks, bias, out, os, vec_ok, 0, pool, ps, mask, ms, pw3)
 #define KCNN_FWD_POOL_KS(PC_)                     \
   do {                                            \
     if (ksn <= 4) KCNN_FWD_POOL(4, PC_);          \
@@ -1329,7 +1384,8 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
     else if (ksn <= 12) KCNN_FWD_POOL(12, PC_);   \
     else KCNN_FWD_POOL(16, PC_);                  \
   } while (0)
-  if (pc == 2) KCNN_FWD_POOL_KS(2);
+  if (win3) KCNN_FWD_POOL_KS(-1);
+  else if (pc == 2) KCNN_FWD_POOL_KS(2);
   else if (pc == 4) KCNN_FWD_POOL_KS(4);
   else KCNN_FWD_POOL_KS(8);
 #undef KCNN_FWD_POOL_KS

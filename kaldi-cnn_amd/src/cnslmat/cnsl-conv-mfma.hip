@@ -1022,6 +1022,33 @@ int hipF_conv2d_maxpool(const float *in, MatrixDim in_dim, int in_height,
                                   kcnn::as_stream(stream)) == 0 ? 0 : -1;
 }
 
+int hipF_conv2d_maxpool3d(const float *in, MatrixDim in_dim, int in_height,
+                          int in_width, int in_channel, int pad_h, int pad_w,
+                          const float *kernel, MatrixDim kernel_dim,
+                          int kernel_height, int kernel_width, int group,
+                          const float *bias, float *out, MatrixDim out_dim,
+                          float *pool, MatrixDim pool_dim, unsigned short *mask,
+                          int mask_stride, int pool_height_dim, int pool_width_dim,
+                          int pool_channel_dim, kcnn_stream_t stream) {
+  ConvGeom g = make_geom(in_dim.rows, in_height, in_width, in_channel, pad_h,
+                         pad_w, kernel_height, kernel_width, group);
+  const int ph = pool_height_dim, pw = pool_width_dim, pc = pool_channel_dim;
+  if (g.oh <= 0 || g.ow <= 0 || in_dim.cols != g.HW * in_channel ||
+      kernel_dim.rows != g.Kdim || kernel_dim.cols != group ||
+      out_dim.rows != g.R || out_dim.cols != g.P * group || ph <= 0 || pw <= 0 ||
+      pc <= 0 || pool_dim.rows != g.R ||
+      (int64_t)pool_dim.cols * ph * pw * pc != out_dim.cols || mask_stride < pool_dim.cols)
+    return (int)hipErrorInvalidValue;
+  if (g.R == 0) return 0;
+  if (g.M >= ((int64_t)1 << 31)) return -1;
+  return kcnn_conv_fwd_frame_pool(g, in, in_dim.stride, kernel, kernel_dim.stride, bias,
+                                  out, out_dim.stride, pool, pool_dim.stride,
+                                  reinterpret_cast<unsigned char *>(mask), mask_stride, pc,
+                                  kcnn::as_stream(stream), ph, pw) == 0
+             ? 0
+             : -1;
+}
+
 int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
                 int in_channel, int pad_h, int pad_w, const float *kernel,
                 MatrixDim kernel_dim, int kernel_height, int kernel_width,

@@ -464,15 +464,25 @@ __global__ __launch_bounds__(256) void maxpool_window_backprop_kernel(
     xv[t] = *reinterpret_cast<const float4 *>(x + (int64_t)row * xs + col);
     const float *yr = y + (int64_t)row * ys;
     const float *dr = dy + (int64_t)row * dys;  // own stride (B14)
+    // window coordinates once, then stepped with the element (h fastest)
+    uint32_t jc, bc, jw, bw, jh, bh;
+    div_pc.divmod(c, jc, bc);
+    div_pw.divmod(w, jw, bw);
+    div_ph.divmod(h, jh, bh);
+    const uint32_t ph = div_ph.d, pw = div_pw.d, pc = div_pc.d;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const uint32_t j = div_pc.div(c) * (uint32_t)outplane +
-                         div_pw.div(w) * (uint32_t)outh + div_ph.div(h);
+      const uint32_t j = jc * (uint32_t)outplane + jw * (uint32_t)outh + jh;
       pv[t][k] = yr[j];
       dv[t][k] = dr[j];
+      if (++bh == ph) { bh = 0; ++jh; }
       if (++h == (uint32_t)H) {
-        h = 0;
-        if (++w == (uint32_t)W) { w = 0; ++c; }
+        h = 0; bh = 0; jh = 0;
+        if (++bw == pw) { bw = 0; ++jw; }
+        if (++w == (uint32_t)W) {
+          w = 0; bw = 0; jw = 0;
+          if (++bc == pc) { bc = 0; ++jc; }
+        }
       }
     }
     off[t] = (int64_t)row * dxs + col;
@@ -739,6 +749,100 @@ __global__ __launch_bounds__(256) void maxpool_overlap2d_backprop_kernel(
   }
 }
 
+// Backprop of a 3-D window pool from the fused forward's 16-bit mask: a
+// thread takes 4 consecutive inputs (16-B store), each one's window j and bit
+// b = (c % pc)*pw*ph + (w % pw)*ph + (h % ph); dX = bit ? dP[j] : 0.
+__global__ __launch_bounds__(256) void maxpool_mask3d_backprop_kernel(
+    const unsigned short *__restrict__ mask, int64_t ms, const float *__restrict__ dy,
+    int64_t dys, float *__restrict__ dx, int64_t dxs, uint32_t total4, FastDiv div_cols4,
+    FastDiv div_plane, FastDiv div_h, FastDiv div_ph, FastDiv div_pw, FastDiv div_pc,
+    int H, int W, int outplane, int outh) {
+  const uint32_t base = blockIdx.x * (256u * kPoolWinVec) + threadIdx.x;
+  float res[kPoolWinVec][4];
+  int64_t off[kPoolWinVec];
+#pragma unroll
+  for (int t = 0; t < kPoolWinVec; t++) {
+    const uint32_t e0 = base + 256u * t;
+    const uint32_t e = e0 < total4 ? e0 : total4 - 1;
+    uint32_t row, q4, c, rem, w, h;
+    div_cols4.divmod(e, row, q4);
+    const uint32_t col = 4 * q4;
+    div_plane.divmod(col, c, rem);
+    div_h.divmod(rem, w, h);
+    const unsigned short *mr = mask + (int64_t)row * ms;
+    const float *dr = dy + (int64_t)row * dys;
+    // window coordinates once, then stepped with the element (h fastest)
+    uint32_t jc, bc, jw, bw, jh, bh;
+    div_pc.divmod(c, jc, bc);
+    div_pw.divmod(w, jw, bw);
+    div_ph.divmod(h, jh, bh);
+    const uint32_t ph = div_ph.d, pw = div_pw.d, pc = div_pc.d;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t j = jc * (uint32_t)outplane + jw * (uint32_t)outh + jh;
+      const uint32_t bit = (bc * pw + bw) * ph + bh;
+      res[t][k] = (mr[j] >> bit) & 1u ? dr[j] : 0.0f;
+      if (++bh == ph) { bh = 0; ++jh; }
+      if (++h == (uint32_t)H) {
+        h = 0; bh = 0; jh = 0;
+        if (++bw == pw) { bw = 0; ++jw; }
+        if (++w == (uint32_t)W) {
+          w = 0; bw = 0; jw = 0;
+          if (++bc == pc) { bc = 0; ++jc; }
+        }
+      }
+    }
+    off[t] = (int64_t)row * dxs + col;
+  }
+#pragma unroll
+  for (int t = 0; t < kPoolWinVec; t++) {
+    if (base + 256u * t >= total4) continue;
+    *reinterpret_cast<float4 *>(dx + off[t]) =
+        make_float4(res[t][0], res[t][1], res[t][2], res[t][3]);
+  }
+}
+
+// Scatter form of the same: a thread owns one pooled value (window) and
+// writes its ph*pw*pc inputs (pc runs of pw runs of ph consecutive floats;
+// the runs of neighbouring lanes tile each map column).  The window index is
+// computed once per window instead of once per input.
+// PH/PW/PC > 0: the window fixed at compile time (c5's 3x1x4, 2x1x4), so the
+// loops unroll into straight stores; 0 = runtime dims.
+template <int PH, int PW, int PC>
+__global__ __launch_bounds__(256) void maxpool_mask3d_scatter_kernel(
+    const unsigned short *__restrict__ mask, int64_t ms, const float *__restrict__ dy,
+    int64_t dys, float *__restrict__ dx, int64_t dxs, uint32_t total, FastDiv div_cols,
+    FastDiv div_OP, FastDiv div_oh2, int H, int plane, int ph_, int pw_, int pc_) {
+  const int ph = PH > 0 ? PH : ph_, pw = PW > 0 ? PW : pw_, pc = PC > 0 ? PC : pc_;
+  const uint32_t e = blockIdx.x * 256u + threadIdx.x;
+  if (e >= total) return;
+  uint32_t row, j, jc, q, wi, hi;
+  div_cols.divmod(e, row, j);
+  div_OP.divmod(j, jc, q);
+  div_oh2.divmod(q, wi, hi);
+  const unsigned m = mask[(int64_t)row * ms + j];
+  const float d = dy[(int64_t)row * dys + j];
+  float *base = dx + (int64_t)row * dxs + (int64_t)jc * pc * plane + (int64_t)wi * pw * H +
+                (int64_t)hi * ph;
+  if constexpr (PH > 0) {  // compile-time window: straight-line stores
+#pragma unroll
+    for (int c = 0; c < PC; c++)
+#pragma unroll
+      for (int w = 0; w < PW; w++)
+#pragma unroll
+        for (int h = 0; h < PH; h++)
+          base[(int64_t)c * plane + (int64_t)w * H + h] =
+              (m >> ((c * PW + w) * PH + h)) & 1u ? d : 0.0f;
+  } else {
+    int bit = 0;
+    for (int c = 0; c < pc; c++)
+      for (int w = 0; w < pw; w++) {
+        float *col = base + (int64_t)c * plane + (int64_t)w * H;
+        for (int h = 0; h < ph; h++, bit++) col[h] = (m >> bit) & 1u ? d : 0.0f;
+      }
+  }
+}
+
 // Backprop of the channel-only pool from the routing mask saved by the fused
 // forward (hipF_conv2d_maxpool): dX[(PC j + c) plane + q] = bit c of
 // mask[j plane + q] ? dP[j plane + q] : 0 -- the same values A.9 produces
@@ -966,6 +1070,58 @@ int hipF_mod_permute_row(const float *in, MatrixDim in_dim, float *out,
   ModPermuteRow f{in, in_dim, out, out_dim, block_size,
                   FastDiv((uint32_t)in_channel)};
   return launch_elem2d(in_dim.rows, in_dim.cols, f, kcnn::as_stream(stream));
+}
+
+int hipF_maxpool_backprop_mask3d(const unsigned short *mask, int mask_stride,
+                                 const float *out_deriv, MatrixDim out_deriv_dim,
+                                 float *in_deriv, MatrixDim in_deriv_dim,
+                                 int in_height, int in_width, int pool_height_dim,
+                                 int pool_width_dim, int pool_channel_dim,
+                                 kcnn_stream_t stream) {
+  const int ph = pool_height_dim, pw = pool_width_dim, pc = pool_channel_dim;
+  const int plane = in_height * in_width;
+  if (plane <= 0 || ph <= 0 || pw <= 0 || pc <= 0 || in_height % ph != 0 ||
+      in_width % pw != 0 || ph * pw * pc > 16 || mask_stride < out_deriv_dim.cols ||
+      in_deriv_dim.rows != out_deriv_dim.rows ||
+      (int64_t)out_deriv_dim.cols * ph * pw * pc != in_deriv_dim.cols ||
+      in_deriv_dim.cols % (plane * pc) != 0 || in_deriv_dim.cols % 4 != 0 ||
+      in_deriv_dim.stride % 4 != 0 || (uintptr_t)in_deriv % 16 != 0)
+    return (int)hipErrorInvalidValue;
+  const int outh = in_height / ph;
+  const int outplane = outh * (in_width / pw);
+  static const int scatter = [] {
+    const char *e = getenv("KCNN_MASK3D_SCATTER");
+    return e && *e ? atoi(e) : 1;
+  }();
+  if (scatter) {
+    const int64_t nout = (int64_t)out_deriv_dim.rows * out_deriv_dim.cols;
+    if (nout == 0) return 0;
+    if (nout >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+    auto kern = maxpool_mask3d_scatter_kernel<0, 0, 0>;
+    if (ph == 3 && pw == 1 && pc == 4) kern = maxpool_mask3d_scatter_kernel<3, 1, 4>;
+    else if (ph == 2 && pw == 1 && pc == 4) kern = maxpool_mask3d_scatter_kernel<2, 1, 4>;
+    else if (ph == 2 && pw == 2 && pc == 2) kern = maxpool_mask3d_scatter_kernel<2, 2, 2>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)((nout + 255) / 256)), dim3(256), 0,
+                       kcnn::as_stream(stream), mask, (int64_t)mask_stride, out_deriv,
+                       (int64_t)out_deriv_dim.stride, in_deriv, (int64_t)in_deriv_dim.stride,
+                       (uint32_t)nout, FastDiv((uint32_t)out_deriv_dim.cols),
+                       FastDiv((uint32_t)outplane), FastDiv((uint32_t)outh), in_height, plane,
+                       ph, pw, pc);
+    return kcnn::launch_status();
+  }
+  const int64_t n4 = (int64_t)in_deriv_dim.rows * in_deriv_dim.cols / 4;
+  if (n4 == 0) return 0;
+  if (n4 >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  const uint32_t total4 = (uint32_t)n4;
+  const unsigned blocks = (total4 + 256 * kPoolWinVec - 1) / (256 * kPoolWinVec);
+  hipLaunchKernelGGL(maxpool_mask3d_backprop_kernel, dim3(blocks), dim3(256), 0,
+                     kcnn::as_stream(stream), mask, (int64_t)mask_stride, out_deriv,
+                     (int64_t)out_deriv_dim.stride, in_deriv, (int64_t)in_deriv_dim.stride,
+                     total4, FastDiv((uint32_t)(in_deriv_dim.cols / 4)),
+                     FastDiv((uint32_t)plane), FastDiv((uint32_t)in_height),
+                     FastDiv((uint32_t)ph), FastDiv((uint32_t)pw), FastDiv((uint32_t)pc),
+                     in_height, in_width, outplane, outh);
+  return kcnn::launch_status();
 }
 
 int hipF_maxpool_backprop_mask(const unsigned char *mask, int mask_stride,

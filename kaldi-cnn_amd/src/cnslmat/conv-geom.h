@@ -54,7 +54,7 @@ int kcnn_conv_fwd_frame_pool(const kcnn::ConvGeom &g, const float *X, int xs,
                              const float *K, int ks, const float *bias,
                              float *out, int os, float *pool, int ps,
                              unsigned char *mask, int ms, int pc,
-                             hipStream_t st);
+                             hipStream_t st, int ph = 1, int pw = 1);
 int kcnn_conv_dgrad_frame(const kcnn::ConvGeom &g, const float *dY, int dys,
                           const float *K, int ks, float *dX, int dxs,
                           hipStream_t st);

@@ -228,7 +228,9 @@ bool ConvolutionComponent::PropagateMaxpool(const CuMatrixBase<BaseFloat> &in,
                                             unsigned char *mask,
                                             int32 mask_stride) const {
   const int32 pc = pool.FusableChannelPool();
-  if (LiteralPath() || pc == 0 || mask == NULL) return false;
+  int32 ph = 1, pw = 1, pc3 = 0;
+  const bool win3 = pc == 0 && pool.FusableWindow3D(&ph, &pw, &pc3);
+  if (LiteralPath() || (pc == 0 && !win3) || mask == NULL) return false;
   if (pool.In_height() != out_height_ || pool.In_width() != out_width_ ||
       pool.In_channels() != group_ || pool.InputDim() != OutputDim())
     return false;
@@ -237,11 +239,18 @@ bool ConvolutionComponent::PropagateMaxpool(const CuMatrixBase<BaseFloat> &in,
   KALDI_ASSERT(pool_out->NumRows() == in.NumRows() &&
                pool_out->NumCols() == pool.OutputDim());
   CuProfileScope prof("ConvolutionComponent::PropagateMaxpool");
-  const int rc = hipF_conv2d_maxpool(
-      in.Data(), in.Dim(), in_height_, in_width_, in_channel_, in_pad_height_,
-      in_pad_width_, linear_params_.Data(), linear_params_.Dim(), kernel_height_,
-      kernel_width_, group_, bias_params_.Data(), out->Data(), out->Dim(),
-      pool_out->Data(), pool_out->Dim(), mask, mask_stride, pc, S());
+  const int rc =
+      win3 ? hipF_conv2d_maxpool3d(
+                 in.Data(), in.Dim(), in_height_, in_width_, in_channel_, in_pad_height_,
+                 in_pad_width_, linear_params_.Data(), linear_params_.Dim(), kernel_height_,
+                 kernel_width_, group_, bias_params_.Data(), out->Data(), out->Dim(),
+                 pool_out->Data(), pool_out->Dim(), reinterpret_cast<unsigned short *>(mask),
+                 mask_stride, ph, pw, pc3, S())
+           : hipF_conv2d_maxpool(
+                 in.Data(), in.Dim(), in_height_, in_width_, in_channel_, in_pad_height_,
+                 in_pad_width_, linear_params_.Data(), linear_params_.Dim(), kernel_height_,
+                 kernel_width_, group_, bias_params_.Data(), out->Data(), out->Dim(),
+                 pool_out->Data(), pool_out->Dim(), mask, mask_stride, pc, S());
   if (rc < 0) return false;
   CNSL_SAFE_CALL(rc);
   return true;
@@ -805,17 +814,47 @@ int32 MaxpoolComponent::FusableChannelPool() const {
   return output_dim_ * pc == input_dim_ ? pc : 0;
 }
 
+bool MaxpoolComponent::FusableWindow3D(int32 *ph, int32 *pw, int32 *pc) const {
+  if (overlap_ || overlap2D_ || (pool_height_dim_ == 1 && pool_width_dim_ == 1))
+    return false;
+  const int32 c = pool_channel_dim_;
+  if (c <= 0 || 32 % c != 0 || in_channel_ % c != 0 ||
+      pool_height_dim_ * pool_width_dim_ * c > 16 || in_height_ % pool_height_dim_ != 0 ||
+      in_width_ % pool_width_dim_ != 0 ||
+      output_dim_ * pool_height_dim_ * pool_width_dim_ * c != input_dim_)
+    return false;
+  *ph = pool_height_dim_;
+  *pw = pool_width_dim_;
+  *pc = c;
+  return true;
+}
+
+int32 MaxpoolComponent::FusedMaskBytes() const {
+  int32 ph, pw, pc;
+  if (FusableChannelPool() > 0) return 1;
+  return FusableWindow3D(&ph, &pw, &pc) ? 2 : 0;
+}
+
 void MaxpoolComponent::BackpropFromMask(const unsigned char *mask,
                                         int32 mask_stride,
                                         const CuMatrixBase<BaseFloat> &out_deriv,
                                         CuMatrix<BaseFloat> *in_deriv) const {
-  const int32 pc = FusableChannelPool();
-  KALDI_ASSERT(pc > 0 && mask != NULL && out_deriv.NumCols() == output_dim_);
+  KALDI_ASSERT(mask != NULL && out_deriv.NumCols() == output_dim_);
   in_deriv->Resize(out_deriv.NumRows(), input_dim_, kUndefined);  // every element written
   CuProfileScope prof("MaxpoolComponent::BackpropFromMask");
-  CNSL_SAFE_CALL(hipF_maxpool_backprop_mask(
-      mask, mask_stride, out_deriv.Data(), out_deriv.Dim(), in_deriv->Data(),
-      in_deriv->Dim(), in_height_, in_width_, pc, S()));
+  const int32 pc = FusableChannelPool();
+  if (pc > 0) {
+    CNSL_SAFE_CALL(hipF_maxpool_backprop_mask(
+        mask, mask_stride, out_deriv.Data(), out_deriv.Dim(), in_deriv->Data(),
+        in_deriv->Dim(), in_height_, in_width_, pc, S()));
+    return;
+  }
+  int32 ph, pw, c3;
+  KALDI_ASSERT(FusableWindow3D(&ph, &pw, &c3));
+  CNSL_SAFE_CALL(hipF_maxpool_backprop_mask3d(
+      reinterpret_cast<const unsigned short *>(mask), mask_stride, out_deriv.Data(),
+      out_deriv.Dim(), in_deriv->Data(), in_deriv->Dim(), in_height_, in_width_, ph, pw, c3,
+      S()));
 }
 
 // :894-934

@@ -217,6 +217,13 @@ class MaxpoolComponent : public nnet2::Component {
   // pool_channel_dim when the pool is channel-only (1 x 1 x pc, no overlap,
   // pc in {2, 4, 8}): the shape the convolution forward can fuse; else 0.
   int32 FusableChannelPool() const;
+  // A non-overlapping 3-D window (ph*pw > 1) the fused forward can pool from
+  // its slab with a 16-bit mask (pc divides 32, ph*pw*pc <= 16): true and
+  // the window, else false.
+  bool FusableWindow3D(int32 *ph, int32 *pw, int32 *pc) const;
+  // Bytes per pooled value of the routing mask the fused forward writes for
+  // this pool: 1 (channel-only), 2 (3-D window), 0 = not fusable.
+  int32 FusedMaskBytes() const;
   // Backprop (:882-892) from the routing mask written by
   // ConvolutionComponent::PropagateMaxpool for the same minibatch: identical
   // in_deriv to Backprop(in_value, out_value, out_deriv, ...), without

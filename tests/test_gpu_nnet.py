@@ -18,7 +18,8 @@ from _util import assert_same, dev, host, randn, rng
 pytestmark = pytest.mark.gpu
 
 
-def stack(H, W, C, kh, kw, G, pc, fc_out, ph=0, pw=0):
+def stack(H, W, C, kh, kw, G, pc, fc_out, ph=0, pw=0, qh=1, qw=1):
+    """qh x qw x pc: the pool window (1 x 1 x pc: channel-only)."""
     oh, ow = H + 2 * ph - kh + 1, W + 2 * pw - kw + 1
     return "\n".join([
         f"ConvolutionComponent in-height={H} in-width={W} in-channel={C} "
@@ -26,8 +27,8 @@ def stack(H, W, C, kh, kw, G, pc, fc_out, ph=0, pw=0):
         f"stride=1 group={G} out-height={oh} out-width={ow} learning-rate=0.02 "
         f"param-stddev=0.1 bias-stddev=0.5",
         f"MaxpoolComponent in-height={oh} in-width={ow} in-channel={G} "
-        f"pool-height-dim=1 pool-width-dim=1 pool-channel-dim={pc}",
-        f"FullyConnectedComponent input-dim={oh * ow * G // pc} output-dim={fc_out} "
+        f"pool-height-dim={qh} pool-width-dim={qw} pool-channel-dim={pc}",
+        f"FullyConnectedComponent input-dim={oh * ow * G // (pc * qh * qw)} output-dim={fc_out} "
         f"learning-rate=0.02 param-stddev=0.05 bias-stddev=1",
     ]), (oh, ow)
 
@@ -40,12 +41,16 @@ STACKS = {
     "G48_pad": (6, 5, 2, 3, 3, 48, 4, 8, 1, 1),     # last filter group of 16 maps
     "pc3_unfused": (8, 6, 1, 3, 1, 30, 3, 8, 0, 0),  # not fusable: plain path
     "G256_pc4": (12, 6, 2, 4, 2, 256, 4, 16, 0, 0),  # 2 filter chunks of 128
+    # 3-D windows (qh x qw x pc, 16-bit routing mask): (..., pad_h, pad_w, qh, qw)
+    "c5_P1_3x1x4": (40, 11, 3, 8, 1, 256, 4, 16, 0, 0, 3, 1),
+    "win_2x2x2": (9, 8, 2, 2, 1, 64, 2, 8, 0, 0, 2, 2),
+    "win_2x1x8_pad": (6, 6, 1, 3, 3, 32, 8, 8, 1, 1, 2, 1),
 }
 
 
 def build(kc, cfg, seed, ties=False):
-    H, W, C, kh, kw, G, pc, fo, ph, pw = cfg
-    text, _ = stack(H, W, C, kh, kw, G, pc, fo, ph, pw)
+    H, W, C, kh, kw, G, pc, fo, ph, pw = cfg[:10]
+    text, _ = stack(*cfg)
     net = kc.Nnet(text)
     conv, pool, fc = net.components
     r = rng(seed)
@@ -113,15 +118,18 @@ def test_fusion_exact_gradient_mode(kc, name):
     assert_same(a[1][0], b[1][0], f"{name} conv input deriv")
 
 
+@pytest.mark.parametrize("name", ["c2", "c5_P1_3x1x4", "win_2x1x8_pad"])
 @pytest.mark.parametrize("ties", [False, True])
-def test_fused_pool_matches_oracle(kc, ties):
-    H, W, C, kh, kw, G, pc, fo, ph, pw = STACKS["c2"]
-    outs, derivs, _, _ = run(kc, STACKS["c2"], fused=True, ties=ties)
-    oh, ow = H - kh + 1, W - kw + 1
+def test_fused_pool_matches_oracle(kc, name, ties):
+    cfg = STACKS[name]
+    H, W, C, kh, kw, G, pc, fo, ph, pw = cfg[:10]
+    qh, qw = (cfg[10], cfg[11]) if len(cfg) > 10 else (1, 1)
+    outs, derivs, _, _ = run(kc, cfg, fused=True, ties=ties)
+    oh, ow = H + 2 * ph - kh + 1, W + 2 * pw - kw + 1
     y, p = outs[0], outs[1]
-    assert_same(p, O.maxpool_prop(y, oh, ow, 1, 1, pc, p.shape[1]), "fused Maxpool_prop")
+    assert_same(p, O.maxpool_prop(y, oh, ow, qh, qw, pc, p.shape[1]), "fused Maxpool_prop")
     dp = derivs[2]
-    assert_same(derivs[1], O.maxpool_backprop(y, p, dp, oh, ow, 1, 1, pc),
+    assert_same(derivs[1], O.maxpool_backprop(y, p, dp, oh, ow, qh, qw, pc),
                 "mask-routed Maxpool_backprop")
-    if ties:  # every map of a group is a maximum: all receive the derivative
+    if ties and qh * qw == 1:  # every map of a group is a maximum: all get the derivative
         assert (derivs[1] != 0).mean() > 0.99 * (dp != 0).mean()

@@ -29,6 +29,23 @@ CFG = "\n".join([
 ])
 
 
+# a long-kernel stack (implicit-GEMM v2 forward, wgrad v2, scatter dgrad,
+# 3-D pool) -- the c5 code paths through the same DP step
+CFG_LONG = "\n".join([
+    "ConvolutionComponent in-height=8 in-width=9 in-channel=16 in-pad-height=1 in-pad-width=1 "
+    "kernel-height=3 kernel-width=3 stride=1 group=128 out-height=8 out-width=9 "
+    "learning-rate=0.02 param-stddev=0.05 bias-stddev=0.5",
+    "MaxpoolComponent in-height=8 in-width=9 in-channel=128 pool-height-dim=2 "
+    "pool-width-dim=1 pool-channel-dim=4",
+    "ConvolutionComponent in-height=4 in-width=9 in-channel=32 kernel-height=3 kernel-width=3 "
+    "stride=1 group=128 out-height=2 out-width=7 learning-rate=0.02 param-stddev=0.05 "
+    "bias-stddev=0.5",
+    f"FullyConnectedComponent input-dim={2 * 7 * 128} output-dim={F} learning-rate=0.02 "
+    f"param-stddev=0.05 bias-stddev=1 weight-decay=0.0002 momentum=0.9",
+])
+CONFIGS = {"c2": (CFG, H * W * C), "long": (CFG_LONG, 8 * 9 * 16)}
+
+
 def params(net):
     out = {}
     for i, c in enumerate(net.components):
@@ -41,13 +58,14 @@ def params(net):
 
 def main():
     out_dir, steps, n_global = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    cfg, in_dim = CONFIGS[sys.argv[4] if len(sys.argv) > 4 else "c2"]
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo")
     kcnn.init(0)
     kcnn.set_randn_seed(7)
-    net = kcnn.Nnet(CFG)
+    net = kcnn.Nnet(cfg)
     r = np.random.default_rng(11)
-    xs = [r.standard_normal((n_global, H * W * C)).astype(np.float32) for _ in range(steps)]
+    xs = [r.standard_normal((n_global, in_dim)).astype(np.float32) for _ in range(steps)]
     dys = [(r.standard_normal((n_global, F)) * 0.05).astype(np.float32) for _ in range(steps)]
     per = n_global // world
     grads = kcnn_dp.gradient_buffers(net, lambda n: torch.empty(n, device="cuda"))
@@ -59,7 +77,7 @@ def main():
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **params(net))
     if rank == 0:
         kcnn.set_randn_seed(7)
-        ref = kcnn.Nnet(CFG)
+        ref = kcnn.Nnet(cfg)
         for s in range(steps):
             ref.Propagate(torch.from_numpy(xs[s]).cuda())
             ref.Backprop(torch.from_numpy(dys[s]).cuda())  # update with N = n_global

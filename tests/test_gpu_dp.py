@@ -23,17 +23,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_dp_two_ranks_match_single_process(tmp_path):
+@pytest.mark.parametrize("stack,n_params", [("c2", 6), ("long", 9)])
+def test_dp_two_ranks_match_single_process(tmp_path, stack, n_params):
     steps, n_global = 2, 48
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
-           os.path.join(HERE, "dp_gpu_worker.py"), str(tmp_path), str(steps), str(n_global)]
+           os.path.join(HERE, "dp_gpu_worker.py"), str(tmp_path), str(steps), str(n_global),
+           stack]
     env = dict(os.environ, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     a, b = np.load(tmp_path / "rank0.npz"), np.load(tmp_path / "rank1.npz")
     single = np.load(tmp_path / "single.npz")
-    assert sorted(a.files) == sorted(single.files) and len(a.files) == 6
+    assert sorted(a.files) == sorted(single.files) and len(a.files) == n_params
     for k in a.files:
         np.testing.assert_array_equal(a[k], b[k], err_msg=f"replicas differ: {k}")
         ref = single[k]

@@ -39,9 +39,11 @@ CONV_BWD_FLOP = 2 * CONV_FLOP_PER_PASS + 2 * P * G    # dgrad + wgrad + bias gra
 POOL_FWD_BYTES = 4 * (P * G + POOL_OUT)               # 232,320
 POOL_BWD_BYTES = 4 * (2 * P * G + 2 * POOL_OUT)       # 464,640
 # Conv -> Maxpool run fused by the kcnn_nnet runtime (kcnn_set_fusion):
-# forward reads X, writes Y, the pooled output and a 1-byte routing mask; the
-# pool backward reads the mask and dP and writes dY.
-CONV_POOL_FWD_BYTES = 4 * (H * W * C + P * G + POOL_OUT) + POOL_OUT  # 246,840
+# forward reads X, writes the pooled output and a 1-byte routing mask (and Y
+# only with --store-conv-out: nothing in the step reads it); the pool
+# backward reads the mask and dP and writes dY.
+CONV_POOL_FWD_BYTES = 4 * (H * W * C + POOL_OUT) + POOL_OUT          # 63,360
+CONV_POOL_FWD_Y_BYTES = CONV_POOL_FWD_BYTES + 4 * P * G             # 249,216
 POOL_BWD_MASK_BYTES = POOL_OUT + 4 * (POOL_OUT + P * G)               # 243,936
 FC_FLOP = 3 * 2 * POOL_OUT * FC_OUT                   # 71,368,704
 
@@ -209,6 +211,8 @@ def main():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--no-fusion", action="store_true",
                     help="run Conv and Maxpool as separate components")
+    ap.add_argument("--store-conv-out", action="store_true",
+                    help="fused Conv -> Maxpool also stores the conv output")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo = rehearsal on shared GPUs")
     ap.add_argument("--config", default="c2", choices=["c2", "c5", "nnet"],
@@ -238,7 +242,7 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
     kcnn.init(device)
-    kcnn.set_fusion(not args.no_fusion)
+    kcnn.set_fusion(0 if args.no_fusion else 2 if args.store_conv_out else 1)
     kcnn.set_randn_seed(20261015)  # identical initial params on every replica
 
     B = args.frames_per_gpu
@@ -356,7 +360,8 @@ def main():
             ("conv_wgrad", k_wgrad, CONV_FLOP_PER_PASS * B, CONV_BYTES_PER_PASS * B),
             ("maxpool_fwd", k_pool_f, 0, POOL_FWD_BYTES * B),
             ("maxpool_bwd", k_pool_b, 0, POOL_BWD_BYTES * B),
-            ("conv_fwd_maxpool", k_fwd_pool, CONV_FLOP_PER_PASS * B, CONV_POOL_FWD_BYTES * B),
+            ("conv_fwd_maxpool", k_fwd_pool, CONV_FLOP_PER_PASS * B,
+             (CONV_POOL_FWD_Y_BYTES if args.store_conv_out else CONV_POOL_FWD_BYTES) * B),
             ("maxpool_bwd_mask", k_pool_bm, 0, POOL_BWD_MASK_BYTES * B)):
         if ms:
             # the roofline that bounds it: the larger of bytes/peak-BW and
@@ -413,7 +418,8 @@ def main():
                                    "FC(11616->1024), fwd+bwd+update",
                        "frames_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"dp{world}",
-                       "conv_maxpool_fusion": not args.no_fusion},
+                       "conv_maxpool_fusion": not args.no_fusion,
+                       "conv_output_stored": args.no_fusion or args.store_conv_out},
             "roofline": roofline,
             "kernels": kernels,
         }

@@ -51,11 +51,17 @@ int kcnn_set_stream(kcnn_stream_t stream);
 int kcnn_synchronize(void);
 int kcnn_set_literal_path(int literal);  /* replay reference call sequences */
 int kcnn_set_profiling(int on);
-/* kcnn_nnet_* runtime: run a ConvolutionComponent followed by a channel-only
- * MaxpoolComponent (1 x 1 x pc) as one fused forward that also saves the
- * pool's routing mask, and backprop that pool from the mask.  Outputs and
- * derivatives are identical either way.  Default on (env KCNN_FUSE=0: off). */
-int kcnn_set_fusion(int on);
+/* kcnn_nnet_* runtime: run a ConvolutionComponent followed by a
+ * non-overlapping MaxpoolComponent (1 x 1 x pc, or a 3-D window) as one fused
+ * forward that also saves the pool's routing mask, and backprop that pool
+ * from the mask.  Outputs and derivatives are identical either way.
+ *   0: off.
+ *   1 (default): on; the conv output, which nothing in the training step
+ *      reads any more, is not stored.  kcnn_nnet_output recomputes it on
+ *      request until that conv's backprop has run, and fails after.
+ *   2: on, and the conv output is stored as well.
+ * Env KCNN_FUSE sets the initial mode. */
+int kcnn_set_fusion(int mode);
 /* Writes the per-function hipEvent profile (CuDevice::PrintProfile). */
 int kcnn_profile_string(char *buf, size_t len);
 void kcnn_set_randn_seed(uint64_t seed);

@@ -133,9 +133,10 @@ def set_profiling(on: bool):
     check(lib().kcnn_set_profiling(int(bool(on))))
 
 
-def set_fusion(on: bool):
-    """kcnn_nnet runtime: fuse Conv -> channel-only Maxpool (see kcnn.h)."""
-    check(lib().kcnn_set_fusion(int(bool(on))))
+def set_fusion(mode):
+    """kcnn_nnet runtime: fuse Conv -> Maxpool (see kcnn.h).  0 / False: off;
+    1 / True: on, the conv output not stored; 2: on, the conv output stored."""
+    check(lib().kcnn_set_fusion(int(mode)))
 
 
 def profile_string() -> str:

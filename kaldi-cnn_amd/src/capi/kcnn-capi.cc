@@ -43,6 +43,11 @@ struct kcnn_nnet {
   std::vector<unsigned char *> mask;
   std::vector<size_t> mask_bytes;
   std::vector<char> mask_valid;
+  // fwd[i] not stored by the fused pass (fusion mode 1; nothing in training
+  // reads it): 1 = kcnn_nnet_output recomputes it on request, 2 = no longer
+  // possible (the producing component's backprop may have changed its
+  // parameters)
+  std::vector<char> out_stale;
   ~kcnn_nnet() {
     for (auto *m : mask)
       if (m) CuDevice::Instantiate().Free(m);
@@ -53,8 +58,8 @@ struct kcnn_nnet {
 namespace {
 thread_local std::string g_err;
 
-// Runtime fusion of Conv -> channel-only Maxpool (kcnn_set_fusion; env
-// KCNN_FUSE=0 turns it off).
+// Runtime fusion of Conv -> Maxpool (kcnn_set_fusion; env KCNN_FUSE): 0 off,
+// 1 on without storing the conv output, 2 on and the conv output stored.
 int g_fusion = [] {
   const char *e = getenv("KCNN_FUSE");
   return e && *e ? atoi(e) : 1;
@@ -186,7 +191,8 @@ int kcnn_set_literal_path(int literal) {
   return 0;
 }
 int kcnn_set_fusion(int on) {
-  g_fusion = on != 0;
+  if (on < 0 || on > 2) return fail("kcnn_set_fusion: mode is 0, 1 or 2");
+  g_fusion = on;
   return 0;
 }
 int kcnn_set_profiling(int on) {
@@ -568,6 +574,7 @@ kcnn_nnet *kcnn_nnet_new(const char *config) {
     n->mask.assign(n->comps.size(), nullptr);
     n->mask_bytes.assign(n->comps.size(), 0);
     n->mask_valid.assign(n->comps.size(), 0);
+    n->out_stale.assign(n->comps.size() + 1, 0);
   });
   return rc ? nullptr : n.release();
 }
@@ -612,10 +619,12 @@ static bool propagate_pair(kcnn_nnet *n, size_t i) {
   }
   size_output(&n->fwd[i + 1], rows, conv->OutputDim());
   size_output(&n->fwd[i + 2], rows, pool->OutputDim());
+  const bool store = g_fusion == 2;
   if (!conv->PropagateMaxpool(n->fwd[i], &n->fwd[i + 1], *pool, &n->fwd[i + 2],
-                              n->mask[i + 1], pool->OutputDim()))
+                              n->mask[i + 1], pool->OutputDim(), store))
     return false;
   n->mask_valid[i + 1] = 1;
+  n->out_stale[i + 1] = !store;
   return true;
 }
 
@@ -629,6 +638,7 @@ int kcnn_nnet_propagate(kcnn_nnet *n, const float *in, MatrixDim in_dim) {
     borrow(&n->fwd[0], in, in_dim);
     n->num_chunks = in_dim.rows / in_cs;
     std::fill(n->mask_valid.begin(), n->mask_valid.end(), 0);
+    std::fill(n->out_stale.begin(), n->out_stale.end(), 0);
     for (size_t i = 0; i < n->comps.size(); i++) {
       if (propagate_pair(n, i)) { i++; continue; }
       ChunkInfo ii = nnet_in_info(n, i), oi = nnet_out_info(n, i);
@@ -641,6 +651,16 @@ int kcnn_nnet_output(const kcnn_nnet *n, int i, const float **data,
                      MatrixDim *dim) {
   return guard([&] {
     KALDI_ASSERT(i >= -1 && i < (int)n->comps.size());
+    if (n->out_stale[i + 1] == 2)
+      KALDI_ERR << "output of component " << i << " was not stored (fused with the "
+                << "next Maxpool, kcnn_set_fusion(1)) and its backprop has run; "
+                << "use kcnn_set_fusion(2) to keep it";
+    if (n->out_stale[i + 1]) {  // a fused conv's output: run its Propagate now
+      kcnn_nnet *nm = const_cast<kcnn_nnet *>(n);
+      nm->comps[i]->Propagate(nnet_in_info(nm, i), nnet_out_info(nm, i), nm->fwd[i],
+                              &nm->fwd[i + 1]);
+      nm->out_stale[i + 1] = 0;
+    }
     const CuMatrix<BaseFloat> &m = n->fwd[i + 1];
     *data = m.Data();
     *dim = m.Dim();
@@ -664,6 +684,7 @@ int kcnn_nnet_backprop_component(kcnn_nnet *n, int i, const float *out_deriv,
     const int nc = (int)n->comps.size();
     KALDI_ASSERT(i >= 0 && i < nc);
     Component *c = n->comps[i];
+    if (n->out_stale[i + 1]) n->out_stale[i + 1] = 2;
     CuSubMatrix<BaseFloat> od = (i == nc - 1)
         ? view(out_deriv, od_dim)
         : CuSubMatrix<BaseFloat>(n->deriv[i + 1].Data(), n->deriv[i + 1].NumRows(),

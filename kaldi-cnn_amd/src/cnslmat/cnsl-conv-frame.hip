@@ -346,8 +346,11 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
       KCNN_TMARK(3)
       const int rows = g.G - gb * 32 < 32 ? g.G - gb * 32 : 32;
       const int cnt = rows * g.P;
-      float *dst = out + (int64_t)n * os + (int64_t)gb * 32 * g.P;
-      if (vec_ok) {
+      // out == nullptr (pooled variants): the caller needs only the pooled
+      // output and the routing mask, Y itself is never stored
+      float *dst = out ? out + (int64_t)n * os + (int64_t)gb * 32 * g.P : nullptr;
+      if (dst == nullptr) {
+      } else if (vec_ok) {
         const float4 *src4 = reinterpret_cast<const float4 *>(T);
         float4 *dst4 = reinterpret_cast<float4 *>(dst);
         for (int e = tid_f; e < (cnt >> 2); e += 256) dst4[e] = src4[e];
@@ -1349,7 +1352,8 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
                                      reinterpret_cast<unsigned short *>(mask) + pofs)
                                : mask + pofs;
       const int rc = kcnn_conv_fwd_frame_pool(gc, X, xs, K + g0, ks, bias ? bias + g0 : nullptr,
-                                              out + (int64_t)g0 * g.P, os, pool + pofs, ps,
+                                              out ? out + (int64_t)g0 * g.P : nullptr, os,
+                                              pool + pofs, ps,
                                               mc, ms, pc, st, ph, pw);
       if (rc) return g0 == 0 ? rc : (rc < 0 ? (int)hipErrorLaunchFailure : rc);
     }

@@ -226,7 +226,7 @@ bool ConvolutionComponent::PropagateMaxpool(const CuMatrixBase<BaseFloat> &in,
                                             const MaxpoolComponent &pool,
                                             CuMatrixBase<BaseFloat> *pool_out,
                                             unsigned char *mask,
-                                            int32 mask_stride) const {
+                                            int32 mask_stride, bool store_out) const {
   const int32 pc = pool.FusableChannelPool();
   int32 ph = 1, pw = 1, pc3 = 0;
   const bool win3 = pc == 0 && pool.FusableWindow3D(&ph, &pw, &pc3);
@@ -243,14 +243,14 @@ bool ConvolutionComponent::PropagateMaxpool(const CuMatrixBase<BaseFloat> &in,
       win3 ? hipF_conv2d_maxpool3d(
                  in.Data(), in.Dim(), in_height_, in_width_, in_channel_, in_pad_height_,
                  in_pad_width_, linear_params_.Data(), linear_params_.Dim(), kernel_height_,
-                 kernel_width_, group_, bias_params_.Data(), out->Data(), out->Dim(),
-                 pool_out->Data(), pool_out->Dim(), reinterpret_cast<unsigned short *>(mask),
+                 kernel_width_, group_, bias_params_.Data(), store_out ? out->Data() : NULL,
+                 out->Dim(), pool_out->Data(), pool_out->Dim(), reinterpret_cast<unsigned short *>(mask),
                  mask_stride, ph, pw, pc3, S())
            : hipF_conv2d_maxpool(
                  in.Data(), in.Dim(), in_height_, in_width_, in_channel_, in_pad_height_,
                  in_pad_width_, linear_params_.Data(), linear_params_.Dim(), kernel_height_,
-                 kernel_width_, group_, bias_params_.Data(), out->Data(), out->Dim(),
-                 pool_out->Data(), pool_out->Dim(), mask, mask_stride, pc, S());
+                 kernel_width_, group_, bias_params_.Data(), store_out ? out->Data() : NULL,
+                 out->Dim(), pool_out->Data(), pool_out->Dim(), mask, mask_stride, pc, S());
   if (rc < 0) return false;
   CNSL_SAFE_CALL(rc);
   return true;

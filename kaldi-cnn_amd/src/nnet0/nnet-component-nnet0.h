@@ -125,11 +125,14 @@ class ConvolutionComponent : public nnet2::UpdatableComponent {
   // pool's routing mask [rows x mask_stride bytes] for
   // MaxpoolComponent::BackpropFromMask.  Returns false, having done nothing,
   // when the pair is not covered (literal path, other pool shapes, ...).
+  // store_out = false leaves `out` unwritten (sized, contents stale): the
+  // pool's backprop from the mask and this component's Backprop never read
+  // it, so a training step does not need it in HBM.
   bool PropagateMaxpool(const CuMatrixBase<BaseFloat> &in,
                         CuMatrixBase<BaseFloat> *out,
                         const MaxpoolComponent &pool,
                         CuMatrixBase<BaseFloat> *pool_out, unsigned char *mask,
-                        int32 mask_stride) const;
+                        int32 mask_stride, bool store_out = true) const;
 
   // Mutable parameter access for hosts (C-ABI).
   CuMatrix<BaseFloat> &LinearParamsMutable() { return linear_params_; }

@@ -91,7 +91,7 @@ def run(kc, cfg, fused, ties=False, N=37, mode=0):
                   for w in (kc.PARAM_LINEAR, kc.PARAM_BIAS)]
         return outs, derivs, params, grads
     finally:
-        kc.set_fusion(True)
+        kc.set_fusion(1)
 
 
 @pytest.mark.parametrize("name", sorted(STACKS))
@@ -106,6 +106,36 @@ def test_fusion_is_exact(kc, name, ties):
         assert_same(u, v, f"{name} input deriv {k}")
     for k, (u, v) in enumerate(zip(a[2], b[2])):
         assert_same(u, v, f"{name} param {k}")
+
+
+@pytest.mark.parametrize("name", ["c2", "c5_P1_3x1x4"])
+def test_fusion_storing_conv_output(kc, name):
+    """Mode 2 stores Y in the fused pass; mode 1 recomputes it on request."""
+    a = run(kc, STACKS[name], fused=2)
+    b = run(kc, STACKS[name], fused=1)
+    for k in range(3):
+        for i in range(3 if k < 2 else 4):
+            assert_same(a[k][i], b[k][i], f"{name} {k}/{i}")
+
+
+def test_unstored_conv_output_after_backprop(kc):
+    """Mode 1: the conv output of a fused pair is gone once its backprop ran."""
+    cfg = STACKS["c2"]
+    for mode in (1, 2):
+        kc.set_fusion(mode)
+        try:
+            net = build(kc, cfg, seed=11)
+            r = rng(3)
+            x = dev(randn(r, (8, net.components[0].InputDim())))
+            net.Propagate(x)
+            net.Backprop(dev(randn(r, (8, net.components[2].OutputDim()), 0.1)))
+            if mode == 1:
+                with pytest.raises(Exception, match="not stored"):
+                    net.Output(0)
+            else:
+                assert host(net.Output(0)).shape == (8, net.components[0].OutputDim())
+        finally:
+            kc.set_fusion(1)
 
 
 @pytest.mark.parametrize("name", ["c2", "pc2_G96", "pc8_G64"])

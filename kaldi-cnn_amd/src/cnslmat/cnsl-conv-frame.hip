@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
       // output and the routing mask, Y itself is never stored
       float *dst = out ? out + (int64_t)n * os + (int64_t)gb * 32 * g.P : nullptr;
       if (dst == nullptr) {
-      } else if (vec_ok & 1) {
+      } else if (vec_ok) {
         const float4 *src4 = reinterpret_cast<const float4 *>(T);
         float4 *dst4 = reinterpret_cast<float4 *>(dst);
         for (int e = tid_f; e < (cnt >> 2); e += 256) dst4[e] = src4[e];
@@ -423,34 +423,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
         const int64_t pb = (int64_t)(gb * 32 / PC) * g.P;
         float *pd = pool + (int64_t)n * ps + pb;
         unsigned char *md = mask + (int64_t)n * ms + pb;
-        // vec_ok bit 1: pooled values 4 at a time, one float4 and one dword
-        // (4 mask bytes) store each; pb is a multiple of 4 (32 / PC * P)
-        const int cnt4 = (vec_ok & 2) ? cnt_p & ~3 : 0;
-        for (int e4 = tid_f * 4; e4 < cnt4; e4 += 1024) {
-          uint32_t j0, q0;
-          g.div_P.divmod((uint32_t)e4, j0, q0);
-          float val[4];
-          unsigned m = 0;
-#pragma unroll
-          for (int u = 0; u < 4; u++) {
-            int q = (int)q0 + u, j = (int)j0;
-            if (q >= g.P) { q -= g.P; j++; }  // P >= 16: at most one wrap
-            const float *t = T + j * PC * g.P + q;
-            float v[PC];
-#pragma unroll
-            for (int c = 0; c < PC; c++) v[c] = t[c * g.P];
-            float mx = -1e20f;
-#pragma unroll
-            for (int c = 0; c < PC; c++)
-              if (mx < v[c]) mx = v[c];
-#pragma unroll
-            for (int c = 0; c < PC; c++) m |= (v[c] == mx ? 1u : 0u) << (8 * u + c);
-            val[u] = mx;
-          }
-          *reinterpret_cast<float4 *>(pd + e4) = make_float4(val[0], val[1], val[2], val[3]);
-          *reinterpret_cast<unsigned *>(md + e4) = m;
-        }
-        for (int e = cnt4 + tid_f; e < cnt_p; e += 256) {
+        for (int e = tid_f; e < cnt_p; e += 256) {
           uint32_t j, q;
           g.div_P.divmod((uint32_t)e, j, q);
           const float *t = T + (int)j * PC * g.P + (int)q;
@@ -1433,9 +1406,7 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
   const size_t lds = (size_t)((32 * g.P + 3) & ~3) * 4 + 128 * 4 + 32 * 8 +
                      (size_t)g.C * g.HW * 4;
   if (lds > (size_t)kFrameLdsMax) return -1;
-  const int vec_ok = (((uintptr_t)out % 16 == 0) && (os % 4 == 0)) |
-                     (((uintptr_t)pool % 16 == 0 && ps % 4 == 0 &&
-                       (uintptr_t)mask % 4 == 0 && ms % 4 == 0) << 1);
+  const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0);
   const int ksn = (g.Kdim + 1) / 2;
   static const int grid_env = env_int("KCNN_FWD_GRID", 0);  // timing experiments
   const unsigned grid = grid_env > 0 ? (unsigned)std::min<int64_t>(grid_env, g.R)

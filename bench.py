@@ -44,6 +44,9 @@ POOL_BWD_BYTES = 4 * (2 * P * G + 2 * POOL_OUT)       # 464,640
 # backward reads the mask and dP and writes dY.
 CONV_POOL_FWD_BYTES = 4 * (H * W * C + POOL_OUT) + POOL_OUT          # 63,360
 CONV_POOL_FWD_Y_BYTES = CONV_POOL_FWD_BYTES + 4 * P * G             # 249,216
+# Maxpool backward folded into the conv backward (fusion mode 1): reads X,
+# dP and the mask, writes dX; dY is built slab by slab in LDS
+CONV_BWD_POOLED_BYTES = 4 * (2 * H * W * C + POOL_OUT) + POOL_OUT    # 68,640
 POOL_BWD_MASK_BYTES = POOL_OUT + 4 * (POOL_OUT + P * G)               # 243,936
 FC_FLOP = 3 * 2 * POOL_OUT * FC_OUT                   # 71,368,704
 
@@ -351,6 +354,7 @@ def main():
     k_pool_b = avg("MaxpoolComponent::Backprop")
     k_fwd_pool = avg("ConvolutionComponent::PropagateMaxpool")
     k_pool_bm = avg("MaxpoolComponent::BackpropFromMask")
+    k_bwd_pooled = avg("ConvolutionComponent::BackpropPooled")
     k_fc = prof.get("AddMatMat", (0.0, 0))
     kernels = {}
     for name, ms, flop, byts in (
@@ -362,7 +366,8 @@ def main():
             ("maxpool_bwd", k_pool_b, 0, POOL_BWD_BYTES * B),
             ("conv_fwd_maxpool", k_fwd_pool, CONV_FLOP_PER_PASS * B,
              (CONV_POOL_FWD_Y_BYTES if args.store_conv_out else CONV_POOL_FWD_BYTES) * B),
-            ("maxpool_bwd_mask", k_pool_bm, 0, POOL_BWD_MASK_BYTES * B)):
+            ("maxpool_bwd_mask", k_pool_bm, 0, POOL_BWD_MASK_BYTES * B),
+            ("conv_bwd_pooled", k_bwd_pooled, CONV_BWD_FLOP * B, CONV_BWD_POOLED_BYTES * B)):
         if ms:
             # the roofline that bounds it: the larger of bytes/peak-BW and
             # flops/peak-MFMA (algorithmic work)
@@ -387,7 +392,8 @@ def main():
         dk = kernels[dom]
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
+        # the counter passes (scripts/gpu_profiles.sh) profile the default c2 step
+        if os.path.exists(pmc) and not (args.no_fusion or args.store_conv_out):
             try:
                 ent = json.load(open(pmc)).get(dom, {})
                 # PMC bytes are per launch of the profiled run: only for that size

@@ -245,6 +245,25 @@ int hipF_conv2d_backward(const float *in, MatrixDim in_dim, int in_height,
                          MatrixDim grad_W_dim, float *grad_b, void *workspace,
                          size_t workspace_bytes, kcnn_stream_t stream);
 
+/* MaxpoolComponent::Backprop of a channel-only pool (1 x 1 x pc, pc in
+ * {4, 8}) from the routing mask of hipF_conv2d_maxpool, followed by
+ * hipF_conv2d_backward of the ConvolutionComponent below it, in one pass:
+ * out_deriv (= hipF_maxpool_backprop_mask(mask, pool_deriv)) is built per
+ * 32-map slab in LDS and never stored.  Same results as the two calls.
+ * grad_W / grad_b nullable when in_deriv is not (and vice versa).  Returns
+ * -1 without launching when the shape is not covered (the fused backward's
+ * range, G <= 128 per launch); the caller then makes the two calls. */
+int hipF_conv2d_backward_pooled(const float *in, MatrixDim in_dim, int in_height,
+                                int in_width, int in_channel, int pad_h, int pad_w,
+                                const unsigned char *mask, int mask_stride,
+                                const float *pool_deriv, MatrixDim pool_deriv_dim,
+                                int pool_channel_dim, const float *kernel,
+                                MatrixDim kernel_dim, int kernel_height,
+                                int kernel_width, int group, float *in_deriv,
+                                MatrixDim in_deriv_dim, float *grad_W,
+                                MatrixDim grad_W_dim, float *grad_b, void *workspace,
+                                size_t workspace_bytes, kcnn_stream_t stream);
+
 /* Momentum / weight-decay step of ConvolutionComponent::Update
  * (nnet-component-nnet0.cc:769-775) and FullyConnectedComponent::UpdateSimple
  * (:1137-1142), one pass:  prev = momentum*prev + a_wd*W + a_g*grad;

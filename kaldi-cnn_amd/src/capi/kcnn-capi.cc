@@ -48,6 +48,10 @@ struct kcnn_nnet {
   // possible (the producing component's backprop may have changed its
   // parameters)
   std::vector<char> out_stale;
+  // deriv[i] of a mask-fused pool not computed (fusion mode 1): the conv
+  // below consumes the pool's out_deriv and mask directly; materialised by
+  // kcnn_nnet_input_deriv on request, or when that conv's pass declines
+  std::vector<char> deriv_deferred;
   ~kcnn_nnet() {
     for (auto *m : mask)
       if (m) CuDevice::Instantiate().Free(m);
@@ -575,6 +579,7 @@ kcnn_nnet *kcnn_nnet_new(const char *config) {
     n->mask_bytes.assign(n->comps.size(), 0);
     n->mask_valid.assign(n->comps.size(), 0);
     n->out_stale.assign(n->comps.size() + 1, 0);
+    n->deriv_deferred.assign(n->comps.size(), 0);
   });
   return rc ? nullptr : n.release();
 }
@@ -639,6 +644,7 @@ int kcnn_nnet_propagate(kcnn_nnet *n, const float *in, MatrixDim in_dim) {
     n->num_chunks = in_dim.rows / in_cs;
     std::fill(n->mask_valid.begin(), n->mask_valid.end(), 0);
     std::fill(n->out_stale.begin(), n->out_stale.end(), 0);
+    std::fill(n->deriv_deferred.begin(), n->deriv_deferred.end(), 0);
     for (size_t i = 0; i < n->comps.size(); i++) {
       if (propagate_pair(n, i)) { i++; continue; }
       ChunkInfo ii = nnet_in_info(n, i), oi = nnet_out_info(n, i);
@@ -667,10 +673,23 @@ int kcnn_nnet_output(const kcnn_nnet *n, int i, const float **data,
   });
 }
 
+// A deferred pool Backprop (see kcnn_nnet::deriv_deferred), run now.
+static void materialise_pool_deriv(kcnn_nnet *n, int i) {
+  auto *pool = dynamic_cast<cnsl::nnet0::MaxpoolComponent *>(n->comps[i]);
+  KALDI_ASSERT(pool != NULL && n->mask_valid[i] && i + 1 < (int)n->comps.size());
+  CuMatrix<BaseFloat> &od = n->deriv[i + 1];
+  pool->BackpropFromMask(n->mask[i], pool->OutputDim(),
+                         CuSubMatrix<BaseFloat>(od.Data(), od.NumRows(), od.NumCols(),
+                                                od.Stride()),
+                         &n->deriv[i]);
+  n->deriv_deferred[i] = 0;
+}
+
 int kcnn_nnet_input_deriv(const kcnn_nnet *n, int i, const float **data,
                           MatrixDim *dim) {
   return guard([&] {
     KALDI_ASSERT(i >= 0 && i < (int)n->comps.size());
+    if (n->deriv_deferred[i]) materialise_pool_deriv(const_cast<kcnn_nnet *>(n), i);
     const CuMatrix<BaseFloat> &m = n->deriv[i];
     *data = m.Data();
     *dim = m.Dim();
@@ -685,14 +704,25 @@ int kcnn_nnet_backprop_component(kcnn_nnet *n, int i, const float *out_deriv,
     KALDI_ASSERT(i >= 0 && i < nc);
     Component *c = n->comps[i];
     if (n->out_stale[i + 1]) n->out_stale[i + 1] = 2;
+    auto *u = dynamic_cast<UpdatableComponent *>(c);
+    CuMatrix<BaseFloat> *dx = &n->deriv[i];
+    if (i == 0 && skip_first_dx && u) dx = nullptr;
+    if (i + 1 < nc && n->deriv_deferred[i + 1]) {  // pool above left its Backprop here
+      auto *conv = dynamic_cast<cnsl::nnet0::ConvolutionComponent *>(c);
+      auto *pool = dynamic_cast<cnsl::nnet0::MaxpoolComponent *>(n->comps[i + 1]);
+      CuMatrix<BaseFloat> &pd = n->deriv[i + 2];
+      CuSubMatrix<BaseFloat> pod(pd.Data(), pd.NumRows(), pd.NumCols(), pd.Stride());
+      if (conv && pool &&
+          conv->BackpropPooled(n->fwd[i], *pool, n->mask[i + 1], pool->OutputDim(), pod,
+                               mode == 0 ? c : nullptr, dx, mode == 1 ? grad : nullptr))
+        return;
+      materialise_pool_deriv(n, i + 1);
+    }
     CuSubMatrix<BaseFloat> od = (i == nc - 1)
         ? view(out_deriv, od_dim)
         : CuSubMatrix<BaseFloat>(n->deriv[i + 1].Data(), n->deriv[i + 1].NumRows(),
                                  n->deriv[i + 1].NumCols(), n->deriv[i + 1].Stride());
     ChunkInfo ii = nnet_in_info(n, i), oi = nnet_out_info(n, i);
-    auto *u = dynamic_cast<UpdatableComponent *>(c);
-    CuMatrix<BaseFloat> *dx = &n->deriv[i];
-    if (i == 0 && skip_first_dx && u) dx = nullptr;
     if (mode == 1 && u) {
       u->BackpropGradient(ii, oi, n->fwd[i], n->fwd[i + 1], od, dx, grad);
       return;
@@ -700,6 +730,13 @@ int kcnn_nnet_backprop_component(kcnn_nnet *n, int i, const float *out_deriv,
     if (n->mask_valid[i]) {  // pool of a fused pair: route through its mask
       auto *pool = dynamic_cast<cnsl::nnet0::MaxpoolComponent *>(c);
       KALDI_ASSERT(pool != NULL);
+      // mode 1, not the last component: left to the conv below, which
+      // builds its out_deriv from od and the mask slab by slab
+      if (g_fusion == 1 && i < nc - 1 && (pool->FusableChannelPool() == 4 ||
+                                          pool->FusableChannelPool() == 8)) {
+        n->deriv_deferred[i] = 1;
+        return;
+      }
       pool->BackpropFromMask(n->mask[i], pool->OutputDim(), od, dx);
       return;
     }

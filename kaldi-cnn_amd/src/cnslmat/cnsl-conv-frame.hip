@@ -709,12 +709,20 @@ __host__ __device__ inline int bwd_dma_sd_floats(int P) {
   return two > BWD_WAVES * 1024 ? two : BWD_WAVES * 1024;
 }
 
-template <int NCH, bool DX, bool WG>
+//
+// PCM > 0: dY is not in HBM.  It is the Backprop of a channel-only Maxpool
+// (1 x 1 x PCM) from its routing mask: dY[g][p] = bit g % PCM of
+// mask[g / PCM][p] ? dP[g / PCM][p] : 0 (hipF_maxpool_backprop_mask).  dY /
+// dys then point at dP, pmask / pms at the mask, and each slab is built in
+// LDS from its 32 / PCM rows of dP and mask, loaded into registers at the
+// start of the phase before it and expanded after that phase's MFMA chains.
+template <int NCH, bool DX, bool WG, int PCM>
 __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
     ConvGeom g, const float *__restrict__ X, int xs,
     const float *__restrict__ dY, int dys, const float *__restrict__ K, int ks,
     float *__restrict__ dX, int dxs, float *__restrict__ ws_part, int ZZ,
-    unsigned long long wg0, unsigned long long wg1, int zsep, int dx_acc, int dbg) {
+    unsigned long long wg0, unsigned long long wg1, int zsep, int dx_acc, int dbg,
+    const unsigned char *__restrict__ pmask, int pms) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int P = g.P;
   const int BUF = bwd_dma_buf_floats(P);
@@ -778,6 +786,39 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
                                                (uint32_t)(c * slab + q * 256) * 4u, 0, 0);
   };
 
+  // PCM: a slab's 32 / PCM rows of dP and mask (contiguous in the pooled
+  // row).  Thread t < P stages position t of every row (P <= 512), so its
+  // slab offsets are j * PCM * P + t: no per-element index arithmetic.
+  constexpr int NJ = PCM > 0 ? 32 / PCM : 1;
+  float pv[NJ];
+  unsigned pm[(NJ + 3) / 4];  // mask bytes, 4 to a register
+  auto stage_load = [&](int n, int c, int tt) {
+    if (tt >= P) return;
+    const int64_t off = (int64_t)c * NJ * P + tt;
+    const float *src = dY + (int64_t)n * dys + off;
+    const unsigned char *msrc = pmask + (int64_t)n * pms + off;
+#pragma unroll
+    for (int i = 0; i < (NJ + 3) / 4; i++) pm[i] = 0;
+#pragma unroll
+    for (int j = 0; j < NJ; j++) {
+      pv[j] = src[j * P];
+      pm[j / 4] |= (unsigned)msrc[j * P] << (8 * (j % 4));
+    }
+  };
+  auto stage_commit = [&](int b, int tt) {
+    if (tt >= P) return;
+    float *d = Sd0 + b * BUF + tt;
+#pragma unroll
+    for (int j = 0; j < NJ; j++) {
+      const unsigned v = __float_as_uint(pv[j]);
+#pragma unroll
+      for (int c = 0; c < PCM; c++) {
+        // bit c of the element's mask byte, sign-extended to 0 / ~0
+        const int sel = __builtin_amdgcn_sbfe((int)pm[j / 4], 8 * (j % 4) + c, 1);
+        d[(j * PCM + c) * P] = __uint_as_float(v & (unsigned)sel);
+      }
+    }
+  };
   floatx16 wacc[NCH];
 #pragma unroll
   for (int c = 0; c < NCH; c++) wacc[c] = zero16();
@@ -869,7 +910,12 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
 #define KCNN_TMARK(i)
 #endif
   if (blockIdx.x < (unsigned)g.R) {
-    dma_slab(blockIdx.x, 0, 0, lane);
+    if constexpr (PCM > 0) {
+      stage_load(blockIdx.x, 0, tid);
+      stage_commit(0, tid);
+    } else {
+      dma_slab(blockIdx.x, 0, 0, lane);
+    }
     KCNN_XLOAD(blockIdx.x)
   }
   __syncthreads();  // zeroed border before the first commit
@@ -895,7 +941,8 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
         const int nn = ch + 1 < NCH ? n : n + (int)gridDim.x;
         const int cc = ch + 1 < NCH ? ch + 1 : 0;
         if (nn < g.R) {
-          if (!(dbg & 64)) dma_slab(nn, cc, cur ^ 1, lane_f);
+          if constexpr (PCM > 0) stage_load(nn, cc, tid_f);
+          else if (!(dbg & 64)) dma_slab(nn, cc, cur ^ 1, lane_f);
           if (ch + 1 == NCH) { KCNN_XLOAD(nn) }
         }
       }
@@ -982,6 +1029,10 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
 #pragma unroll
         for (int s = 0; s < 16; s++)
           wacc[ch] = __builtin_amdgcn_mfma_f32_32x32x2f32(ain[j][s], wb[s], wacc[ch], 0, 0, 0);
+      }
+      if constexpr (PCM > 0) {  // the next slab, expanded into the other buffer
+        const int nn = ch + 1 < NCH ? n : n + (int)gridDim.x;
+        if (nn < g.R) stage_commit(cur ^ 1, tid_f);
       }
       KCNN_TMARK(3)
       if (ch + 1 < NCH) cur ^= 1;
@@ -1513,10 +1564,13 @@ static size_t bwd_dma_lds(const ConvGeom &g) {
 }
 
 // One filter chunk (G <= 128) of kcnn_conv_bwd_frame; dx_acc adds to dX.
+// pc > 0: dY / dys are the pooled derivative dP of a 1 x 1 x pc Maxpool and
+// pmask / pms its routing mask (see conv_bwd_dma_kernel).
 static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
                            const float *dY, int dys, const float *K, int ks,
                            float *dX, int dxs, float *gW, int gws, float *gb,
-                           void *ws, size_t ws_bytes, int dx_acc, hipStream_t st) {
+                           void *ws, size_t ws_bytes, int dx_acc, hipStream_t st,
+                           const unsigned char *pmask = nullptr, int pms = 0, int pc = 0) {
   static const int enabled = env_int("KCNN_FUSED_BWD", 1);
   static const int variant = env_int("KCNN_BWD_VARIANT", 3);  // 1: register-staged
   static const int bdbg = env_int("KCNN_BWD_DEBUG", 0);
@@ -1524,7 +1578,9 @@ static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
   if (g.Kdim > 31 || g.G % 32 != 0 || g.G > 128 || g.G == 0) return -1;
   if (g.P < 16 || g.P > 32 * BWD_WAVES * BWD_MAXT || 8 * g.P > BWD_THREADS * BWD_MAXV)
     return -1;
-  if ((uintptr_t)dY % 16 != 0 || dys % 4 != 0) return -1;  // 16-B slab loads
+  if (pc == 0 && ((uintptr_t)dY % 16 != 0 || dys % 4 != 0)) return -1;  // 16-B slab loads
+  // pc = 2 would stage 16 rows per slab: past the register budget
+  if (pc != 0 && (!(pc == 4 || pc == 8) || variant != 3)) return -1;
   const int S = (int)frame_grid(g, 1);
   const int E = (g.Kdim + 1) * g.G;
   const int ZZ = g.Kdim | 1;
@@ -1559,9 +1615,16 @@ static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
   if (zsep) lds3 += zbytes;
   if (variant == 3 && g.C * g.HW <= BWD_THREADS * BWD_MAXX &&
       lds3 <= (size_t)kBwdLdsMax) {
-#define KCNN_BWD3(NCH, DXB, WGB)                                                     \
-  hipLaunchKernelGGL((conv_bwd_dma_kernel<NCH, DXB, WGB>), dim3(S), dim3(BWD_THREADS), \
-                     lds3, st, g, X, xs, dY, dys, K, ks, dX, dxs, part, ZZ, wg[0], wg[1], zsep, dx_acc, bdbg)
+#define KCNN_BWD3P(NCH, DXB, WGB, PCM)                                                 \
+  hipLaunchKernelGGL((conv_bwd_dma_kernel<NCH, DXB, WGB, PCM>), dim3(S), dim3(BWD_THREADS), \
+                     lds3, st, g, X, xs, dY, dys, K, ks, dX, dxs, part, ZZ, wg[0], wg[1], zsep, \
+                     dx_acc, bdbg, pmask, pms)
+#define KCNN_BWD3(NCH, DXB, WGB)                  \
+  do {                                            \
+    if (pc == 4) KCNN_BWD3P(NCH, DXB, WGB, 4);    \
+    else if (pc == 8) KCNN_BWD3P(NCH, DXB, WGB, 8); \
+    else KCNN_BWD3P(NCH, DXB, WGB, 0);            \
+  } while (0)
 #define KCNN_BWD3_NCH(NCH)                                  \
   do {                                                      \
     if (dX && gW) KCNN_BWD3(NCH, true, true);               \
@@ -1576,9 +1639,10 @@ static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
     }
 #undef KCNN_BWD3_NCH
 #undef KCNN_BWD3
+#undef KCNN_BWD3P
   } else {
     // register-staged variant: needs the gradient outputs, writes dX
-    if (gW == nullptr || dx_acc) return -1;
+    if (gW == nullptr || dx_acc || pc) return -1;
     const int SP = bwd_sp(g);
     const size_t lds = bwd_lds(g, SP);
     if (lds > (size_t)kFrameLdsMax) return -1;
@@ -1618,19 +1682,22 @@ static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
 int kcnn_conv_bwd_frame(const ConvGeom &g, const float *X, int xs,
                         const float *dY, int dys, const float *K, int ks,
                         float *dX, int dxs, float *gW, int gws, float *gb,
-                        void *ws, size_t ws_bytes, hipStream_t st) {
+                        void *ws, size_t ws_bytes, hipStream_t st,
+                        const unsigned char *pmask, int pms, int pc) {
   if (g.G <= 128)
     return bwd_frame_chunk(g, X, xs, dY, dys, K, ks, dX, dxs, gW, gws, gb, ws,
-                           ws_bytes, 0, st);
+                           ws_bytes, 0, st, pmask, pms, pc);
   if (g.G % 32 != 0 || (int64_t)g.G * g.P * 4 % 16 != 0) return -1;
   static const int variant = env_int("KCNN_BWD_VARIANT", 3);
   if (variant != 3 && dX != nullptr) return -1;  // chunking needs dX accumulation
   for (int g0 = 0; g0 < g.G; g0 += 128) {
     ConvGeom gc = g;
     gc.G = g.G - g0 < 128 ? g.G - g0 : 128;
+    const int64_t dofs = (int64_t)(pc ? g0 / pc : g0) * g.P;  // pooled rows when pc
     const int rc = bwd_frame_chunk(
-        gc, X, xs, dY + (int64_t)g0 * g.P, dys, K + g0, ks, dX, dxs,
-        gW ? gW + g0 : nullptr, gws, gb ? gb + g0 : nullptr, ws, ws_bytes, g0 > 0, st);
+        gc, X, xs, dY + dofs, dys, K + g0, ks, dX, dxs, gW ? gW + g0 : nullptr, gws,
+        gb ? gb + g0 : nullptr, ws, ws_bytes, g0 > 0, st, pmask ? pmask + dofs : nullptr,
+        pms, pc);
     if (rc) {
       // only the first chunk may decline (nothing written yet); a later
       // failure is a launch error

@@ -61,10 +61,15 @@ int kcnn_conv_dgrad_frame(const kcnn::ConvGeom &g, const float *dY, int dys,
 // Fused backward (one pass over dY): dX (nullable) and gW/gb.  ws must hold
 // kcnn_conv_bwd_frame_ws(g) bytes (0 = shape not eligible).
 size_t kcnn_conv_bwd_frame_ws(const kcnn::ConvGeom &g);
+// pc > 0: dY / dys are instead the derivative of a 1 x 1 x pc Maxpool over
+// Y and pmask / pms its routing mask (hipF_conv2d_maxpool); dY is built per
+// slab in LDS and never stored.
 int kcnn_conv_bwd_frame(const kcnn::ConvGeom &g, const float *X, int xs,
                         const float *dY, int dys, const float *K, int ks,
                         float *dX, int dxs, float *gW, int gws, float *gb,
-                        void *ws, size_t ws_bytes, hipStream_t st);
+                        void *ws, size_t ws_bytes, hipStream_t st,
+                        const unsigned char *pmask = nullptr, int pms = 0,
+                        int pc = 0);
 size_t kcnn_conv_wgrad_frame_ws(const kcnn::ConvGeom &g);
 int kcnn_conv_wgrad_frame(const kcnn::ConvGeom &g, const float *X, int xs,
                           const float *dY, int dys, float *gW, int gws,

@@ -641,6 +641,61 @@ void ConvolutionComponent::BackpropGradient(const ChunkInfo &in_info,
       grad + (size_t)KernelDim() * group_, ws, ws_bytes, S()));
 }
 
+bool ConvolutionComponent::BackpropPooled(const CuMatrixBase<BaseFloat> &in_value,
+                                          const MaxpoolComponent &pool,
+                                          const unsigned char *mask, int32 mask_stride,
+                                          const CuMatrixBase<BaseFloat> &pool_deriv,
+                                          Component *to_update_in,
+                                          CuMatrix<BaseFloat> *in_deriv,
+                                          BaseFloat *grad) const {
+  ConvolutionComponent *to_update =
+      grad ? NULL : dynamic_cast<ConvolutionComponent *>(to_update_in);
+  const int32 pc = pool.FusableChannelPool();
+  if (LiteralPath() || mask == NULL || !(pc == 4 || pc == 8)) return false;
+  // Backprop without in_deriv: nothing to do, or (with an update) Update in
+  // the unfused path, whose gradient kernel sums in another order: keep its bits
+  if (grad == NULL && in_deriv == NULL) return false;
+  if (pool.In_height() != out_height_ || pool.In_width() != out_width_ ||
+      pool.In_channels() != group_ || pool.InputDim() != OutputDim())
+    return false;
+  const int32 num_chunks = in_value.NumRows();
+  KALDI_ASSERT(in_value.NumCols() == InputDim() &&
+               pool_deriv.NumCols() == pool.OutputDim() &&
+               pool_deriv.NumRows() == num_chunks);
+  if (in_deriv != NULL) {
+    if (kernel_height_ - 1 - in_pad_height_ < 0 || kernel_width_ - 1 - in_pad_width_ < 0)
+      return false;
+    if (in_deriv->NumRows() != num_chunks || in_deriv->NumCols() != InputDim())
+      in_deriv->Resize(num_chunks, InputDim(), kUndefined);
+  }
+  CuDevice &dev = CuDevice::Instantiate();
+  Scratch own(grad == NULL && to_update != NULL
+                  ? sizeof(BaseFloat) * (size_t)NumGradientParams() : 0);
+  BaseFloat *g = grad ? grad : own.f();
+  const size_t ws_bytes = g ? hipF_conv2d_backward_workspace_bytes(
+                                  in_value.Dim(), in_height_, in_width_, in_channel_,
+                                  in_pad_height_, in_pad_width_, kernel_height_,
+                                  kernel_width_, group_)
+                            : 0;
+  void *ws = ws_bytes ? dev.Workspace(ws_bytes) : nullptr;
+  MatrixDim idd = in_value.Dim();
+  int rc;
+  {
+    CuProfileScope prof("ConvolutionComponent::BackpropPooled");
+    rc = hipF_conv2d_backward_pooled(
+        in_value.Data(), in_value.Dim(), in_height_, in_width_, in_channel_,
+        in_pad_height_, in_pad_width_, mask, mask_stride, pool_deriv.Data(),
+        pool_deriv.Dim(), pc, linear_params_.Data(), linear_params_.Dim(),
+        kernel_height_, kernel_width_, group_, in_deriv ? in_deriv->Data() : nullptr,
+        in_deriv ? in_deriv->Dim() : idd, g, Dense(KernelDim(), group_),
+        g ? g + (size_t)KernelDim() * group_ : nullptr, ws, ws_bytes, S());
+  }
+  if (rc < 0) return false;
+  CNSL_SAFE_CALL(rc);
+  if (to_update != NULL) to_update->ApplyGradient(g, num_chunks);
+  return true;
+}
+
 // Apply half of Update (:767-775), one pass over W / prev_grad_ / grad.
 void ConvolutionComponent::ApplyGradient(const BaseFloat *grad, int32 num_sample) {
   KALDI_ASSERT(num_sample > 0);

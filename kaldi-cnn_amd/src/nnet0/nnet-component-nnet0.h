@@ -134,6 +134,20 @@ class ConvolutionComponent : public nnet2::UpdatableComponent {
                         CuMatrixBase<BaseFloat> *pool_out, unsigned char *mask,
                         int32 mask_stride, bool store_out = true) const;
 
+  // The Backprop of `pool` (a channel-only MaxpoolComponent fed by this
+  // component, forward fused by PropagateMaxpool with routing mask `mask`)
+  // followed by this component's Backprop, in one pass
+  // (hipF_conv2d_backward_pooled): pool_deriv is the pool's out_deriv, and
+  // the pool's in_deriv (this component's out_deriv) is never stored.
+  // grad != NULL: BackpropGradient (gradient out, no update); else Backprop
+  // with the update going to to_update.  Returns false, having done nothing,
+  // when not covered (the caller then runs the two Backprops).
+  bool BackpropPooled(const CuMatrixBase<BaseFloat> &in_value,
+                      const MaxpoolComponent &pool, const unsigned char *mask,
+                      int32 mask_stride, const CuMatrixBase<BaseFloat> &pool_deriv,
+                      Component *to_update, CuMatrix<BaseFloat> *in_deriv,
+                      BaseFloat *grad) const;
+
   // Mutable parameter access for hosts (C-ABI).
   CuMatrix<BaseFloat> &LinearParamsMutable() { return linear_params_; }
   CuVector<BaseFloat> &BiasParamsMutable() { return bias_params_; }

@@ -1,8 +1,9 @@
 """GPU tests of the kcnn_nnet runtime (the NnetUpdater-style component stack,
-include/kcnn.h kcnn_nnet_*), in particular its Conv -> channel-only Maxpool
-fusion: ConvolutionComponent::PropagateMaxpool writes Y, the pooled output
-and the pool's routing mask in one pass, and the pool's Backprop runs from
-the mask (MaxpoolComponent::BackpropFromMask).
+include/kcnn.h kcnn_nnet_*), in particular its Conv -> Maxpool fusion:
+ConvolutionComponent::PropagateMaxpool writes the pooled output and the pool's
+routing mask in one pass (Y too in fusion mode 2), and the pool's Backprop
+runs from the mask (MaxpoolComponent::BackpropFromMask), or for 1x1x4 / 1x1x8
+pools inside the conv's backward (ConvolutionComponent::BackpropPooled).
 
 The fusion is an exact transformation, so every output, input derivative and
 updated parameter must be bit-identical with fusion on and off; the pool
@@ -146,6 +147,33 @@ def test_fusion_exact_gradient_mode(kc, name):
         if u is not None:
             assert_same(u, v, f"{name} grad {k}")
     assert_same(a[1][0], b[1][0], f"{name} conv input deriv")
+
+
+def _calls(kc, key):
+    """Calls of one profile scope so far (the profile accumulates)."""
+    for line in kc.profile_string().splitlines():
+        parts = line.split("\t")
+        if parts[0] == key:
+            return int(parts[2].split()[0])
+    return 0
+
+
+@pytest.mark.parametrize("name,pooled", [("c2", True), ("pc8_G64", True), ("G256_pc4", True),
+                                         ("pc2_G96", False), ("G48_pad", False)])
+def test_pooled_backward_path(kc, name, pooled):
+    """Fusion mode 1 runs a 1x1x4 / 1x1x8 pool's Backprop inside the conv's
+    (ConvolutionComponent::BackpropPooled); other shapes fall back to
+    BackpropFromMask + the conv's own Backprop (the exactness tests above
+    cover both routes)."""
+    key = "ConvolutionComponent::BackpropPooled"
+    kc.set_profiling(True)
+    try:
+        before = _calls(kc, key)
+        run(kc, STACKS[name], fused=1)
+        after = _calls(kc, key)
+    finally:
+        kc.set_profiling(False)
+    assert (after > before) == pooled
 
 
 @pytest.mark.parametrize("name", ["c2", "c5_P1_3x1x4", "win_2x1x8_pad"])

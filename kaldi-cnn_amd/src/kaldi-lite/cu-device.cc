@@ -209,6 +209,13 @@ CuProfileScope::CuProfileScope(const char *key) : key_(key) {
   (void)hipEventRecord(beg_, d.Stream());
 }
 
+void CuProfileScope::Cancel() {
+  if (!beg_) return;
+  (void)hipEventDestroy(beg_);
+  (void)hipEventDestroy(end_);
+  beg_ = end_ = nullptr;
+}
+
 CuProfileScope::~CuProfileScope() {
   if (!beg_) return;
   CuDevice &d = CuDevice::Instantiate();

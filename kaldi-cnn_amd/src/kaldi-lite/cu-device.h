@@ -102,6 +102,8 @@ class CuProfileScope {
  public:
   explicit CuProfileScope(const char *key);
   ~CuProfileScope();
+  // nothing launched after all (e.g. a fused path declined): record nothing
+  void Cancel();
 
  private:
   const char *key_;

@@ -689,6 +689,7 @@ bool ConvolutionComponent::BackpropPooled(const CuMatrixBase<BaseFloat> &in_valu
         kernel_height_, kernel_width_, group_, in_deriv ? in_deriv->Data() : nullptr,
         in_deriv ? in_deriv->Dim() : idd, g, Dense(KernelDim(), group_),
         g ? g + (size_t)KernelDim() * group_ : nullptr, ws, ws_bytes, S());
+    if (rc < 0) prof.Cancel();  // declined: nothing launched
   }
   if (rc < 0) return false;
   CNSL_SAFE_CALL(rc);

@@ -11,6 +11,7 @@ tail -1 $O/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 4
 timeout -k 10 600 python bench.py --json-out $O/bench.json > $O/bench.log 2>&1 || exit 5
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-fusion --json-out $O/bench_nofusion.json > $O/bench_nofusion.log 2>&1 || exit 5
+timeout -k 10 300 python bench.py --no-cpu-baseline --store-conv-out --json-out $O/bench_store.json > $O/bench_store.log 2>&1 || exit 5
 timeout -k 10 300 python bench.py --config c5 --json-out $O/bench_c5.json > $O/bench_c5.log 2>&1 || exit 5
 timeout -k 10 300 python bench.py --config nnet --json-out $O/bench_nnet.json > $O/bench_nnet.log 2>&1 || exit 5
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c2/prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/c2.prof.log 2>&1 || exit 6

@@ -1100,9 +1100,15 @@ int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
       (uintptr_t)kernel % 16 == 0 && (!padded || g.kh * g.kw <= 32)) {
     const int bg = 64 * wgg, bm = 64 * (4 / wgg);
     dim3 grid2((unsigned)((g.M + bm - 1) / bm), (unsigned)((g.G + bg - 1) / bg));
+  // timing experiments (operand loads / LDS stores / traffic switched off):
+  // only in the phase-timing build (make timing), never in libkcnn.so
   static const int ig2dbg = [] {
+#ifdef KCNN_PHASE_TIMING
     const char *e = getenv("KCNN_IGEMM2_DEBUG");
     return e && *e ? atoi(e) : 0;
+#else
+    return 0;
+#endif
   }();
   static const int ig2bk = [] {
     const char *e = getenv("KCNN_IGEMM2_BK");

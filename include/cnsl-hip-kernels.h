@@ -175,6 +175,18 @@ int hipF_conv2d_maxpool(const float *in, MatrixDim in_dim, int in_height,
                         int mask_stride, int pool_channel_dim,
                         kcnn_stream_t stream);
 
+/* ConvolutionComponent::Propagate followed by RectifiedLinearComponent::
+ * Propagate (reference nnet-component.cc:799-805, ApplyFloor(0)) in one pass:
+ * out = max(conv(in) + bias, 0) in the concat layout (x < 0 -> 0, NaN kept).
+ * The conv output itself is not stored.  Returns -1 without launching when
+ * the shape takes a forward kernel without this epilogue (the caller then
+ * runs the two components). */
+int hipF_conv2d_relu(const float *in, MatrixDim in_dim, int in_height, int in_width,
+                     int in_channel, int pad_h, int pad_w, const float *kernel,
+                     MatrixDim kernel_dim, int kernel_height, int kernel_width,
+                     int group, const float *bias, float *out, MatrixDim out_dim,
+                     kcnn_stream_t stream);
+
 /* The same fusion for a 3-D pooling window (ph x pw x pc, non-overlapping,
  * pc dividing 32, ph*pw*pc <= 16; c5's 3 x 1 x 4): pool as A.8 and a 16-bit
  * mask per pooled value, bit c*pw*ph + w*ph + h = "input (c, w, h) of the

@@ -633,6 +633,22 @@ static bool propagate_pair(kcnn_nnet *n, size_t i) {
   return true;
 }
 
+// Component i (Conv) and i+1 (RectifiedLinearComponent) in one pass, fusion
+// mode 1 only: the conv output (the ReLU's in_value, which its Backprop does
+// not read) is left unstored; false when the pair does not qualify.
+static bool propagate_relu_pair(kcnn_nnet *n, size_t i) {
+  if (g_fusion != 1 || i + 1 >= n->comps.size()) return false;
+  auto *conv = dynamic_cast<cnsl::nnet0::ConvolutionComponent *>(n->comps[i]);
+  auto *relu = dynamic_cast<kaldi::nnet2::RectifiedLinearComponent *>(n->comps[i + 1]);
+  if (!conv || !relu || relu->InputDim() != conv->OutputDim()) return false;
+  const int rows = n->fwd[i].NumRows();
+  size_output(&n->fwd[i + 1], rows, conv->OutputDim());
+  size_output(&n->fwd[i + 2], rows, relu->OutputDim());
+  if (!conv->PropagateRelu(n->fwd[i], &n->fwd[i + 2])) return false;
+  n->out_stale[i + 1] = 1;
+  return true;
+}
+
 int kcnn_nnet_propagate(kcnn_nnet *n, const float *in, MatrixDim in_dim) {
   return guard([&] {
     KALDI_ASSERT(in_dim.cols == n->comps[0]->InputDim());
@@ -646,7 +662,7 @@ int kcnn_nnet_propagate(kcnn_nnet *n, const float *in, MatrixDim in_dim) {
     std::fill(n->out_stale.begin(), n->out_stale.end(), 0);
     std::fill(n->deriv_deferred.begin(), n->deriv_deferred.end(), 0);
     for (size_t i = 0; i < n->comps.size(); i++) {
-      if (propagate_pair(n, i)) { i++; continue; }
+      if (propagate_pair(n, i) || propagate_relu_pair(n, i)) { i++; continue; }
       ChunkInfo ii = nnet_in_info(n, i), oi = nnet_out_info(n, i);
       n->comps[i]->Propagate(ii, oi, n->fwd[i], &n->fwd[i + 1]);
     }

@@ -150,6 +150,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(
 //   * Operands per MFMA: one LDS read (A: W tile, B: im2col tile).
 constexpr int IG2_KTAB = 2304;  // im2col-row table entries (c5 C3: Kdim 2304)
 
+// flags bit: RectifiedLinearComponent's Propagate in the epilogue (the other
+// bits are timing switches of the phase-timing build)
+constexpr int kIg2Relu = 1 << 16;
+
 template <int WGG, bool PADDED, int IG2_BK, bool TAB>
 __global__ __launch_bounds__(256) void conv_igemm2_kernel(
     ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ Kmat,
@@ -339,6 +343,7 @@ __global__ __launch_bounds__(256) void conv_igemm2_kernel(
         if (gg >= g.G) continue;
         float v = acc[a][b][r];
         if (bias) v = v + bias[gg];
+        if (dbg & kIg2Relu) v = v < 0.0f ? 0.0f : v;  // ApplyFloor(0)
         orow[(int64_t)gg * g.P] = v;
       }
     }
@@ -1049,12 +1054,13 @@ int hipF_conv2d_maxpool3d(const float *in, MatrixDim in_dim, int in_height,
              : -1;
 }
 
-int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
-                int in_channel, int pad_h, int pad_w, const float *kernel,
-                MatrixDim kernel_dim, int kernel_height, int kernel_width,
-                int group, const float *bias, float *out, MatrixDim out_dim,
-                int concat, void *workspace, size_t workspace_bytes,
-                kcnn_stream_t stream) {
+// relu: the implicit-GEMM v2 path only (-1 for shapes that take another)
+static int conv2d_impl(const float *in, MatrixDim in_dim, int in_height, int in_width,
+                       int in_channel, int pad_h, int pad_w, const float *kernel,
+                       MatrixDim kernel_dim, int kernel_height, int kernel_width,
+                       int group, const float *bias, float *out, MatrixDim out_dim,
+                       int concat, void *workspace, size_t workspace_bytes,
+                       kcnn_stream_t stream, int relu) {
   hipStream_t st = kcnn::as_stream(stream);
   ConvGeom g = make_geom(in_dim.rows, in_height, in_width, in_channel, pad_h,
                          pad_w, kernel_height, kernel_width, group);
@@ -1068,11 +1074,14 @@ int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
   if (g.M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   if (!concat) bias = nullptr;
 
-  if (concat && kcnn_conv_fwd_frame(g, in, in_dim.stride, kernel,
-                                    kernel_dim.stride, bias, out,
-                                    out_dim.stride, st) == 0)
+  // shapes in the frame kernels' range (kcnn_conv_fwd_frame) run unfused:
+  // the fused result then comes from the same kernel as the unfused one
+  if (relu && g.Kdim <= 64 && g.P >= 16) return -1;
+  if (!relu && concat && kcnn_conv_fwd_frame(g, in, in_dim.stride, kernel,
+                                             kernel_dim.stride, bias, out,
+                                             out_dim.stride, st) == 0)
     return 0;
-  if (use_direct(g, concat)) {
+  if (!relu && use_direct(g, concat)) {
     const unsigned blocks = (unsigned)((g.M + 255) / 256);
 #define KCNN_DIRECT(NG)                                                        \
   hipLaunchKernelGGL(conv_direct_smallg_kernel<NG>, dim3(blocks), dim3(256), 0, \
@@ -1100,26 +1109,27 @@ int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
       (uintptr_t)kernel % 16 == 0 && (!padded || g.kh * g.kw <= 32)) {
     const int bg = 64 * wgg, bm = 64 * (4 / wgg);
     dim3 grid2((unsigned)((g.M + bm - 1) / bm), (unsigned)((g.G + bg - 1) / bg));
-  // timing experiments (operand loads / LDS stores / traffic switched off):
-  // only in the phase-timing build (make timing), never in libkcnn.so
-  static const int ig2dbg = [] {
+    // timing experiments (operand loads / LDS stores / traffic switched off):
+    // only in the phase-timing build (make timing), never in libkcnn.so
+    static const int ig2timing = [] {
 #ifdef KCNN_PHASE_TIMING
-    const char *e = getenv("KCNN_IGEMM2_DEBUG");
-    return e && *e ? atoi(e) : 0;
+      const char *e = getenv("KCNN_IGEMM2_DEBUG");
+      return e && *e ? atoi(e) : 0;
 #else
-    return 0;
+      return 0;
 #endif
-  }();
-  static const int ig2bk = [] {
-    const char *e = getenv("KCNN_IGEMM2_BK");
-    return e && *e ? atoi(e) : 16;
-  }();
-  static const int ig2tab = [] {
-    const char *e = getenv("KCNN_IGEMM2_TAB");
-    return e && *e ? atoi(e) : 1;
-  }();
-  const bool tab = ig2tab && (g.Kdim + 15) / 16 * 16 <= IG2_KTAB &&
-                   (int64_t)g.HW * g.C < (1 << 28) && (!padded || g.kh * g.kw <= 31);
+    }();
+    const int ig2dbg = ig2timing | (relu ? kIg2Relu : 0);
+    static const int ig2bk = [] {
+      const char *e = getenv("KCNN_IGEMM2_BK");
+      return e && *e ? atoi(e) : 16;
+    }();
+    static const int ig2tab = [] {
+      const char *e = getenv("KCNN_IGEMM2_TAB");
+      return e && *e ? atoi(e) : 1;
+    }();
+    const bool tab = ig2tab && (g.Kdim + 15) / 16 * 16 <= IG2_KTAB &&
+                     (int64_t)g.HW * g.C < (1 << 28) && (!padded || g.kh * g.kw <= 31);
 #define KCNN_IG2(W_, P_)                                                                  \
   do {                                                                                    \
     if (tab)                                                                              \
@@ -1143,6 +1153,7 @@ int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
 #undef KCNN_IG2
     return kcnn::launch_status();
   }
+  if (relu) return -1;
 
   IgemmPlan pl = plan_igemm(g);
   if (pl.S > 1 && (workspace == nullptr || workspace_bytes < pl.ws_bytes)) {
@@ -1177,6 +1188,27 @@ int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
                        out, out_dim.stride, nullptr, pl.k_per_split);
   }
   return kcnn::launch_status();
+}
+
+int hipF_conv2d(const float *in, MatrixDim in_dim, int in_height, int in_width,
+                int in_channel, int pad_h, int pad_w, const float *kernel,
+                MatrixDim kernel_dim, int kernel_height, int kernel_width,
+                int group, const float *bias, float *out, MatrixDim out_dim,
+                int concat, void *workspace, size_t workspace_bytes,
+                kcnn_stream_t stream) {
+  return conv2d_impl(in, in_dim, in_height, in_width, in_channel, pad_h, pad_w, kernel,
+                     kernel_dim, kernel_height, kernel_width, group, bias, out, out_dim,
+                     concat, workspace, workspace_bytes, stream, 0);
+}
+
+int hipF_conv2d_relu(const float *in, MatrixDim in_dim, int in_height, int in_width,
+                     int in_channel, int pad_h, int pad_w, const float *kernel,
+                     MatrixDim kernel_dim, int kernel_height, int kernel_width,
+                     int group, const float *bias, float *out, MatrixDim out_dim,
+                     kcnn_stream_t stream) {
+  return conv2d_impl(in, in_dim, in_height, in_width, in_channel, pad_h, pad_w, kernel,
+                     kernel_dim, kernel_height, kernel_width, group, bias, out, out_dim,
+                     1, nullptr, 0, stream, 1);
 }
 
 size_t hipF_conv2d_wgrad_workspace_bytes(MatrixDim in_dim, int in_height,

@@ -256,6 +256,25 @@ bool ConvolutionComponent::PropagateMaxpool(const CuMatrixBase<BaseFloat> &in,
   return true;
 }
 
+bool ConvolutionComponent::PropagateRelu(const CuMatrixBase<BaseFloat> &in,
+                                         CuMatrixBase<BaseFloat> *relu_out) const {
+  if (LiteralPath()) return false;
+  KALDI_ASSERT(in.NumCols() == InputDim());
+  KALDI_ASSERT(relu_out->NumRows() == in.NumRows() && relu_out->NumCols() == OutputDim());
+  int rc;
+  {
+    CuProfileScope prof("ConvolutionComponent::PropagateRelu");
+    rc = hipF_conv2d_relu(in.Data(), in.Dim(), in_height_, in_width_, in_channel_,
+                          in_pad_height_, in_pad_width_, linear_params_.Data(),
+                          linear_params_.Dim(), kernel_height_, kernel_width_, group_,
+                          bias_params_.Data(), relu_out->Data(), relu_out->Dim(), S());
+    if (rc < 0) prof.Cancel();  // declined: nothing launched
+  }
+  if (rc < 0) return false;
+  CNSL_SAFE_CALL(rc);
+  return true;
+}
+
 void ConvolutionComponent::PropagateLiteral(const ChunkInfo &in_info,
                                             const CuMatrixBase<BaseFloat> &in,
                                             CuMatrixBase<BaseFloat> *out) const {

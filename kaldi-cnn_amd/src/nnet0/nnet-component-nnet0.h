@@ -134,6 +134,13 @@ class ConvolutionComponent : public nnet2::UpdatableComponent {
                         CuMatrixBase<BaseFloat> *pool_out, unsigned char *mask,
                         int32 mask_stride, bool store_out = true) const;
 
+  // Propagate and the Propagate of a RectifiedLinearComponent that consumes
+  // `out`, in one pass (hipF_conv2d_relu): relu_out = max(out, 0), `out`
+  // itself not written.  Returns false, having done nothing, when the shape
+  // takes a forward kernel without the ReLU epilogue.
+  bool PropagateRelu(const CuMatrixBase<BaseFloat> &in,
+                     CuMatrixBase<BaseFloat> *relu_out) const;
+
   // The Backprop of `pool` (a channel-only MaxpoolComponent fed by this
   // component, forward fused by PropagateMaxpool with routing mask `mask`)
   // followed by this component's Backprop, in one pass

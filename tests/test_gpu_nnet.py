@@ -191,3 +191,71 @@ def test_fused_pool_matches_oracle(kc, name, ties):
                 "mask-routed Maxpool_backprop")
     if ties and qh * qw == 1:  # every map of a group is a maximum: all get the derivative
         assert (derivs[1] != 0).mean() > 0.99 * (dp != 0).mean()
+
+
+# Conv -> RectifiedLinearComponent: fusion mode 1 runs the ReLU in the conv's
+# forward epilogue (ConvolutionComponent::PropagateRelu, implicit-GEMM shapes)
+RELU_STACKS = {
+    # name: (H, W, C, kh, kw, G, pad, fused)
+    "ig2": (9, 8, 8, 3, 3, 64, 0, True),        # kh*kw*C = 72: implicit GEMM v2
+    "ig2_pad": (8, 9, 8, 3, 3, 128, 1, True),   # padded, 2 filter groups per block
+    "c2_frame": (40, 11, 3, 8, 1, 128, 0, False),  # frame kernels: ReLU runs separately
+    "nnet_conv2": (1, 18, 128, 1, 3, 128, 0, True),  # nnet.config's second conv
+}
+
+
+def relu_stack(H, W, C, kh, kw, G, pad):
+    oh, ow = H + 2 * pad - kh + 1, W + 2 * pad - kw + 1
+    return "\n".join([
+        f"ConvolutionComponent in-height={H} in-width={W} in-channel={C} "
+        f"in-pad-height={pad} in-pad-width={pad} kernel-height={kh} kernel-width={kw} "
+        f"stride=1 group={G} out-height={oh} out-width={ow} learning-rate=0.02 "
+        f"param-stddev=0.1 bias-stddev=0.5",
+        f"RectifiedLinearComponent dim={oh * ow * G}",
+        f"FullyConnectedComponent input-dim={oh * ow * G} output-dim=16 "
+        f"learning-rate=0.02 param-stddev=0.05 bias-stddev=1",
+    ])
+
+
+def run_relu(kc, cfg, mode, N=33):
+    kc.set_fusion(mode)
+    try:
+        net = kc.Nnet(relu_stack(*cfg[:7]))
+        conv, _, fc = net.components
+        r = rng(5)
+        conv.SetParam(kc.PARAM_LINEAR, dev(randn(r, (cfg[3] * cfg[4] * cfg[2], cfg[5]), 0.1)))
+        conv.SetParam(kc.PARAM_BIAS, dev(randn(r, (cfg[5],), 0.5)))
+        fc.SetParam(kc.PARAM_LINEAR, dev(randn(r, (16, fc.InputDim()), 0.05)))
+        x = dev(randn(r, (N, net.components[0].InputDim())))
+        dy = dev(randn(r, (N, 16), 0.1))
+        net.Propagate(x)
+        outs = [host(net.Output(i)) for i in range(3)]
+        net.Backprop(dy)
+        derivs = [host(net.InputDeriv(i)) for i in range(3)]
+        params = [host(c.GetParam(w)) for c in (net.components[0], net.components[2])
+                  for w in (kc.PARAM_LINEAR, kc.PARAM_BIAS)]
+        vs, ds, cnt = net.components[1].NonlinearStats()
+        return outs, derivs, params, (np.asarray(vs), np.asarray(ds), cnt)
+    finally:
+        kc.set_fusion(1)
+
+
+@pytest.mark.parametrize("name", sorted(RELU_STACKS))
+def test_conv_relu_fusion_is_exact(kc, name):
+    cfg = RELU_STACKS[name]
+    key = "ConvolutionComponent::PropagateRelu"
+    kc.set_profiling(True)
+    try:
+        before = _calls(kc, key)
+        a = run_relu(kc, cfg, 1)
+        after = _calls(kc, key)
+    finally:
+        kc.set_profiling(False)
+    assert (after > before) == cfg[7]
+    b = run_relu(kc, cfg, 0)
+    for k in range(3):
+        for i, (u, v) in enumerate(zip(a[k], b[k])):
+            assert_same(u, v, f"{name} {k}/{i}")
+    assert np.array_equal(a[3][0], b[3][0]) and np.array_equal(a[3][1], b[3][1])
+    assert a[3][2] == b[3][2]
+    assert (a[0][1] >= 0).all()

@@ -44,8 +44,8 @@ def main():
         for c in sorted(means):
             print(f"    {c:28s} {means[c]:16.1f}  (n={len(cs[c])})")
         if "SQ_VALU_MFMA_BUSY_CYCLES" in means and "GRBM_GUI_ACTIVE" in means:
-            # 256 CUs x 4 SIMDs
-            util = means["SQ_VALU_MFMA_BUSY_CYCLES"] / (means["GRBM_GUI_ACTIVE"] * 1024)
+            # 256 CUs x 4 SIMDs; GRBM_GUI_ACTIVE comes summed over the 8 XCDs
+            util = means["SQ_VALU_MFMA_BUSY_CYCLES"] / (means["GRBM_GUI_ACTIVE"] / 8 * 1024)
             print(f"    -> MFMA busy {100 * util:.1f}% of SIMD-cycles")
         if "FETCH_SIZE" in means:
             print(f"    -> FETCH_SIZE {means['FETCH_SIZE'] / 1e6:.1f} (x1 KB units?)")

@@ -64,6 +64,8 @@ int kcnn_set_profiling(int on);
 int kcnn_set_fusion(int mode);
 /* Writes the per-function hipEvent profile (CuDevice::PrintProfile). */
 int kcnn_profile_string(char *buf, size_t len);
+/* Drops every accumulated and pending profile entry (CuDevice::ResetProfile). */
+int kcnn_reset_profile(void);
 void kcnn_set_randn_seed(uint64_t seed);
 /* Host-side self test of the FastDiv helper; no GPU needed. */
 int kcnn_selftest_fastdiv(void);

@@ -145,6 +145,10 @@ def profile_string() -> str:
     return buf.value.decode()
 
 
+def reset_profile():
+    check(lib().kcnn_reset_profile())
+
+
 def set_randn_seed(seed: int):
     lib().kcnn_set_randn_seed(ctypes.c_uint64(seed))
 

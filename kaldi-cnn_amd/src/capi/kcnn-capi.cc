@@ -206,6 +206,13 @@ int kcnn_set_profiling(int on) {
 int kcnn_profile_string(char *buf, size_t len) {
   return guard([&] { copy_out(CuDevice::Instantiate().ProfileString(), buf, len); });
 }
+int kcnn_reset_profile(void) {
+  return guard([&] {
+    CuDevice &d = CuDevice::Instantiate();
+    (void)d.ProfileString();  // resolves and recycles the pending events
+    d.ResetProfile();
+  });
+}
 void kcnn_set_randn_seed(uint64_t seed) { SetRandnSeed(seed); }
 
 int kcnn_selftest_fastdiv(void) {

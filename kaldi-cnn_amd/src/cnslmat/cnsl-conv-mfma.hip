@@ -1077,6 +1077,8 @@ static int conv2d_impl(const float *in, MatrixDim in_dim, int in_height, int in_
   // shapes in the frame kernels' range (kcnn_conv_fwd_frame) run unfused:
   // the fused result then comes from the same kernel as the unfused one
   if (relu && g.Kdim <= 64 && g.P >= 16) return -1;
+  // likewise the small-filter-count shapes the direct kernel serves
+  if (relu && use_direct(g, concat)) return -1;
   if (!relu && concat && kcnn_conv_fwd_frame(g, in, in_dim.stride, kernel,
                                              kernel_dim.stride, bias, out,
                                              out_dim.stride, st) == 0)

@@ -52,6 +52,25 @@ std::vector<PendingEvent> &pending() {
   static std::vector<PendingEvent> p;
   return p;
 }
+// Events of resolved scopes are kept for reuse: a profiled step creates no
+// new events once the pool holds one pair per scope.
+std::vector<hipEvent_t> &event_pool() {
+  static std::vector<hipEvent_t> p;
+  return p;
+}
+hipEvent_t take_event() {
+  auto &p = event_pool();
+  if (!p.empty()) {
+    hipEvent_t e = p.back();
+    p.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+}
+void give_event(hipEvent_t e) {
+  if (e) event_pool().push_back(e);
+}
 size_t round_block(size_t bytes) {
   // 256-B granules below 1 MiB, 1 MiB granules above: bounded waste, high reuse.
   if (bytes < (1u << 20)) return (bytes + 255) & ~(size_t)255;
@@ -107,6 +126,9 @@ void CuDevice::EnsureInit() {
 
 void CuDevice::SetStream(hipStream_t s) {
   EnsureInit();
+  // Cached blocks and the workspace are reused in stream order on stream_:
+  // let the old stream drain before kernels on the new one can get them.
+  if (s != stream_) CU_SAFE_CALL(hipStreamSynchronize(stream_));
   stream_ = s;
   rocblas_set_stream(blas_, stream_);
 }
@@ -187,8 +209,8 @@ std::string CuDevice::ProfileString() const {
     if (hipEventSynchronize(pe.end) == hipSuccess &&
         hipEventElapsedTime(&ms, pe.beg, pe.end) == hipSuccess)
       self->AccuProfile(pe.key, ms);
-    (void)hipEventDestroy(pe.beg);
-    (void)hipEventDestroy(pe.end);
+    give_event(pe.beg);
+    give_event(pe.end);
   }
   pending().clear();
   std::ostringstream os;
@@ -202,7 +224,11 @@ std::string CuDevice::ProfileString() const {
 CuProfileScope::CuProfileScope(const char *key) : key_(key) {
   CuDevice &d = CuDevice::Instantiate();
   if (!d.Profiling()) return;
-  if (hipEventCreate(&beg_) != hipSuccess || hipEventCreate(&end_) != hipSuccess) {
+  beg_ = take_event();
+  end_ = take_event();
+  if (!beg_ || !end_) {
+    give_event(beg_);
+    give_event(end_);
     beg_ = end_ = nullptr;
     return;
   }
@@ -211,8 +237,8 @@ CuProfileScope::CuProfileScope(const char *key) : key_(key) {
 
 void CuProfileScope::Cancel() {
   if (!beg_) return;
-  (void)hipEventDestroy(beg_);
-  (void)hipEventDestroy(end_);
+  give_event(beg_);
+  give_event(end_);
   beg_ = end_ = nullptr;
 }
 

@@ -201,6 +201,7 @@ RELU_STACKS = {
     "ig2_pad": (8, 9, 8, 3, 3, 128, 1, True),   # padded, 2 filter groups per block
     "c2_frame": (40, 11, 3, 8, 1, 128, 0, False),  # frame kernels: ReLU runs separately
     "nnet_conv2": (1, 18, 128, 1, 3, 128, 0, True),  # nnet.config's second conv
+    "direct_g8": (8, 8, 8, 3, 3, 8, 0, False),   # G <= 8: direct kernel, ReLU separate
 }
 
 

@@ -62,6 +62,20 @@ int kcnn_set_profiling(int on);
  *   2: on, and the conv output is stored as well.
  * Env KCNN_FUSE sets the initial mode. */
 int kcnn_set_fusion(int mode);
+/* How CuMatrixBase::AddMatMat (every FullyConnectedComponent GEMM) computes
+ * its fp32 product (upstream: cuBLAS sgemm, cu-matrix.cc AddMatMat):
+ *   0: rocBLAS sgemm on the fp32-input MFMA;
+ *   1 (default): the in-house kernel on the bf16 MFMA with each fp32 operand
+ *      split exactly into three bf16 parts and the six leading cross products
+ *      kept (cu-gemm-x6.hip); same error bound as sgemm.
+ * Env KCNN_GEMM (0/1) sets the initial mode. */
+int kcnn_set_gemm_mode(int mode);
+/* C[m x n] = alpha * op(A) op(B) + beta * C on row-major fp32 matrices,
+ * exactly CuMatrixBase::AddMatMat(alpha, A, transA, B, transB, beta) with
+ * op(X) = X^T when trans_x (cu-matrix.h, upstream Kaldi). */
+int kcnn_gemm(int trans_a, int trans_b, int m, int n, int k, float alpha,
+              const float *a, int lda, const float *b, int ldb, float beta,
+              float *c, int ldc);
 /* Writes the per-function hipEvent profile (CuDevice::PrintProfile). */
 int kcnn_profile_string(char *buf, size_t len);
 /* Drops every accumulated and pending profile entry (CuDevice::ResetProfile). */

@@ -145,6 +145,24 @@ def profile_string() -> str:
     return buf.value.decode()
 
 
+def set_gemm_mode(mode: int):
+    """AddMatMat's fp32 product: 0 = rocBLAS sgemm, 1 = bf16x6 split kernel."""
+    check(lib().kcnn_set_gemm_mode(int(mode)))
+
+
+def gemm(a, b, c, trans_a=False, trans_b=False, alpha=1.0, beta=0.0):
+    """c = alpha * op(a) op(b) + beta * c (CuMatrixBase::AddMatMat) on torch
+    fp32 device matrices with contiguous rows."""
+    m, n = c.shape
+    k = a.shape[0] if trans_a else a.shape[1]
+    for t in (a, b, c):
+        dim(t)
+    check(lib().kcnn_gemm(int(bool(trans_a)), int(bool(trans_b)), m, n, k,
+                          ctypes.c_float(alpha), ctypes.c_void_p(a.data_ptr()), a.stride(0),
+                          ctypes.c_void_p(b.data_ptr()), b.stride(0), ctypes.c_float(beta),
+                          ctypes.c_void_p(c.data_ptr()), c.stride(0)))
+
+
 def reset_profile():
     check(lib().kcnn_reset_profile())
 

@@ -199,6 +199,25 @@ int kcnn_set_fusion(int on) {
   g_fusion = on;
   return 0;
 }
+int kcnn_set_gemm_mode(int mode) {
+  if (mode < 0 || mode > 1) return fail("kcnn_set_gemm_mode: mode is 0 or 1");
+  CuDevice::Instantiate().SetGemmMode(mode);
+  return 0;
+}
+int kcnn_gemm(int trans_a, int trans_b, int m, int n, int k, float alpha,
+              const float *a, int lda, const float *b, int ldb, float beta,
+              float *c, int ldc) {
+  return guard([&] {
+    if (m < 0 || n < 0 || k < 0) KALDI_ERR << "kcnn_gemm: negative dimension";
+    const int ar = trans_a ? k : m, ac = trans_a ? m : k;
+    const int br = trans_b ? n : k, bc = trans_b ? k : n;
+    if (lda < ac || ldb < bc || ldc < n) KALDI_ERR << "kcnn_gemm: leading dimension too small";
+    CuSubMatrix<BaseFloat> A(const_cast<float *>(a), ar, ac, lda);
+    CuSubMatrix<BaseFloat> B(const_cast<float *>(b), br, bc, ldb);
+    CuSubMatrix<BaseFloat> C(c, m, n, ldc);
+    C.AddMatMat(alpha, A, trans_a ? kTrans : kNoTrans, B, trans_b ? kTrans : kNoTrans, beta);
+  });
+}
 int kcnn_set_profiling(int on) {
   CuDevice::Instantiate().SetProfiling(on != 0);
   return 0;

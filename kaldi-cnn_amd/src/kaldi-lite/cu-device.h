@@ -76,6 +76,10 @@ class CuDevice {
   std::string ProfileString() const;
   void ResetProfile() { profile_.clear(); }
 
+  // AddMatMat's fp32 product: 0 = rocBLAS sgemm, 1 = bf16x6 split kernel
+  void SetGemmMode(int m) { gemm_mode_ = m; }
+  int GemmMode() const { return gemm_mode_; }
+
   void Synchronize();
 
  private:
@@ -87,6 +91,7 @@ class CuDevice {
   hipStream_t stream_ = nullptr;
   rocblas_handle blas_ = nullptr;
   bool profiling_ = false;
+  int gemm_mode_ = 1;
   std::map<std::string, std::pair<double, long>> profile_;
 
   std::mutex mu_;

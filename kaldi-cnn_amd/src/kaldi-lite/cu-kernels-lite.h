@@ -22,6 +22,11 @@ int kl_sum_partials(const float *parts, int S, int m, int n, float beta,
 size_t kl_col_sum_workspace_bytes(MatrixDim md);
 int kl_col_sum(const float *M, MatrixDim md, float alpha, float beta, float *v,
                void *ws, kcnn_stream_t st);
+/* fp32 GEMM on the bf16 MFMAs by an exact 3-way operand split (cu-gemm-x6.hip) */
+size_t kl_gemm_x6_workspace_bytes(int M, int N, int K);
+int kl_gemm_x6(int transA, int transB, int M, int N, int K, float alpha,
+               const float *A, int lda, const float *B, int ldb, float beta,
+               float *C, int ldc, void *ws, size_t ws_bytes, kcnn_stream_t st);
 int kl_dot(const float *A, MatrixDim ad, const float *B, MatrixDim bd,
            int transB, double *out_dev, kcnn_stream_t st);
 #ifdef __cplusplus

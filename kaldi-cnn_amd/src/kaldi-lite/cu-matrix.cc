@@ -266,6 +266,21 @@ void CuMatrixBase<Real>::AddMatMat(Real alpha, const CuMatrixBase<Real> &A,
   if (m == 0 || n == 0) return;
   if (k == 0) { if (beta != 1.0f) Scale(beta); return; }
   CuProfileScope prof("AddMatMat");
+  CuDevice &dev0 = CuDevice::Instantiate();
+  if (dev0.GemmMode() == 1) {
+    // fp32 product on the bf16 MFMAs (exact operand split, cu-gemm-x6.hip);
+    // declines only operands its 16-B loads cannot address
+    const size_t wsb = kl_gemm_x6_workspace_bytes(m, n, k);
+    void *ws = wsb ? dev0.Malloc(wsb) : nullptr;
+    const int rc = kl_gemm_x6(transA == kTrans, transB == kTrans, m, n, k, alpha,
+                              A.Data(), A.Stride(), B.Data(), B.Stride(), beta,
+                              data_, stride_, ws, wsb, S());
+    if (ws) dev0.Free(ws);
+    if (rc != (int)hipErrorInvalidValue) {
+      CNSL_SAFE_CALL(rc);
+      return;
+    }
+  }
   // Row-major C = op(A) op(B)  <=>  column-major C^T = op(B)^T op(A)^T.
   const rocblas_operation opB =
       transB == kTrans ? rocblas_operation_transpose : rocblas_operation_none;

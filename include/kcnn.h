@@ -76,6 +76,18 @@ int kcnn_set_gemm_mode(int mode);
 int kcnn_gemm(int trans_a, int trans_b, int m, int n, int k, float alpha,
               const float *a, int lda, const float *b, int ldb, float beta,
               float *c, int ldc);
+/* The bf16 plane form of an fp32 matrix (kaldi-lite/cu-gemm-x6.hip): x =
+ * h + m + l exactly, the three bf16 planes [rows x cols] at dst, dst + ps,
+ * dst + 2 ps (pitch ldp elements). */
+int kcnn_split_planes(const float *src, int rows, int cols, int ld, uint16_t *dst, int ldp,
+                      int64_t ps);
+/* kcnn_gemm from plane-split operands (a, b as made by kcnn_split_planes,
+ * plane strides aps, bps): the six-product bf16 MFMA kernel with no split
+ * work in it.  Needs k % 32 == 0, lda / ldb / plane strides % 8 == 0 and,
+ * on a row-contiguous operand (A^T or B), its row count % 8 == 0. */
+int kcnn_gemm_planes(int trans_a, int trans_b, int m, int n, int k, float alpha,
+                     const uint16_t *a, int lda, int64_t aps, const uint16_t *b, int ldb,
+                     int64_t bps, float beta, float *c, int ldc);
 /* Writes the per-function hipEvent profile (CuDevice::PrintProfile). */
 int kcnn_profile_string(char *buf, size_t len);
 /* Drops every accumulated and pending profile entry (CuDevice::ResetProfile). */

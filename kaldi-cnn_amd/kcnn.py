@@ -163,6 +163,30 @@ def gemm(a, b, c, trans_a=False, trans_b=False, alpha=1.0, beta=0.0):
                           ctypes.c_void_p(c.data_ptr()), c.stride(0)))
 
 
+def split_planes(x):
+    """fp32 [rows x cols] device matrix -> int16 tensor [3, rows, cols'] of its
+    bf16 planes h, m, l (x = h + m + l exactly); cols' = cols rounded up to 8."""
+    import torch
+    rows, cols = x.shape
+    ldp = (cols + 7) // 8 * 8
+    out = torch.zeros((3, rows, ldp), dtype=torch.int16, device=x.device)
+    check(lib().kcnn_split_planes(ctypes.c_void_p(x.data_ptr()), rows, cols, x.stride(0),
+                                  ctypes.c_void_p(out.data_ptr()), ldp,
+                                  ctypes.c_int64(rows * ldp)))
+    return out
+
+
+def gemm_planes(ap, bp, c, k, trans_a=False, trans_b=False, alpha=1.0, beta=0.0):
+    """kcnn_gemm from split_planes() operands; c fp32 [m x n]."""
+    m, n = c.shape
+    check(lib().kcnn_gemm_planes(int(bool(trans_a)), int(bool(trans_b)), m, n, k,
+                                 ctypes.c_float(alpha), ctypes.c_void_p(ap.data_ptr()),
+                                 ap.stride(1), ctypes.c_int64(ap.stride(0)),
+                                 ctypes.c_void_p(bp.data_ptr()), bp.stride(1),
+                                 ctypes.c_int64(bp.stride(0)), ctypes.c_float(beta),
+                                 ctypes.c_void_p(c.data_ptr()), c.stride(0)))
+
+
 def reset_profile():
     check(lib().kcnn_reset_profile())
 

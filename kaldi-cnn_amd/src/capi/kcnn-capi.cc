@@ -16,6 +16,7 @@
 
 #include "../cnslmat/hip-util.h"
 #include "../kaldi-lite/cu-device.h"
+#include "../kaldi-lite/cu-kernels-lite.h"
 #include "../kaldi-lite/cu-matrix.h"
 #include "../kaldi-lite/kaldi-io.h"
 #include "../nnet0/nnet-component-nnet0.h"
@@ -216,6 +217,28 @@ int kcnn_gemm(int trans_a, int trans_b, int m, int n, int k, float alpha,
     CuSubMatrix<BaseFloat> B(const_cast<float *>(b), br, bc, ldb);
     CuSubMatrix<BaseFloat> C(c, m, n, ldc);
     C.AddMatMat(alpha, A, trans_a ? kTrans : kNoTrans, B, trans_b ? kTrans : kNoTrans, beta);
+  });
+}
+int kcnn_split_planes(const float *src, int rows, int cols, int ld, uint16_t *dst, int ldp,
+                      int64_t ps) {
+  return guard([&] {
+    CuDevice &d = CuDevice::Instantiate();
+    const int rc = kl_split_planes(src, rows, cols, ld, dst, ldp, ps,
+                                   reinterpret_cast<kcnn_stream_t>(d.Stream()));
+    if (rc) KALDI_ERR << "kcnn_split_planes: " << hipGetErrorString((hipError_t)rc);
+  });
+}
+int kcnn_gemm_planes(int trans_a, int trans_b, int m, int n, int k, float alpha,
+                     const uint16_t *a, int lda, int64_t aps, const uint16_t *b, int ldb,
+                     int64_t bps, float beta, float *c, int ldc) {
+  return guard([&] {
+    CuDevice &d = CuDevice::Instantiate();
+    const size_t wsb = kl_gemm_planes_workspace_bytes(m, n, k);
+    void *ws = wsb ? d.Workspace(wsb) : nullptr;
+    const int rc = kl_gemm_planes(trans_a, trans_b, m, n, k, alpha, a, lda, aps, b, ldb, bps,
+                                  beta, c, ldc, ws, wsb,
+                                  reinterpret_cast<kcnn_stream_t>(d.Stream()));
+    if (rc) KALDI_ERR << "kcnn_gemm_planes: " << hipGetErrorString((hipError_t)rc);
   });
 }
 int kcnn_set_profiling(int on) {

@@ -4,6 +4,7 @@
 #define KCNN_KALDI_LITE_CU_KERNELS_LITE_H_
 
 #include <stddef.h>
+#include <stdint.h>
 
 #include "cnsl-hip-kernels.h"
 
@@ -27,6 +28,15 @@ size_t kl_gemm_x6_workspace_bytes(int M, int N, int K);
 int kl_gemm_x6(int transA, int transB, int M, int N, int K, float alpha,
                const float *A, int lda, const float *B, int ldb, float beta,
                float *C, int ldc, void *ws, size_t ws_bytes, kcnn_stream_t st);
+/* the same product from operands already split into bf16 planes h, m, l
+   (plane p of X at X + p * ps elements); kl_split_planes makes them */
+int kl_split_planes(const float *src, int rows, int cols, int ld, uint16_t *dst, int ldp,
+                    int64_t ps, kcnn_stream_t st);
+size_t kl_gemm_planes_workspace_bytes(int M, int N, int K);
+int kl_gemm_planes(int transA, int transB, int M, int N, int K, float alpha,
+                   const uint16_t *A, int lda, int64_t aps, const uint16_t *B, int ldb,
+                   int64_t bps, float beta, float *C, int ldc, void *ws, size_t ws_bytes,
+                   kcnn_stream_t st);
 int kl_dot(const float *A, MatrixDim ad, const float *B, MatrixDim bd,
            int transB, double *out_dev, kcnn_stream_t st);
 #ifdef __cplusplus

@@ -96,3 +96,53 @@ def test_gemm_c2_fc_shapes(kc, name, m, n, k, ta, tb):
     _, w6, r6 = _check(torch, kc, m, n, k, ta, tb, mode=1)
     _, w0, r0 = _check(torch, kc, m, n, k, ta, tb, mode=0)
     assert w6 <= 1.5 * w0 + 1e-8 and r6 <= 1.5 * r0 + 1e-8, (w6, w0, r6, r0)
+
+
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("shape,pitch", [((4, 4, 32), 0), ((260, 132, 64), 4),
+                                         ((300, 1000, 2048), 0), ((256, 256, 9024), 8),
+                                         ((1028, 516, 96), 0)])
+def test_gemm_x6_fast_path_shapes(kc, ta, tb, shape, pitch):
+    """Shapes the one-block-per-K-step kernel takes (K a multiple of 32, rows
+    multiples of 4, 16-B aligned pitches): partial tiles read 0 past M / N
+    through the buffer range, split K, both operand layouts."""
+    import torch
+    m, n, k = shape
+    _check(torch, kc, m, n, k, ta, tb, pitch=pitch)
+    _check(torch, kc, m, n, k, ta, tb, alpha=0.5, beta=1.0, pitch=pitch)
+
+
+def _check_planes(torch, kc, m, n, k, ta, tb, alpha=1.0, beta=0.0, seed=3):
+    a, b, c0 = _mats(torch, m, n, k, ta, tb, seed)
+    ap, bp = kc.split_planes(a), kc.split_planes(b)
+    # the planes are an exact encoding: h + m + l == x
+    for x, xp in ((a, ap), (b, bp)):
+        f = (xp.to(torch.int32) << 16).view(torch.float32)[..., :x.shape[1]]
+        assert torch.equal(f[0] + f[1] + f[2], x)
+    c = c0.clone()
+    kc.gemm_planes(ap, bp, c, k, ta, tb, alpha, beta)
+    torch.cuda.synchronize()
+    A = (a.t() if ta else a).double()
+    B = (b.t() if tb else b).double()
+    t = alpha * (A @ B) + beta * c0.double()
+    s = abs(alpha) * (A.abs() @ B.abs()) + abs(beta) * c0.double().abs()
+    worst = float(((c.double() - t).abs() / s.clamp_min(1e-30)).max())
+    rel = float((c.double() - t).norm() / t.norm())
+    assert worst <= RTOL and rel <= RTOL, (worst, rel)
+    return c
+
+
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("shape", [(8, 8, 32), (264, 136, 64), (1024, 1000, 2048),
+                                   (256, 256, 9024)])
+def test_gemm_planes(kc, ta, tb, shape):
+    """The plane GEMM (LDS-DMA of pre-split operands) against float64, with
+    partial tiles, split K and both operand layouts; bitwise equal to the
+    in-kernel split path's product is not required (different kernels), the
+    bound is."""
+    import torch
+    m, n, k = shape
+    _check_planes(torch, kc, m, n, k, ta, tb)
+    _check_planes(torch, kc, m, n, k, ta, tb, alpha=0.5, beta=1.0)

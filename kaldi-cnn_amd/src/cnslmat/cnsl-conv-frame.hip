@@ -1541,7 +1541,8 @@ size_t kcnn_conv_bwd_frame_ws(const ConvGeom &g) {
     return kcnn_conv_bwd_frame_ws(gc);
   }
   if (g.Kdim > 31 || g.G % 32 != 0 || g.G > 128 || g.G == 0) return 0;
-  if (g.P < 16 || g.P > 32 * BWD_WAVES * BWD_MAXT || 8 * g.P > BWD_THREADS * BWD_MAXV)
+  if ((g.P < 16 || g.P > 32 * BWD_WAVES * BWD_MAXT || 8 * g.P > BWD_THREADS * BWD_MAXV) &&
+      !kcnn_conv_bwd_x6_eligible(g, true, 0))
     return 0;
   const int S = (int)frame_grid(g, 1);
   const int E = (g.Kdim + 1) * g.G;
@@ -1567,6 +1568,24 @@ static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
   static const int bdbg = env_int("KCNN_BWD_DEBUG", 0);
   if (!enabled || (dX == nullptr && gW == nullptr)) return -1;
   if (g.Kdim > 31 || g.G % 32 != 0 || g.G > 128 || g.G == 0) return -1;
+  // the bf16x6 kernel (cnsl-conv-x6.hip) where the shape allows; KCNN_BWD_X6=0
+  // keeps the fp32-MFMA kernels below
+  static const int use_x6 = env_int("KCNN_BWD_X6", 1);
+  if (use_x6 && variant == 3 && kcnn_conv_bwd_x6_eligible(g, dX != nullptr, pc)) {
+    const int S = (int)frame_grid(g, 1);
+    const int E = (g.Kdim + 1) * g.G;
+    float *part = static_cast<float *>(ws);
+    if (gW != nullptr) {
+      const size_t need = kcnn_conv_bwd_frame_ws(g);
+      if (need == 0 || ws == nullptr || ws_bytes < need) return -1;
+    }
+    int rc = kcnn_conv_bwd_x6(g, X, xs, dY, dys, K, ks, dX, dxs, gW ? part : nullptr, S,
+                              dx_acc, st, pmask, pms, pc);
+    if (rc || gW == nullptr) return rc;
+    hipLaunchKernelGGL(reduce_splits_kernel, dim3((E + 63) / 64), dim3(256), 0, st, part, S,
+                       E, g.Kdim * g.G, g.G, 0, gW, gws, gb);
+    return (int)hipGetLastError();
+  }
   if (g.P < 16 || g.P > 32 * BWD_WAVES * BWD_MAXT || 8 * g.P > BWD_THREADS * BWD_MAXV)
     return -1;
   if (pc == 0 && ((uintptr_t)dY % 16 != 0 || dys % 4 != 0)) return -1;  // 16-B slab loads

@@ -1,0 +1,567 @@
+// cnslmat/cnsl-conv-x6.hip -- the fused convolution backward of the thin
+// frame layers (Kdim = kh*kw*C <= 31, P <= 384: BASELINE c2's 8x1x3 input
+// layer) on the bf16 matrix cores, with every fp32 operand split exactly
+// into three bf16 parts (x = h + m + l) and the six leading cross products
+// of each product kept (the bf16x6 scheme of kaldi-lite/cu-gemm-x6.hip; the
+// three dropped terms are below fp32's own rounding of a product).
+//
+// Reference: ConvolutionComponent::Backprop (nnet-component-nnet0.cc:461-544)
+// = dX by Conv2D of the padded dY with the flipped kernel (:489-540) and the
+// update gradient of Update (:738-777: TpBlock(X) conv TpInsideBlock(dY),
+// ModPermuteRow, bias = row sum of dY).  Here both come out of one pass over
+// dY, as in conv_bwd_dma_kernel (cnsl-conv-frame.hip), whose fp32 MFMA
+// (v_mfma_f32_32x32x2_f32, 64 FLOP/clk/SIMD) holds the SIMD's vector issue
+// for all of its 64 cycles.  v_mfma_f32_32x32x16_bf16 does 8x the work in
+// half the cycles; six of them replace eight fp32 MFMAs of the same tile at
+// 3/8 of the matrix-pipe time.
+//
+// One workgroup (512 threads) per CU walks frames; per frame and 32-filter
+// slab of dY:
+//   split   the slab's dY (PCM > 0: built from the pooled derivative dP and
+//           the 1-byte routing mask of a fused 1 x 1 x PCM Maxpool, i.e.
+//           MaxpoolComponent::Backprop folded in) is gated, split and written
+//           as three bf16 planes of a [g][p] LDS image (768-B rows, 16-B
+//           chunks XOR-swizzled per 256-B segment, so that 32-lane row reads
+//           and ds_read_b64_tr_b16 column reads are both conflict-free);
+//   dgrad   Z[p][k] += sum_g dY[g][p] W[k][g]: A = dY^T by transposed reads of
+//           the image, B = W from its own plane image; each wave owns position
+//           tiles, Z stays in its accumulators for the frame;
+//   wgrad   gW[k][g] += sum_p im2col(X)[k][p] dY[g][p]: A = the frame's im2col
+//           values (gathered once per frame from the LDS-resident map and split
+//           in registers; row Kdim is the constant 1, so the bias gradient falls
+//           out of the same MFMAs), B = row reads of the image; the k16 steps
+//           over p are dealt to the waves so every wave runs the same number
+//           of MFMAs.
+// At the end of a frame Z goes to LDS and is col2im'ed into dX during the
+// next frame's first split phase.  Per-wave gradient partials are summed in a
+// fixed order through LDS, workgroup partials by reduce_splits_kernel:
+// deterministic, and bitwise the same with or without dX.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "conv-geom.h"
+
+using namespace kcnn;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int NT = 512, NW = NT / 64;
+constexpr int PP = 384;             // positions per image row (768 B)
+constexpr int ROWB = PP * 2;
+constexpr int YPL = 32 * ROWB;      // one plane of a 32-filter slab: 24 KB
+constexpr int WROWB = 256;          // W image row: 128 filters
+constexpr int WPL = 32 * WROWB;     // 8 KB
+constexpr int MAXS = 6;             // wgrad k16 steps per wave (24 over waves 4-7)
+constexpr int MAXT = 3;             // dgrad position tiles per wave (12 over waves 0-3)
+constexpr int MAXU = 2;             // split units per thread (8 * 96 <= 2 * 512)
+constexpr int MAXX = 4;             // X values per thread (C*H*W <= 2048)
+
+struct X6Steps {
+  uint8_t s[NW][MAXS];  // wgrad k16 steps of each wave, 0xff = none
+};
+
+__device__ __forceinline__ int swz4(int row) {
+  return ((row & 3) << 2) | ((row >> 2) & 3);
+}
+// byte offset of (row, p) in a [row][384] bf16 image
+__device__ __forceinline__ int yoff(int row, int p) {
+  return row * ROWB + ((p >> 7) << 8) + ((((p >> 3) & 15) ^ swz4(row)) << 4) +
+         ((p & 7) << 1);
+}
+// byte offset of (k, g) in the [32][128] bf16 W image
+__device__ __forceinline__ int woff(int k, int g) {
+  return k * WROWB + ((((g >> 3) & 15) ^ swz4(k)) << 4) + ((g & 7) << 1);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
+  f32x2 v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+// (x0, x1) -> bf16 pairs h, m, l with x = h + m + l exactly (finite x)
+__device__ __forceinline__ void split2(float x0, float x1, uint32_t &h, uint32_t &m,
+                                       uint32_t &l) {
+  h = pack_bf16(x0, x1);
+  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xffff0000u);
+  m = pack_bf16(r0, r1);
+  l = pack_bf16(r0 - __uint_as_float(m << 16), r1 - __uint_as_float(m & 0xffff0000u));
+}
+// eight values -> the three bf16x8 fragments
+__device__ __forceinline__ void split8(const float *v, bf16x8 &h, bf16x8 &m, bf16x8 &l) {
+  uint32_t hh[4], mm[4], ll[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) split2(v[2 * i], v[2 * i + 1], hh[i], mm[i], ll[i]);
+  h = __builtin_bit_cast(bf16x8, make_uint4(hh[0], hh[1], hh[2], hh[3]));
+  m = __builtin_bit_cast(bf16x8, make_uint4(mm[0], mm[1], mm[2], mm[3]));
+  l = __builtin_bit_cast(bf16x8, make_uint4(ll[0], ll[1], ll[2], ll[3]));
+}
+
+__device__ __forceinline__ floatx16 mfma(const bf16x8 &a, const bf16x8 &b,
+                                         const floatx16 &c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// the six products of a split pair, small to large
+__device__ __forceinline__ floatx16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3],
+                                          floatx16 c) {
+  c = mfma(a[2], b[0], c);
+  c = mfma(a[0], b[2], c);
+  c = mfma(a[1], b[1], c);
+  c = mfma(a[1], b[0], c);
+  c = mfma(a[0], b[1], c);
+  c = mfma(a[0], b[0], c);
+  return c;
+}
+
+__device__ __forceinline__ floatx16 zero16() {
+  floatx16 z;
+#pragma unroll
+  for (int i = 0; i < 16; i++) z[i] = 0.0f;
+  return z;
+}
+
+__host__ __device__ inline int round4(int n) { return (n + 3) & ~3; }
+
+// PCM > 0: dY / dys are the pooled derivative dP of a 1 x 1 x PCM Maxpool,
+// pmask / pms its routing mask: dY[g][p] = bit g % PCM of mask[g / PCM][p] ?
+// dP[g / PCM][p] : +0 (hipF_maxpool_backprop_mask).
+template <int NCH, bool DX, bool WG, int PCM>
+__global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ dY, int dys,
+    const float *__restrict__ K, int ks, float *__restrict__ dX, int dxs,
+    float *__restrict__ ws_part, int ZZ, X6Steps steps, int dx_acc,
+    const unsigned char *__restrict__ pmask, int pms) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int P = g.P;
+  const int Hp = g.H + 2 * g.pad_h, Wp = g.W + 2 * g.pad_w;
+  const int CHWp = g.C * Hp * Wp;
+  char *Yp = smem;                                   // [3][32][384] bf16
+  char *Wimg = Yp + 3 * YPL;                         // [3][32][128] bf16
+  float *Zs = reinterpret_cast<float *>(Wimg + (DX ? 3 * WPL : 0));  // [P][ZZ]
+  float *Xs = Zs + (DX ? round4(P * ZZ) : 0);         // padded map + {1}
+  int *qtab = reinterpret_cast<int *>(Xs + round4(CHWp + 1));  // [384]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l = lane & 31, hf = lane >> 5;
+  const int CHW = g.C * g.HW;
+  const bool unpadded = g.pad_h == 0 && g.pad_w == 0;
+  const int ntile = (P + 31) >> 5;
+  const int PW = (P + 15) & ~15;     // wgrad contraction range (k16 steps)
+  const int NPQ = PW >> 2;           // position quads per image row
+  const int NU = 8 * NPQ;            // split units per slab
+
+  // W planes (dgrad B operand): rows k < Kdim, filters g < G; zero elsewhere
+  if (DX) {
+    for (int e = tid; e < 32 * 64; e += NT) {
+      const int k = e >> 6, gg = (e & 63) * 2;
+      const float v0 = (k < g.Kdim && gg < g.G) ? K[(int64_t)k * ks + gg] : 0.0f;
+      const float v1 = (k < g.Kdim && gg + 1 < g.G) ? K[(int64_t)k * ks + gg + 1] : 0.0f;
+      uint32_t h, m, lo;
+      split2(v0, v1, h, m, lo);
+      const int o = woff(k, gg);
+      *reinterpret_cast<uint32_t *>(Wimg + o) = h;
+      *reinterpret_cast<uint32_t *>(Wimg + WPL + o) = m;
+      *reinterpret_cast<uint32_t *>(Wimg + 2 * WPL + o) = lo;
+    }
+  }
+  // im2col addressing: lane l's A row is k = l (row Kdim and above: the
+  // constant-1 slot); position p of the frame at qtab[p] (past P: clamped to
+  // the constant slot too, where the dY image is 0)
+  int abase = CHWp * 4, qmul = 0;
+  if (l < g.Kdim) {
+    uint32_t c, r, qx, qy;
+    g.div_khkw.divmod((uint32_t)l, c, r);
+    g.div_kh.divmod(r, qx, qy);
+    abase = ((int)c * Hp * Wp + (int)qx * Hp + (int)qy) * 4;
+    qmul = 1;
+  }
+  if (WG) {
+    for (int e = tid; e < CHWp; e += NT) Xs[e] = 0.0f;
+    if (tid == 0) Xs[CHWp] = 1.0f;
+    for (int p = tid; p < PP; p += NT) {
+      uint32_t px, py;
+      g.div_oh.divmod((uint32_t)p, px, py);
+      qtab[p] = p < P ? ((int)px * Hp + (int)py) * 4 : 0x3fffffff;
+    }
+  }
+  const uint32_t amax = (uint32_t)CHWp * 4;
+  const char *Xb = reinterpret_cast<const char *>(Xs);
+
+  // ---- staging of one slab: unit u = (g quad gq, position quad pq) ----
+  float sv[MAXU][PCM > 0 ? 4 : 16];
+  unsigned mb[MAXU][PCM > 0 ? 4 : 1];
+  auto load_slab = [&](int n, int ch) {
+#pragma unroll
+    for (int i = 0; i < MAXU; ++i) {
+      const int u = tid + NT * i;
+      if (u >= NU) break;
+      const int gq = u / NPQ, p0 = (u - gq * NPQ) * 4;
+      if constexpr (PCM > 0) {
+        const int jj = (ch * 32 + 4 * gq) / PCM;
+        const float *src = dY + (int64_t)n * dys + (int64_t)jj * P;
+        const unsigned char *msrc = pmask + (int64_t)n * pms + (int64_t)jj * P;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sv[i][q] = p0 + q < P ? src[p0 + q] : 0.0f;
+          mb[i][q] = p0 + q < P ? (unsigned)msrc[p0 + q] : 0u;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float *src = dY + (int64_t)n * dys + (int64_t)(ch * 32 + 4 * gq + r) * P;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) sv[i][4 * r + q] = p0 + q < P ? src[p0 + q] : 0.0f;
+        }
+      }
+    }
+  };
+  auto split_slab = [&](int ch) {
+#pragma unroll
+    for (int i = 0; i < MAXU; ++i) {
+      const int u = tid + NT * i;
+      if (u >= NU) break;
+      const int gq = u / NPQ, p0 = (u - gq * NPQ) * 4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if constexpr (PCM > 0) {
+            // bit (4 gq + r) % PCM of the element's mask byte, sign-extended
+            const int bit = (4 * gq + r) % PCM;
+            const int sel = __builtin_amdgcn_sbfe((int)mb[i][q], bit, 1);
+            x[q] = __uint_as_float(__float_as_uint(sv[i][q]) & (unsigned)sel);
+          } else {
+            x[q] = sv[i][4 * r + q];
+          }
+        }
+        uint32_t h0, m0, l0, h1, m1, l1;
+        split2(x[0], x[1], h0, m0, l0);
+        split2(x[2], x[3], h1, m1, l1);
+        const int o = yoff(4 * gq + r, p0);
+        *reinterpret_cast<uint2 *>(Yp + o) = make_uint2(h0, h1);
+        *reinterpret_cast<uint2 *>(Yp + YPL + o) = make_uint2(m0, m1);
+        *reinterpret_cast<uint2 *>(Yp + 2 * YPL + o) = make_uint2(l0, l1);
+      }
+    }
+    (void)ch;
+  };
+
+  // ---- X map (wgrad) ----
+  float xv[MAXX];
+  auto load_x = [&](int n) {
+#pragma unroll
+    for (int i = 0; i < MAXX; i++)
+      if (tid + NT * i < CHW) xv[i] = X[(int64_t)n * xs + tid + NT * i];
+  };
+  auto commit_x = [&]() {
+#pragma unroll
+    for (int i = 0; i < MAXX; i++) {
+      const int e = tid + NT * i;
+      if (e < CHW) {
+        int slot = e;
+        if (!unpadded) {
+          uint32_t c, q, wi, hi;
+          g.div_HW.divmod((uint32_t)e, c, q);
+          g.div_H.divmod(q, wi, hi);
+          slot = (int)c * Hp * Wp + ((int)wi + g.pad_w) * Hp + (int)hi + g.pad_h;
+        }
+        Xs[slot] = xv[i];
+      }
+    }
+  };
+
+  // ---- col2im (dX) from Zs, as conv_bwd_dma_kernel ----
+  const int khkw = g.kh * g.kw;
+  const int zax = g.oh * ZZ - g.kh, zby = ZZ - 1;
+  int c2b[MAXX], c2r[MAXX];
+#pragma unroll
+  for (int i = 0; i < MAXX; i++) {
+    const int e = tid + NT * i;
+    c2b[i] = 0;
+    c2r[i] = (int)0xff000000u;
+    if (DX && e < CHW) {
+      uint32_t c, q, wi, hi;
+      g.div_HW.divmod((uint32_t)e, c, q);
+      g.div_H.divmod(q, wi, hi);
+      const int ty = (int)hi + g.pad_h, tx = (int)wi + g.pad_w;
+      c2b[i] = (tx * g.oh + ty) * ZZ + (int)c * khkw;
+      const int ylo = max(0, ty - g.oh + 1), yhi = min(g.kh - 1, ty);
+      const int xlo = max(0, tx - g.ow + 1), xhi = min(g.kw - 1, tx);
+      if (ylo <= yhi && xlo <= xhi)
+        c2r[i] = ylo | (yhi - ylo) << 8 | xlo << 16 | (xhi - xlo) << 24;
+    }
+  }
+  auto col2im = [&](int nn) {
+#pragma unroll
+    for (int i = 0; i < MAXX; i++) {
+      const int e = tid + NT * i;
+      if (e >= CHW) continue;
+      const int rg = c2r[i];
+      const int ylo = rg & 255, ny = (rg >> 8) & 255, xlo = (rg >> 16) & 255, nx = rg >> 24;
+      float sum = 0.0f;
+      for (int kx = xlo; kx <= xlo + nx; kx++) {
+        const int zk = c2b[i] - kx * zax;
+        for (int k0 = 0; k0 < g.kh; k0 += 8) {
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) v[u] = Zs[zk - (k0 + u) * zby];
+#pragma unroll
+          for (int u = 0; u < 8; u++)
+            sum += (unsigned)(k0 + u - ylo) <= (unsigned)ny ? v[u] : 0.0f;
+        }
+      }
+      float *d = dX + (int64_t)nn * dxs + e;
+      *d = dx_acc ? *d + sum : sum;
+    }
+  };
+
+  // Roles.  With both outputs, waves 0-3 run the data gradient (position
+  // tiles w, w + 4, w + 8) and waves 4-7 the weight gradient (the host's
+  // step table), so each SIMD pairs one of each (waves w and w + 4 share a
+  // SIMD) and each wave keeps only its own accumulators: the dgrad waves Z
+  // (3 tiles), the wgrad waves the frame's im2col fragments and the four
+  // slabs' gradient partials.  dX only: all 8 waves, tiles w and w + 8.
+  // Gradient only: the same wgrad waves and table as with dX (bitwise the
+  // same gradient), waves 0-3 only split.  Both roles run the same barrier
+  // sequence: every thread splits, commits the map and runs the col2im.
+  const bool dgrad_wave = DX && (!WG || wave < 4);
+  const int tslot = WG ? wave : wave, tstride = WG ? 4 : NW;
+  auto frames = [&](auto role) {
+    constexpr bool RD = decltype(role)::value == 1;  // dgrad role
+    constexpr bool RW = decltype(role)::value == 2;  // wgrad role
+    int my_steps = 0;
+    int stp[MAXS];
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) {
+      stp[s] = steps.s[wave][s];
+      if (RW && stp[s] != 0xff) my_steps = s + 1;
+    }
+    floatx16 wacc[RW ? NCH : 1];
+#pragma unroll
+    for (int c = 0; c < (RW ? NCH : 1); c++) wacc[c] = zero16();
+    bf16x8 ain[RW ? MAXS : 1][3];
+    int nprev = -1;
+    for (int n = blockIdx.x; n < g.R; n += gridDim.x) {
+      floatx16 zacc[RD ? MAXT : 1];
+#pragma unroll
+      for (int t = 0; t < (RD ? MAXT : 1); ++t) zacc[t] = zero16();
+#pragma unroll
+      for (int ch = 0; ch < NCH; ch++) {
+        __syncthreads();  // B1: the image's readers are done; last frame's Z is in LDS
+        if (ch == 0) {
+          if (WG) commit_x();
+          if (DX && nprev >= 0) col2im(nprev);
+        }
+        split_slab(ch);
+        __syncthreads();  // B2: the slab (and the frame's map) are in LDS
+        if (RW && ch == 0) {
+          // the frame's im2col values of this wave's steps, split once
+#pragma unroll
+          for (int s = 0; s < MAXS; ++s) {
+            if (s >= my_steps) break;
+            const int pbase = 16 * stp[s] + 8 * hf;
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t off = min((uint32_t)(abase + qmul * qtab[pbase + e]), amax);
+              v[e] = *reinterpret_cast<const float *>(Xb + off);
+            }
+            split8(v, ain[s][0], ain[s][1], ain[s][2]);
+          }
+        }
+        // the next slab (or the next frame's first slab and map) into registers
+        {
+          const int nn = ch + 1 < NCH ? n : n + (int)gridDim.x;
+          const int cc = ch + 1 < NCH ? ch + 1 : 0;
+          if (nn < g.R) {
+            load_slab(nn, cc);
+            if (WG && ch + 1 == NCH) load_x(nn);
+          }
+        }
+        if constexpr (RD) {
+          // Z[p][k] += dY^T W on this wave's position tiles
+          bf16x8 wf[2][3];
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+              wf[s][pl] = *reinterpret_cast<const bf16x8 *>(
+                  Wimg + pl * WPL + woff(l, ch * 32 + 16 * s + 8 * hf));
+          const int G4 = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+          for (int t = 0; t < MAXT; ++t) {
+            const int pt = tslot + tstride * t;
+            if (pt >= ntile) break;  // uniform
+            const int col = pt * 32 + 16 * (G4 & 1) + 4 * pp;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              bf16x8 af[3];
+              const int row = 16 * s + 8 * (G4 >> 1) + q;
+#pragma unroll
+              for (int pl = 0; pl < 3; ++pl) {
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (lds_s16x4 *)(Yp + pl * YPL + yoff(row, col)));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (lds_s16x4 *)(Yp + pl * YPL + yoff(row + 4, col)));
+                af[pl] = __builtin_bit_cast(
+                    bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+              }
+              zacc[t] = mfma6(af, wf[s], zacc[t]);
+            }
+          }
+        }
+        if constexpr (RW) {
+          // gW[k][g] += im2col(X) dY^T over this wave's k16 steps of p
+#pragma unroll
+          for (int s = 0; s < MAXS; ++s) {
+            if (s >= my_steps) break;
+            bf16x8 bf[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+              bf[pl] = *reinterpret_cast<const bf16x8 *>(Yp + pl * YPL +
+                                                         yoff(l, 16 * stp[s] + 8 * hf));
+            wacc[ch] = mfma6(ain[s], bf, wacc[ch]);
+          }
+        }
+      }
+      if constexpr (RD) {
+        // Z of this frame -> LDS (its last reader, the col2im in this frame's
+        // first split phase, finished before that phase's barrier)
+#pragma unroll
+        for (int t = 0; t < MAXT; ++t) {
+          const int pt = tslot + tstride * t;
+          if (pt >= ntile) break;
+#pragma unroll
+          for (int r = 0; r < 16; r++) {
+            const int pl = pt * 32 + mfma32_row(r, lane);
+            if (pl < P && l < g.Kdim) Zs[pl * ZZ + l] = zacc[t][r];
+          }
+        }
+      }
+      nprev = n;
+    }
+    if (DX && nprev >= 0) {
+      __syncthreads();
+      col2im(nprev);
+    }
+    if (!WG) return;
+    // the wgrad waves' partials (waves 4-7) summed in a fixed order
+    const int E = (g.Kdim + 1) * g.G;
+    float *dst = ws_part + (int64_t)blockIdx.x * E;
+    float *red = reinterpret_cast<float *>(Yp);  // [4][32 x 32], 16 KB
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++) {
+      __syncthreads();
+      if constexpr (RW) {
+        if (wave >= 4) {
+#pragma unroll
+          for (int r = 0; r < 16; r++)
+            red[(wave - 4) * 1024 + mfma32_row(r, lane) * 32 + l] = wacc[ch][r];
+        }
+      }
+      __syncthreads();
+      for (int e = tid; e < 1024; e += NT) {
+        const int i = e >> 5, j = e & 31;
+        if (i > g.Kdim) continue;
+        float sum = 0.0f;
+#pragma unroll
+        for (int w = 0; w < 4; w++) sum += red[w * 1024 + e];
+        dst[i * g.G + ch * 32 + j] = sum;
+      }
+    }
+  };
+  if (blockIdx.x < (unsigned)g.R) {
+    load_slab(blockIdx.x, 0);
+    if (WG) load_x(blockIdx.x);
+  }
+  if (dgrad_wave) frames(std::integral_constant<int, 1>{});
+  else frames(std::integral_constant<int, 2>{});
+}
+
+size_t x6_lds(const ConvGeom &g, bool dx) {
+  const int CHWp = g.C * (g.H + 2 * g.pad_h) * (g.W + 2 * g.pad_w);
+  const int ZZ = g.Kdim | 1;
+  return (size_t)3 * YPL + (dx ? 3 * WPL + (size_t)round4(g.P * ZZ) * 4 : 0) +
+         (size_t)round4(CHWp + 1) * 4 + (size_t)PP * 4;
+}
+
+}  // namespace
+
+// Eligible shapes: Kdim <= 31, 1 <= P <= 384, G a multiple of 32 up to 128,
+// C*H*W <= 2048, pc in {0, 4, 8}, and the LDS plan within 160 KB.
+bool kcnn_conv_bwd_x6_eligible(const ConvGeom &g, bool dx, int pc) {
+  if (g.Kdim > 31 || g.Kdim < 1 || g.P < 1 || g.P > PP) return false;
+  if (g.G % 32 != 0 || g.G > 128 || g.G == 0) return false;
+  if (g.C * g.HW > NT * MAXX) return false;
+  if (!(pc == 0 || pc == 4 || pc == 8)) return false;
+  return x6_lds(g, dx) <= (size_t)160 * 1024;
+}
+
+// One filter chunk (G <= 128): the workgroup partials ws_part[S][(Kdim+1) G]
+// (gW rows, then the bias row) for kcnn_conv_bwd_frame's reduction, S =
+// gridDim = min(R, 256); dX written (or added, dx_acc) when dX != NULL.
+int kcnn_conv_bwd_x6(const ConvGeom &g, const float *X, int xs, const float *dY, int dys,
+                     const float *K, int ks, float *dX, int dxs, float *ws_part, int S,
+                     int dx_acc, hipStream_t st, const unsigned char *pmask, int pms,
+                     int pc) {
+  const bool dx = dX != nullptr, wg = ws_part != nullptr;
+  if (!dx && !wg) return 0;
+  if (!kcnn_conv_bwd_x6_eligible(g, dx, pc)) return -1;
+  // wgrad k16 steps: each goes to the wave with the fewest MFMAs so far
+  // (a dgrad tile is 12, a step 6); the same table with or without dX would
+  // change the partial sums' split, so the table depends on dX only through
+  // the load, and the result is summed in a fixed order either way
+  // wgrad k16 steps dealt round-robin to waves 4-7 (the same table with or
+  // without dX: it fixes how the gradient splits over the waves' partials)
+  X6Steps tab;
+  for (int w = 0; w < NW; ++w)
+    for (int s = 0; s < MAXS; ++s) tab.s[w][s] = 0xff;
+  {
+    const int nstep = (g.P + 15) / 16;
+    if (nstep > 4 * MAXS) return -1;
+    for (int s = 0; s < nstep; ++s) tab.s[4 + s % 4][s / 4] = (uint8_t)s;
+  }
+  const size_t lds = x6_lds(g, dx);
+  const int ZZ = g.Kdim | 1;
+#define KCNN_X6P(NCH, DXB, WGB, PCM)                                                       \
+  do {                                                                                     \
+    static bool attr = hipFuncSetAttribute(                                               \
+        reinterpret_cast<const void *>(&conv_bwd_x6_kernel<NCH, DXB, WGB, PCM>),            \
+        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;             \
+    (void)attr;                                                                            \
+    hipLaunchKernelGGL((conv_bwd_x6_kernel<NCH, DXB, WGB, PCM>), dim3(S), dim3(NT), lds, st, \
+                       g, X, xs, dY, dys, K, ks, dX, dxs, ws_part, ZZ, tab, dx_acc, pmask, \
+                       pms);                                                               \
+  } while (0)
+#define KCNN_X6M(NCH, DXB, WGB)                   \
+  do {                                            \
+    if (pc == 4) KCNN_X6P(NCH, DXB, WGB, 4);      \
+    else if (pc == 8) KCNN_X6P(NCH, DXB, WGB, 8); \
+    else KCNN_X6P(NCH, DXB, WGB, 0);              \
+  } while (0)
+#define KCNN_X6N(NCH)                          \
+  do {                                         \
+    if (dx && wg) KCNN_X6M(NCH, true, true);   \
+    else if (wg) KCNN_X6M(NCH, false, true);   \
+    else KCNN_X6M(NCH, true, false);           \
+  } while (0)
+  switch (g.G / 32) {
+    case 1: KCNN_X6N(1); break;
+    case 2: KCNN_X6N(2); break;
+    case 3: KCNN_X6N(3); break;
+    default: KCNN_X6N(4); break;
+  }
+#undef KCNN_X6N
+#undef KCNN_X6M
+#undef KCNN_X6P
+  return (int)hipGetLastError();
+}

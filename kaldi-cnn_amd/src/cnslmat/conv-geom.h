@@ -70,6 +70,13 @@ int kcnn_conv_bwd_frame(const kcnn::ConvGeom &g, const float *X, int xs,
                         void *ws, size_t ws_bytes, hipStream_t st,
                         const unsigned char *pmask = nullptr, int pms = 0,
                         int pc = 0);
+// The same fused backward on the bf16 MFMAs with exact three-way operand
+// splits (cnsl-conv-x6.hip); ws_part == NULL runs the data gradient only.
+bool kcnn_conv_bwd_x6_eligible(const kcnn::ConvGeom &g, bool dx, int pc);
+int kcnn_conv_bwd_x6(const kcnn::ConvGeom &g, const float *X, int xs, const float *dY,
+                     int dys, const float *K, int ks, float *dX, int dxs, float *ws_part,
+                     int S, int dx_acc, hipStream_t st, const unsigned char *pmask,
+                     int pms, int pc);
 size_t kcnn_conv_wgrad_frame_ws(const kcnn::ConvGeom &g);
 int kcnn_conv_wgrad_frame(const kcnn::ConvGeom &g, const float *X, int xs,
                           const float *dY, int dys, float *gW, int gws,

@@ -53,7 +53,9 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int NT = 512, NW = NT / 64;
 constexpr int PP = 384;             // positions per image row (768 B)
@@ -129,6 +131,14 @@ __device__ __forceinline__ floatx16 zero16() {
 }
 
 __host__ __device__ inline int round4(int n) { return (n + 3) & ~3; }
+// staging floats for one slab's dP rows (whole 1-KiB DMA chunks), and bytes
+// for its mask (whole 256-B chunks)
+__host__ __device__ inline int x6_stage_floats(int P, int pcm) {
+  return (((pcm > 0 ? 32 / pcm : 32) * P * 4 + 1023) & ~1023) / 4;
+}
+__host__ __device__ inline int x6_stage_mask_bytes(int P, int pcm) {
+  return pcm > 0 ? (((32 / pcm) * P + 255) & ~255) : 0;
+}
 
 // PCM > 0: dY / dys are the pooled derivative dP of a 1 x 1 x PCM Maxpool,
 // pmask / pms its routing mask: dY[g][p] = bit g % PCM of mask[g / PCM][p] ?
@@ -143,11 +153,23 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
   const int P = g.P;
   const int Hp = g.H + 2 * g.pad_h, Wp = g.W + 2 * g.pad_w;
   const int CHWp = g.C * Hp * Wp;
+  // DEFER (PCM > 0): Z has its own buffer and the col2im of frame n runs in
+  // frame n+1's first split phase.  PCM == 0 needs that space to stage the
+  // raw dY slab (46 KB at c2), so Z goes to the image at the frame's end and
+  // is col2im'ed there, between two more barriers.
+  constexpr bool DEFER = PCM > 0;
   char *Yp = smem;                                   // [3][32][384] bf16
   char *Wimg = Yp + 3 * YPL;                         // [3][32][128] bf16
-  float *Zs = reinterpret_cast<float *>(Wimg + (DX ? 3 * WPL : 0));  // [P][ZZ]
-  float *Xs = Zs + (DX ? round4(P * ZZ) : 0);         // padded map + {1}
+  float *Zs = DEFER ? reinterpret_cast<float *>(Wimg + (DX ? 3 * WPL : 0))  // [P][ZZ]
+                    : reinterpret_cast<float *>(Yp);
+  float *Xs = reinterpret_cast<float *>(Wimg + (DX ? 3 * WPL : 0)) +
+              (DX && DEFER ? round4(P * ZZ) : 0);    // padded map + {1}
   int *qtab = reinterpret_cast<int *>(Xs + round4(CHWp + 1));  // [384]
+  // the next slab's raw values, landed by LDS-DMA: PCM > 0 its dP rows and
+  // mask bytes, PCM == 0 its 32 rows of dY
+  constexpr int NJ = PCM > 0 ? 32 / PCM : 32;
+  float *Sdp = reinterpret_cast<float *>(qtab + PP);          // [NJ][P] (+ DMA tail)
+  unsigned char *Smk = reinterpret_cast<unsigned char *>(Sdp + x6_stage_floats(P, PCM));
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = lane & 31, hf = lane >> 5;
@@ -156,7 +178,8 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
   const int ntile = (P + 31) >> 5;
   const int PW = (P + 15) & ~15;     // wgrad contraction range (k16 steps)
   const int NPQ = PW >> 2;           // position quads per image row
-  const int NU = 8 * NPQ;            // split units per slab
+  const int NU = (PCM > 0 ? NJ : 8) * NPQ;  // split units per slab
+  (void)Smk;
 
   // W planes (dgrad B operand): rows k < Kdim, filters g < G; zero elsewhere
   if (DX) {
@@ -195,32 +218,28 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
   const uint32_t amax = (uint32_t)CHWp * 4;
   const char *Xb = reinterpret_cast<const char *>(Xs);
 
-  // ---- staging of one slab: unit u = (g quad gq, position quad pq) ----
-  float sv[MAXU][PCM > 0 ? 4 : 16];
-  unsigned mb[MAXU][PCM > 0 ? 4 : 1];
+  // ---- staging of one slab ----
+  // LDS-DMA into Sdp (16 B per lane) / Smk (4 B per lane); a DMA lands by
+  // the next barrier (s_waitcnt vmcnt(0)).  PCM > 0: the slab's NJ rows of
+  // dP and of the mask, unit u = (pooled row j, position quad pq); PCM == 0:
+  // its 32 rows of dY, unit u = (filter quad gq, position quad pq).
   auto load_slab = [&](int n, int ch) {
-#pragma unroll
-    for (int i = 0; i < MAXU; ++i) {
-      const int u = tid + NT * i;
-      if (u >= NU) break;
-      const int gq = u / NPQ, p0 = (u - gq * NPQ) * 4;
-      if constexpr (PCM > 0) {
-        const int jj = (ch * 32 + 4 * gq) / PCM;
-        const float *src = dY + (int64_t)n * dys + (int64_t)jj * P;
-        const unsigned char *msrc = pmask + (int64_t)n * pms + (int64_t)jj * P;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          sv[i][q] = p0 + q < P ? src[p0 + q] : 0.0f;
-          mb[i][q] = p0 + q < P ? (unsigned)msrc[p0 + q] : 0u;
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float *src = dY + (int64_t)n * dys + (int64_t)(ch * 32 + 4 * gq + r) * P;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) sv[i][4 * r + q] = p0 + q < P ? src[p0 + q] : 0.0f;
-        }
-      }
+    const int rowf = (PCM > 0 ? g.G / PCM : g.G) * P;  // values per frame row
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(dY + (int64_t)n * dys), (short)0, rowf * 4, 0x00020000);
+    const int nq = (NJ * P * 4 + 1023) >> 10;
+    for (int q = wave; q < nq; q += NW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rd, (lds_void_t *)(Sdp + q * 256), 16,
+                                               (uint32_t)lane * 16u,
+                                               (uint32_t)(ch * NJ * P * 4 + q * 1024), 0, 0);
+    if constexpr (PCM > 0) {
+      const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(pmask + (int64_t)n * pms), (short)0, rowf, 0x00020000);
+      const int nm = (NJ * P + 255) >> 8;
+      for (int q = wave; q < nm; q += NW)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, (lds_void_t *)(Smk + q * 256), 4,
+                                                 (uint32_t)lane * 4u,
+                                                 (uint32_t)(ch * NJ * P + q * 256), 0, 0);
     }
   };
   auto split_slab = [&](int ch) {
@@ -228,28 +247,51 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
     for (int i = 0; i < MAXU; ++i) {
       const int u = tid + NT * i;
       if (u >= NU) break;
-      const int gq = u / NPQ, p0 = (u - gq * NPQ) * 4;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      if constexpr (PCM > 0) {
+        // split the pooled values once, then gate the planes per map: map c
+        // of the pool group gets the value where bit c of the mask byte is
+        // set (the in_value == out_value test of Maxpool_backprop), +0 else
+        const int j = u / NPQ, p0 = (u - j * NPQ) * 4;
         float x[4];
+        unsigned mk[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          if constexpr (PCM > 0) {
-            // bit (4 gq + r) % PCM of the element's mask byte, sign-extended
-            const int bit = (4 * gq + r) % PCM;
-            const int sel = __builtin_amdgcn_sbfe((int)mb[i][q], bit, 1);
-            x[q] = __uint_as_float(__float_as_uint(sv[i][q]) & (unsigned)sel);
-          } else {
-            x[q] = sv[i][4 * r + q];
-          }
+          const bool in = p0 + q < P;
+          x[q] = in ? Sdp[j * P + p0 + q] : 0.0f;
+          mk[q] = in ? (unsigned)Smk[j * P + p0 + q] : 0u;
         }
-        uint32_t h0, m0, l0, h1, m1, l1;
-        split2(x[0], x[1], h0, m0, l0);
-        split2(x[2], x[3], h1, m1, l1);
-        const int o = yoff(4 * gq + r, p0);
-        *reinterpret_cast<uint2 *>(Yp + o) = make_uint2(h0, h1);
-        *reinterpret_cast<uint2 *>(Yp + YPL + o) = make_uint2(m0, m1);
-        *reinterpret_cast<uint2 *>(Yp + 2 * YPL + o) = make_uint2(l0, l1);
+        uint32_t h01, m01, l01, h23, m23, l23;
+        split2(x[0], x[1], h01, m01, l01);
+        split2(x[2], x[3], h23, m23, l23);
+        const s16x2 w01 = __builtin_bit_cast(s16x2, mk[0] | (mk[1] << 16));
+        const s16x2 w23 = __builtin_bit_cast(s16x2, mk[2] | (mk[3] << 16));
+#pragma unroll
+        for (int c = 0; c < PCM; ++c) {
+          // bit c of each 16-bit half, sign-extended to 0 / 0xffff
+          const s16x2 sh = {(short)(15 - c), (short)(15 - c)}, k15 = {15, 15};
+          const uint32_t s01 = __builtin_bit_cast(uint32_t, (s16x2)((w01 << sh) >> k15));
+          const uint32_t s23 = __builtin_bit_cast(uint32_t, (s16x2)((w23 << sh) >> k15));
+          const int o = yoff(j * PCM + c, p0);
+          *reinterpret_cast<uint2 *>(Yp + o) = make_uint2(h01 & s01, h23 & s23);
+          *reinterpret_cast<uint2 *>(Yp + YPL + o) = make_uint2(m01 & s01, m23 & s23);
+          *reinterpret_cast<uint2 *>(Yp + 2 * YPL + o) = make_uint2(l01 & s01, l23 & s23);
+        }
+      } else {
+        const int gq = u / NPQ, p0 = (u - gq * NPQ) * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float *srow = Sdp + (4 * gq + r) * P + p0;
+          float x[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x[q] = p0 + q < P ? srow[q] : 0.0f;
+          uint32_t h0, m0, l0, h1, m1, l1;
+          split2(x[0], x[1], h0, m0, l0);
+          split2(x[2], x[3], h1, m1, l1);
+          const int o = yoff(4 * gq + r, p0);
+          *reinterpret_cast<uint2 *>(Yp + o) = make_uint2(h0, h1);
+          *reinterpret_cast<uint2 *>(Yp + YPL + o) = make_uint2(m0, m1);
+          *reinterpret_cast<uint2 *>(Yp + 2 * YPL + o) = make_uint2(l0, l1);
+        }
       }
     }
     (void)ch;
@@ -279,37 +321,25 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
     }
   };
 
-  // ---- col2im (dX) from Zs, as conv_bwd_dma_kernel ----
+  // ---- col2im (dX) from Zs, as conv_bwd_dma_kernel (tap ranges per call:
+  // a few VALU per output and frame instead of two registers held all along)
   const int khkw = g.kh * g.kw;
   const int zax = g.oh * ZZ - g.kh, zby = ZZ - 1;
-  int c2b[MAXX], c2r[MAXX];
-#pragma unroll
-  for (int i = 0; i < MAXX; i++) {
-    const int e = tid + NT * i;
-    c2b[i] = 0;
-    c2r[i] = (int)0xff000000u;
-    if (DX && e < CHW) {
-      uint32_t c, q, wi, hi;
-      g.div_HW.divmod((uint32_t)e, c, q);
-      g.div_H.divmod(q, wi, hi);
-      const int ty = (int)hi + g.pad_h, tx = (int)wi + g.pad_w;
-      c2b[i] = (tx * g.oh + ty) * ZZ + (int)c * khkw;
-      const int ylo = max(0, ty - g.oh + 1), yhi = min(g.kh - 1, ty);
-      const int xlo = max(0, tx - g.ow + 1), xhi = min(g.kw - 1, tx);
-      if (ylo <= yhi && xlo <= xhi)
-        c2r[i] = ylo | (yhi - ylo) << 8 | xlo << 16 | (xhi - xlo) << 24;
-    }
-  }
   auto col2im = [&](int nn) {
 #pragma unroll
     for (int i = 0; i < MAXX; i++) {
       const int e = tid + NT * i;
       if (e >= CHW) continue;
-      const int rg = c2r[i];
-      const int ylo = rg & 255, ny = (rg >> 8) & 255, xlo = (rg >> 16) & 255, nx = rg >> 24;
+      uint32_t c, q, wi, hi;
+      g.div_HW.divmod((uint32_t)e, c, q);
+      g.div_H.divmod(q, wi, hi);
+      const int ty = (int)hi + g.pad_h, tx = (int)wi + g.pad_w;
+      const int zb = (tx * g.oh + ty) * ZZ + (int)c * khkw;
+      const int ylo = max(0, ty - g.oh + 1), ny = min(g.kh - 1, ty) - ylo;
+      const int xlo = max(0, tx - g.ow + 1), xhi = min(g.kw - 1, tx);
       float sum = 0.0f;
-      for (int kx = xlo; kx <= xlo + nx; kx++) {
-        const int zk = c2b[i] - kx * zax;
+      for (int kx = xlo; kx <= xhi; kx++) {
+        const int zk = zb - kx * zax;
         for (int k0 = 0; k0 < g.kh; k0 += 8) {
           float v[8];
 #pragma unroll
@@ -359,7 +389,7 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
         __syncthreads();  // B1: the image's readers are done; last frame's Z is in LDS
         if (ch == 0) {
           if (WG) commit_x();
-          if (DX && nprev >= 0) col2im(nprev);
+          if (DX && DEFER && nprev >= 0) col2im(nprev);
         }
         split_slab(ch);
         __syncthreads();  // B2: the slab (and the frame's map) are in LDS
@@ -433,9 +463,10 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
           }
         }
       }
+      if (DX && !DEFER) __syncthreads();  // the image is read no more: Z goes there
       if constexpr (RD) {
-        // Z of this frame -> LDS (its last reader, the col2im in this frame's
-        // first split phase, finished before that phase's barrier)
+        // Z of this frame -> LDS (DEFER: its last reader, the col2im in this
+        // frame's first split phase, finished before that phase's barrier)
 #pragma unroll
         for (int t = 0; t < MAXT; ++t) {
           const int pt = tslot + tstride * t;
@@ -447,9 +478,13 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
           }
         }
       }
+      if (DX && !DEFER) {
+        __syncthreads();
+        col2im(n);
+      }
       nprev = n;
     }
-    if (DX && nprev >= 0) {
+    if (DX && DEFER && nprev >= 0) {
       __syncthreads();
       col2im(nprev);
     }
@@ -487,11 +522,13 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
   else frames(std::integral_constant<int, 2>{});
 }
 
-size_t x6_lds(const ConvGeom &g, bool dx) {
+size_t x6_lds(const ConvGeom &g, bool dx, int pc) {
   const int CHWp = g.C * (g.H + 2 * g.pad_h) * (g.W + 2 * g.pad_w);
   const int ZZ = g.Kdim | 1;
-  return (size_t)3 * YPL + (dx ? 3 * WPL + (size_t)round4(g.P * ZZ) * 4 : 0) +
-         (size_t)round4(CHWp + 1) * 4 + (size_t)PP * 4;
+  return (size_t)3 * YPL + (dx ? 3 * WPL : 0) +
+         (dx && pc > 0 ? (size_t)round4(g.P * ZZ) * 4 : 0) +
+         (size_t)round4(CHWp + 1) * 4 + (size_t)PP * 4 +
+         (size_t)x6_stage_floats(g.P, pc) * 4 + (size_t)x6_stage_mask_bytes(g.P, pc);
 }
 
 }  // namespace
@@ -503,7 +540,7 @@ bool kcnn_conv_bwd_x6_eligible(const ConvGeom &g, bool dx, int pc) {
   if (g.G % 32 != 0 || g.G > 128 || g.G == 0) return false;
   if (g.C * g.HW > NT * MAXX) return false;
   if (!(pc == 0 || pc == 4 || pc == 8)) return false;
-  return x6_lds(g, dx) <= (size_t)160 * 1024;
+  return x6_lds(g, dx, pc) <= (size_t)160 * 1024;
 }
 
 // One filter chunk (G <= 128): the workgroup partials ws_part[S][(Kdim+1) G]
@@ -516,6 +553,9 @@ int kcnn_conv_bwd_x6(const ConvGeom &g, const float *X, int xs, const float *dY,
   const bool dx = dX != nullptr, wg = ws_part != nullptr;
   if (!dx && !wg) return 0;
   if (!kcnn_conv_bwd_x6_eligible(g, dx, pc)) return -1;
+  // LDS-DMA of dP (16 B per lane) and of the mask (4 B per lane)
+  if ((uintptr_t)dY % 16 || dys % 4) return -1;
+  if (pc > 0 && ((uintptr_t)pmask % 4 || pms % 4)) return -1;
   // wgrad k16 steps: each goes to the wave with the fewest MFMAs so far
   // (a dgrad tile is 12, a step 6); the same table with or without dX would
   // change the partial sums' split, so the table depends on dX only through
@@ -530,7 +570,7 @@ int kcnn_conv_bwd_x6(const ConvGeom &g, const float *X, int xs, const float *dY,
     if (nstep > 4 * MAXS) return -1;
     for (int s = 0; s < nstep; ++s) tab.s[4 + s % 4][s / 4] = (uint8_t)s;
   }
-  const size_t lds = x6_lds(g, dx);
+  const size_t lds = x6_lds(g, dx, pc);
   const int ZZ = g.Kdim | 1;
 #define KCNN_X6P(NCH, DXB, WGB, PCM)                                                       \
   do {                                                                                     \

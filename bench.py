@@ -30,6 +30,7 @@ P = OH * OW
 POOL_OUT = P * G // PC
 PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 matrix (dense)
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 matrix (dense, spec)
 
 # Algorithmic work per frame (SURVEY 8d / BASELINE.md 3).
 CONV_FLOP_PER_PASS = 2 * P * G * KH * KW * C          # 2,230,272
@@ -419,13 +420,18 @@ def main():
                              "hbm_frac": round(byts / ms / 1e6 / PEAK_HBM_GBS, 4),
                              "TFLOP/s": round(flop / ms / 1e9, 2) if flop else None,
                              "mfma_frac": round(flop / ms / 1e9 / PEAK_FP32_MFMA_TFLOPS, 4) if flop else None}
+    gemm_x6 = os.environ.get("KCNN_GEMM", "1") != "0"
     if k_fc[1]:
-        kernels["fc_gemms_rocblas"] = {
+        # FullyConnectedComponent's three GEMMs (CuMatrixBase::AddMatMat):
+        # the in-house bf16x6 kernel (kaldi-lite/cu-gemm-x6.hip) by default,
+        # rocBLAS sgemm with KCNN_GEMM=0
+        kernels["fc_gemms"] = {
+            "engine": "bf16x6 (cu-gemm-x6.hip)" if gemm_x6 else "rocBLAS sgemm",
             "ms_per_step": round(k_fc[0] / args.steps, 4),
             "TFLOP/s": round(FC_FLOP * B / (k_fc[0] / args.steps) / 1e9, 2)}
 
     # Dominant hand-written hot-path kernel by time.
-    dom = max((k for k in kernels if not k.startswith("fc")),
+    dom = max((k for k in kernels if not k.startswith("fc_")),
               key=lambda k: kernels[k]["ms"], default=None)
     roofline = None
     if dom:
@@ -451,6 +457,17 @@ def main():
                     "algorithmic_bytes_per_launch": dk["bytes"],
                     "algorithmic_flop_per_launch": dk["flop"],
                     "launch_ms": dk["ms"]}
+        if dk["bound"] == "mfma" and dom.startswith("conv_bwd") and \
+                os.environ.get("KCNN_BWD_X6", "1") != "0":
+            # the backward computes its fp32 products on the bf16 matrix cores
+            # (cnsl-conv-x6.hip: each operand split exactly into three bf16
+            # parts, six products kept).  `frac` prices the fp32 work against
+            # the fp32 MFMA peak (north_star's target); this is the fraction of
+            # the bf16 engine's dense peak that the six products occupy.
+            roofline["engine"] = {
+                "mfma": "v_mfma_f32_32x32x16_bf16, fp32 operands split 3-way, 6 products",
+                "bf16_dense_peak_tflops": PEAK_BF16_MFMA_TFLOPS,
+                "frac_of_bf16_peak": round(6 * achieved / PEAK_BF16_MFMA_TFLOPS, 4)}
 
     if rank == 0:
         result = {

@@ -2,6 +2,7 @@
 #include "cu-matrix.h"
 
 #include <math.h>
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -268,12 +269,22 @@ void CuMatrixBase<Real>::AddMatMat(Real alpha, const CuMatrixBase<Real> &A,
   CuProfileScope prof("AddMatMat");
   CuDevice &dev0 = CuDevice::Instantiate();
   if (dev0.GemmMode() == 1) {
-    // fp32 product on the bf16 MFMAs (exact operand split, cu-gemm-x6.hip);
-    // declines only operands its 16-B loads cannot address
+    // fp32 product on the bf16 MFMAs (exact operand split, cu-gemm-x6.hip).
+    // Its 16-B loads need the K-contiguous operands (A untransposed, B
+    // transposed) row-aligned; one that is not (a caller's matrix with an
+    // odd pitch, e.g. an output derivative of 3454 columns) is copied once
+    // into a padded-pitch CuMatrix, which costs far less than the GEMM.
+    auto aligned = [](const CuMatrixBase<Real> &X) {
+      return X.Stride() % 4 == 0 && reinterpret_cast<uintptr_t>(X.Data()) % 16 == 0;
+    };
+    CuMatrix<Real> Acopy, Bcopy;
+    const CuMatrixBase<Real> *Ap = &A, *Bp = &B;
+    if (transA == kNoTrans && !aligned(A)) { Acopy = A; Ap = &Acopy; }
+    if (transB == kTrans && !aligned(B)) { Bcopy = B; Bp = &Bcopy; }
     const size_t wsb = kl_gemm_x6_workspace_bytes(m, n, k);
     void *ws = wsb ? dev0.Malloc(wsb) : nullptr;
     const int rc = kl_gemm_x6(transA == kTrans, transB == kTrans, m, n, k, alpha,
-                              A.Data(), A.Stride(), B.Data(), B.Stride(), beta,
+                              Ap->Data(), Ap->Stride(), Bp->Data(), Bp->Stride(), beta,
                               data_, stride_, ws, wsb, S());
     if (ws) dev0.Free(ws);
     if (rc != (int)hipErrorInvalidValue) {

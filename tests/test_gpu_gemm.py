@@ -88,6 +88,9 @@ def test_gemm_x6_beta_zero_ignores_nan(kc):
     ("fc_fwd", 4096, 1024, 11616, False, True),     # out = in W^T
     ("fc_dgrad", 4096, 11616, 1024, False, False),  # in_deriv = out_deriv W
     ("fc_wgrad", 1024, 11616, 4096, True, False),   # gW = out_deriv^T in
+    # nnet.config's last FC dX: out_deriv has 3454 columns and that pitch, so
+    # its rows are not 16-B aligned; AddMatMat copies it to a padded pitch
+    ("nnet_fc3_dgrad", 4096, 4096, 3454, False, False),
 ])
 def test_gemm_c2_fc_shapes(kc, name, m, n, k, ta, tb):
     """The c2 stack's three FC GEMMs at full size: the split kernel meets the

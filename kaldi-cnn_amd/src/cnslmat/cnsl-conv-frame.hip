@@ -27,6 +27,7 @@
 #include <stdlib.h>
 
 #include "conv-geom.h"
+#include "x6-util.h"
 
 using namespace kcnn;
 
@@ -224,12 +225,18 @@ __global__ __launch_bounds__(256) void conv_fwd_slab_kernel(
 // Backprop (A.9) would recompute from Y.
 // PC == -1: a 3-D window (ph x pw x pc, runtime; pc divides 32) pooled from
 // the same slab, with a 16-bit mask (bit c*pw*ph + w*ph + h).
+// X6: the products on the bf16 matrix cores (x6-util.h).  KS is then the
+// number of k16 steps; A = W^T split into its three bf16 planes once per
+// kernel (4 groups x KS x 3 fragments in VGPRs), with the bias as row k =
+// Kdim against a constant-1 row of B, so the accumulators hold conv + bias
+// and no epilogue add remains; B = the gathered im2col values, split in
+// registers once per frame and tile.  Unpadded maps only (host check).
 struct PoolWin {
   int ph, pw, pc, oh2, OP;
   FastDiv div_OP, div_oh2;
 };
 
-template <int KS, int FT, int PC>
+template <int KS, int FT, int PC, bool X6>
 __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
     ConvGeom g, const float *__restrict__ X, int xs,
     const float *__restrict__ K, int ks, const float *__restrict__ bias,
@@ -240,29 +247,52 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
   float *T = reinterpret_cast<float *>(smem);                 // [32][P]
   float *Bs = T + ((32 * g.P + 3) & ~3);                      // [128] bias
   int2 *koff = reinterpret_cast<int2 *>(Bs + 128);             // [2*KS] taps
-  float *Xs = reinterpret_cast<float *>(koff + 2 * KS);         // [C*HW]
+  constexpr int NKT = X6 ? 16 * KS : 2 * KS;                    // tap entries (<= 32)
+  float *Xs = reinterpret_cast<float *>(koff + NKT);            // [C*HW]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = lane & 31, h = lane >> 5;
   const int NG = (g.G + 31) >> 5;  // <= 4 (host check)
   if (tid < 128) Bs[tid] = (bias && tid < g.G) ? bias[tid] : 0.0f;
   // A operand: W[k = 2s + h][gb*32 + l]
-  float wreg[4][KS];
+  float wreg[X6 ? 1 : 4][X6 ? 1 : KS];
+  // X6: W^T[gb*32 + l][k = 16s + 8h + e] (e < 8), the bias at k = Kdim
+  x6::bf16x8 w6[X6 ? 4 : 1][X6 ? KS : 1][3];
+  if constexpr (X6) {
 #pragma unroll
-  for (int gb = 0; gb < 4; gb++)
+    for (int gb = 0; gb < 4; gb++)
 #pragma unroll
-    for (int s = 0; s < KS; s++) {
-      const int k = 2 * s + h, gg = gb * 32 + l;
-      wreg[gb][s] = (k < g.Kdim && gg < g.G) ? K[(int64_t)k * ks + gg] : 0.0f;
-    }
-  // tap k -> (channel offset, kx << 16 | ky); padded taps never in bounds
-  if (tid < 2 * KS) {
+      for (int s = 0; s < KS; s++) {
+        const int gg = gb * 32 + l;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          const int k = 16 * s + 8 * h + e;
+          v[e] = gg >= g.G ? 0.0f
+                 : k < g.Kdim ? K[(int64_t)k * ks + gg]
+                 : (k == g.Kdim && bias) ? bias[gg] : 0.0f;
+        }
+        x6::split8(v, w6[gb][s][0], w6[gb][s][1], w6[gb][s][2]);
+      }
+  } else {
+#pragma unroll
+    for (int gb = 0; gb < 4; gb++)
+#pragma unroll
+      for (int s = 0; s < KS; s++) {
+        const int k = 2 * s + h, gg = gb * 32 + l;
+        wreg[gb][s] = (k < g.Kdim && gg < g.G) ? K[(int64_t)k * ks + gg] : 0.0f;
+      }
+  }
+  // tap k -> (channel offset, kx << 16 | ky); padded taps never in bounds.
+  // X6 (unpadded maps): tap k -> its map offset c*HW + kx*H + ky in .x
+  if (tid < NKT) {
     int2 v = make_int2(0, 0x3fff << 16);
     if (tid < g.Kdim) {
       uint32_t c, r, qx, qy;
       g.div_khkw.divmod((uint32_t)tid, c, r);
       g.div_kh.divmod(r, qx, qy);
-      v = make_int2((int)c * g.HW, (int)((qx << 16) | qy));
+      v = X6 ? make_int2((int)c * g.HW + (int)qx * g.H + (int)qy, 0)
+             : make_int2((int)c * g.HW, (int)((qx << 16) | qy));
     }
     koff[tid] = v;
   }
@@ -302,9 +332,33 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
     }
     __syncthreads();
     KCNN_TMARK(0)
-    float bx[FT][KS];
+    float bx[X6 ? 1 : FT][X6 ? 1 : KS];
+    x6::bf16x8 bx6[X6 ? FT : 1][X6 ? KS : 1][3];
 #pragma unroll
     for (int t = 0; t < FT; t++) {
+      if constexpr (X6) {
+        // B[k = 16s + 8h + e][p]: the map value of tap k at p (one add: the
+        // maps are unpadded, so every tap of a valid position is inside),
+        // 1 at k = Kdim (the bias row), 0 past it; positions past P read a
+        // clamped position and are never stored
+        if ((wave + 4 * t) * 32 >= g.P) continue;  // wave-uniform: no tile
+        const int p = min((wave + 4 * t) * 32 + l_f, g.P - 1);
+        uint32_t px, py;
+        g.div_oh.divmod((uint32_t)p, px, py);
+        const int pb = (int)px * g.H + (int)py;
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; e++) {
+            const int k = 16 * s + 8 * h_f + e;
+            const float xval = Xs[koff[k].x + pb];
+            v[e] = k < g.Kdim ? xval : (k == g.Kdim ? 1.0f : 0.0f);
+          }
+          x6::split8(v, bx6[t][s][0], bx6[t][s][1], bx6[t][s][2]);
+        }
+        continue;
+      }
       const int p = (wave + 4 * t) * 32 + l_f;
       const bool pv = p < g.P;
       uint32_t px = 0, py = 0;
@@ -320,20 +374,71 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
       }
     }
     KCNN_TMARK(1)
+    if constexpr (X6 && (PC == 2 || PC == 4)) {
+      if (out == nullptr) {  // uniform: pooled straight from the registers
+        // items (gb, t) in order; the MFMA chain of item i is issued before
+        // the pooling of item i - 1, so that VALU work runs under the chain
+        constexpr int NI = 4 * FT;
+        floatx16 accp[2];
+        auto valid = [&](int i) { return i / FT < NG && wave + 4 * (i % FT) < ntile; };
+#pragma unroll
+        for (int i = 0; i <= NI; i++) {
+          if (i < NI && valid(i)) {
+            const int gb = i / FT, t = i % FT;
+            floatx16 a = zero16();
+#pragma unroll
+            for (int s = 0; s < KS; s++) a = x6::mfma6(w6[gb][s], bx6[t][s], a);
+            accp[i & 1] = a;
+          }
+          if (i == 0 || !valid(i - 1)) continue;
+          const int gb = (i - 1) / FT, t = (i - 1) % FT;
+          const floatx16 &acc = accp[(i - 1) & 1];
+          const int p = (wave + 4 * t) * 32 + l_f;
+          if (p >= g.P) continue;
+          // accumulator r = 4k + i of lane (l, h) is filter 8k + 4h + i at
+          // position p: a pool group is PC consecutive registers (the
+          // compares and order of the LDS epilogue, so the same bits)
+          float *pd = pool + (int64_t)n * ps + p;
+          unsigned char *md = mask + (int64_t)n * ms + p;
+#pragma unroll
+          for (int r0 = 0; r0 < 16; r0 += PC) {
+            const int row = gb * 32 + mfma32_row(r0, lane_f);
+            if (row >= g.G) continue;
+            float mx = -1e20f;
+#pragma unroll
+            for (int c = 0; c < PC; c++)
+              if (mx < acc[r0 + c]) mx = acc[r0 + c];
+            unsigned m = 0;
+#pragma unroll
+            for (int c = 0; c < PC; c++) m |= (acc[r0 + c] == mx ? 1u : 0u) << c;
+            const int64_t off = (int64_t)(row / PC) * g.P;
+            pd[off] = mx;
+            md[off] = (unsigned char)m;
+          }
+        }
+        KCNN_TMARK(2)
+        continue;  // next frame
+      }
+    }
 #pragma unroll
     for (int gb = 0; gb < 4; gb++) {
       if (gb >= NG) break;
-      float bsv[16];  // this lane_f's 16 accumulator rows' bias, read ahead
+      float bsv[16];  // this lane_f's 16 accumulator rows' bias, read ahead (X6: 0, in acc)
 #pragma unroll
-      for (int r = 0; r < 16; r++) bsv[r] = Bs[gb * 32 + mfma32_row(r, lane_f)];
+      for (int r = 0; r < 16; r++) bsv[r] = X6 ? 0.0f : Bs[gb * 32 + mfma32_row(r, lane_f)];
 #pragma unroll
       for (int t = 0; t < FT; t++) {
         const int pt = wave + 4 * t;
         if (pt >= ntile) continue;  // wave-uniform
         floatx16 acc = zero16();
+        if constexpr (X6) {
 #pragma unroll
-        for (int s = 0; s < KS; s++)
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wreg[gb][s], bx[t][s], acc, 0, 0, 0);
+          for (int s = 0; s < KS; s++) acc = x6::mfma6(w6[gb][s], bx6[t][s], acc);
+        } else {
+#pragma unroll
+          for (int s = 0; s < KS; s++)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wreg[gb][s], bx[t][s], acc, 0, 0, 0);
+        }
         const int p = pt * 32 + l_f;
         if constexpr (PC == 2 || PC == 4) {
           if (out == nullptr) {  // uniform: pooled straight from the registers
@@ -351,7 +456,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
                 float mx = -1e20f, v[PC];
 #pragma unroll
                 for (int c = 0; c < PC; c++) {
-                  v[c] = acc[r0 + c] + bsv[r0 + c];
+                  v[c] = X6 ? acc[r0 + c] : acc[r0 + c] + bsv[r0 + c];
                   if (mx < v[c]) mx = v[c];
                 }
                 unsigned m = 0;
@@ -368,7 +473,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
         if (p < g.P) {
 #pragma unroll
           for (int r = 0; r < 16; r++)
-            T[mfma32_row(r, lane_f) * g.P + p] = acc[r] + bsv[r];
+            T[mfma32_row(r, lane_f) * g.P + p] = X6 ? acc[r] : acc[r] + bsv[r];
         }
       }
       KCNN_TMARK(2)
@@ -1320,6 +1425,19 @@ int fwd_regs_blocks_per_cu(size_t lds) {
   return lds * 3 <= 160 * 1024 ? 3 : 2;
 }
 
+// The register forward on the bf16 matrix cores (X6): unpadded maps with
+// Kdim <= 31 (the bias takes row Kdim of at most two k16 steps) and one
+// filter chunk (G <= 128).  Its ~200 VGPRs hold two workgroups per CU where
+// the fp32 kernel holds three, and the kernel is bound by its gather and
+// pool/store epilogue more than by its MFMAs: c2 fused forward + pool 137 ->
+// 132 us, but c5 C1 (G = 256 in two chunks, 3-D pool from LDS) 0.52 ->
+// 0.62 ms, so chunked layers keep the fp32 MFMA.  The rule depends on the
+// layer's shape only, so a fused and an unfused run of a layer use the same
+// arithmetic (bitwise-equal outputs).  KCNN_FWD_X6=0 keeps the fp32 MFMA.
+bool fwd_x6_ok(const ConvGeom &g, int use) {
+  return use && g.pad_h == 0 && g.pad_w == 0 && g.Kdim <= 31 && g.Gtot <= 128;
+}
+
 unsigned frame_grid(const ConvGeom &g, int blocks_per_cu) {
   int64_t b = 256LL * blocks_per_cu;
   if (b > g.R) b = g.R;
@@ -1358,17 +1476,24 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
       const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0);
       const int ksn = (g.Kdim + 1) / 2;
       static const int bpc_env = env_int("KCNN_FWD_BPC", 0);  // timing experiments
-      const unsigned grid = frame_grid(g, bpc_env > 0 ? bpc_env : fwd_regs_blocks_per_cu(lds));
-#define KCNN_FWD_REGS(KS_)                                                         \
-  hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, 0>), dim3(grid), dim3(256), lds, st, \
-                     g, X, xs, K, ks, bias, out, os, vec_ok, dbg, nullptr, 0, nullptr, 0, \
-                     PoolWin{})
+      static const int use_x6 = env_int("KCNN_FWD_X6", 1);
+      const bool x6 = fwd_x6_ok(g, use_x6);
+      const unsigned grid = frame_grid(
+          g, bpc_env > 0 ? bpc_env : x6 ? 2 : fwd_regs_blocks_per_cu(lds));
+#define KCNN_FWD_REGS_T(KS_, X6_)                                                       \
+  hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, 0, X6_>), dim3(grid), dim3(256), lds, \
+                     st, g, X, xs, K, ks, bias, out, os, vec_ok, dbg, nullptr, 0, nullptr, \
+                     0, PoolWin{})
+#define KCNN_FWD_REGS(KS_) KCNN_FWD_REGS_T(KS_, false)
       static const int dbg = env_int("KCNN_FWD_DEBUG", 0);
-      if (ksn <= 4) KCNN_FWD_REGS(4);
+      if (x6 && g.Kdim < 16) KCNN_FWD_REGS_T(1, true);
+      else if (x6) KCNN_FWD_REGS_T(2, true);
+      else if (ksn <= 4) KCNN_FWD_REGS(4);
       else if (ksn <= 8) KCNN_FWD_REGS(8);
       else if (ksn <= 12) KCNN_FWD_REGS(12);
       else KCNN_FWD_REGS(16);
 #undef KCNN_FWD_REGS
+#undef KCNN_FWD_REGS_T
       return (int)hipGetLastError();
     }
   }
@@ -1451,15 +1576,20 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
   const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0);
   const int ksn = (g.Kdim + 1) / 2;
   static const int grid_env = env_int("KCNN_FWD_GRID", 0);  // timing experiments
+  static const int use_x6 = env_int("KCNN_FWD_X6", 1);
+  const bool x6 = fwd_x6_ok(g, use_x6);
   const unsigned grid = grid_env > 0 ? (unsigned)std::min<int64_t>(grid_env, g.R)
-                                     : frame_grid(g, fwd_regs_blocks_per_cu(lds));
+                                     : frame_grid(g, x6 ? 2 : fwd_regs_blocks_per_cu(lds));
   static const int dbg = env_int("KCNN_FWD_DEBUG", 0);
-#define KCNN_FWD_POOL(KS_, PC_)                                                       \
-  hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_>), dim3(grid), dim3(256), lds, \
+#define KCNN_FWD_POOL_T(KS_, PC_, X6_)                                                      \
+  hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_, X6_>), dim3(grid), dim3(256), lds, \
                      st, g, X, xs, K, ks, bias, out, os, vec_ok, dbg, pool, ps, mask, ms, pw3)
+#define KCNN_FWD_POOL(KS_, PC_) KCNN_FWD_POOL_T(KS_, PC_, false)
 #define KCNN_FWD_POOL_KS(PC_)                     \
   do {                                            \
-    if (ksn <= 4) KCNN_FWD_POOL(4, PC_);          \
+    if (x6 && g.Kdim < 16) KCNN_FWD_POOL_T(1, PC_, true); \
+    else if (x6) KCNN_FWD_POOL_T(2, PC_, true);   \
+    else if (ksn <= 4) KCNN_FWD_POOL(4, PC_);     \
     else if (ksn <= 8) KCNN_FWD_POOL(8, PC_);     \
     else if (ksn <= 12) KCNN_FWD_POOL(12, PC_);   \
     else KCNN_FWD_POOL(16, PC_);                  \
@@ -1470,6 +1600,7 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
   else KCNN_FWD_POOL_KS(8);
 #undef KCNN_FWD_POOL_KS
 #undef KCNN_FWD_POOL
+#undef KCNN_FWD_POOL_T
   return (int)hipGetLastError();
 }
 

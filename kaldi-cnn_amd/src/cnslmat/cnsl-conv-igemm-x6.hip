@@ -1,0 +1,262 @@
+// cnslmat/cnsl-conv-igemm-x6.hip -- the implicit-GEMM convolution of the
+// long-kernel layers (BASELINE c5 C2-C4, every conv of the reference's
+// egs/exp/nnet/nnet.config, and the flipped-kernel / 1x1 data gradients) on
+// the bf16 matrix cores, with every fp32 operand split exactly into three
+// bf16 parts and the six leading cross products kept (x6-util.h).
+//
+// Reference: CuMatrixBase::Conv2D (conv2D.cc:43-201) = im2col span (:105,
+// _span_row_to_convmat) + cuBLAS GEMM (:138-139) + _convmat_to_out (:181) +
+// AddMatRepVec bias (nnet-component-nnet0.cc:443).  Here, with no span
+// matrix:  out[n][g*P + p] = sum_k W[k][g] im2col(X)[k][n*P + p] + b[g],
+// a GEMM with rows g (A = W^T) and columns m = n*P + p (B = im2col(X)).
+//
+// 512 threads, a BG x BN tile of [g x m] (BG + BN = 384: 256 x 128 for wide
+// layers, 128 x 256 for G <= 128), 8 waves of 64 x 64 (2 x 2 accumulators of
+// 32 x 32), K steps of 32.  Per step each thread loads its share of the next
+// step's operands as fp32 into registers (A: W rows, lanes along g, 256-B
+// runs; B: im2col gathered straight from X: a wave's k rows are uniform, so
+// the tap offset of each k is a scalar stepped on the SALU and an element
+// costs one vector add, plus a tap-mask test on padded maps), then splits
+// them into three bf16 planes of the
+// [row][k] LDS images (64-B rows, 16-B chunks XOR-swizzled), double
+// buffered (2 x 72 KB), one barrier per step.  Out-of-range k rows, columns
+// past M and taps outside a padded map read 0 through the buffer range.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "conv-geom.h"
+#include "x6-util.h"
+
+using namespace kcnn;
+
+namespace {
+
+constexpr int NT = 512, BK = 32, ROWB = BK * 2;
+constexpr unsigned kOob = 0x7ffffff0u;  // an offset past every buffer range used
+
+__device__ __forceinline__ int swz(int r, int c) {
+  return r * ROWB + ((c ^ ((r >> 2) & 3)) << 4);
+}
+
+// eight fp32 -> one 16-B chunk of each plane
+__device__ __forceinline__ void put8(char *img, int pl_bytes, int off, const float *v) {
+  uint32_t h[4], m[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x6::split2(v[2 * i], v[2 * i + 1], h[i], m[i], l[i]);
+  *reinterpret_cast<uint4 *>(img + off) = make_uint4(h[0], h[1], h[2], h[3]);
+  *reinterpret_cast<uint4 *>(img + pl_bytes + off) = make_uint4(m[0], m[1], m[2], m[3]);
+  *reinterpret_cast<uint4 *>(img + 2 * pl_bytes + off) = make_uint4(l[0], l[1], l[2], l[3]);
+}
+
+template <int BG, bool PADDED>
+__global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ Kw, int ks,
+    const float *__restrict__ bias, float *__restrict__ out, int os, int relu) {
+  constexpr int BN = 384 - BG;
+  constexpr int APT = BG * BK / NT, BPT = BN * BK / NT;  // values per thread per step
+  constexpr int PLA = BG * ROWB, PLB = BN * ROWB, BUF = 3 * (PLA + PLB);
+  constexpr int WN = BN / 64;                            // waves along m
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int l = lane & 31, h = lane >> 5;
+
+  // XCD-aware order: consecutive logical ids on one XCD (blocks are dealt
+  // round-robin over the 8 XCDs), g tiles fastest (they share the X columns)
+  const int tiles_g = (g.G + BG - 1) / BG;
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, q = nb >> 3, rr = nb & 7;
+  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
+  const int g0 = (lid % tiles_g) * BG;
+  const int64_t m0 = (int64_t)(lid / tiles_g) * BN;
+  const int T = (g.Kdim + BK - 1) / BK;
+
+  // A = W^T: thread row g0 + a_row, k = kt*32 + a_kc*APT + j (a_kc uniform)
+  const int a_row = tid % BG;
+  const int a_kc = __builtin_amdgcn_readfirstlane(tid / BG);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)Kw, (short)0, g.Kdim * ks * 4, 0x00020000);
+  const unsigned a_voff = (unsigned)(g0 + a_row) * 4u;
+  // B = im2col(X): thread column m0 + b_row, k = kt*32 + b_kc*BPT + e
+  const int b_row = tid % BN;
+  const int b_kc = __builtin_amdgcn_readfirstlane(tid / BN);
+  const int64_t mcol = m0 + b_row;
+  const bool mvalid = mcol < g.M;
+  // byte offset of tap (0, 0) of this column (unpadded: in [0, range); a
+  // column past M: kOob, so that kOob + any tap offset stays past the range
+  // without wrapping; padded: may wrap below 0, the tap mask guards it)
+  unsigned xoff4 = kOob;
+  unsigned nmask = 0;  // PADDED: bit tap set = tap outside the map
+  {
+    uint32_t n = 0, p = 0, px = 0, py = 0;
+    if (mvalid) {
+      g.div_P.divmod((uint32_t)mcol, n, p);
+      g.div_oh.divmod(p, px, py);
+      xoff4 = (unsigned)((int)n * xs + ((int)px - g.pad_w) * g.H + (int)py - g.pad_h) * 4u;
+    }
+    if (PADDED) {
+      nmask = 0xffffffffu;
+      if (mvalid)
+        for (int kx = 0; kx < g.kw; kx++)
+          for (int ky = 0; ky < g.kh; ky++) {
+            const int xx = (int)px + kx - g.pad_w, yy = (int)py + ky - g.pad_h;
+            if ((unsigned)xx < (unsigned)g.W && (unsigned)yy < (unsigned)g.H)
+              nmask &= ~(1u << (kx * g.kh + ky));
+          }
+    }
+  }
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)X, (short)0, (int)((int64_t)g.R * xs * 4), 0x00020000);
+
+  float av[APT], bv[BPT];
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int j = 0; j < APT; j++) {
+      // k uniform; the whole offset goes in voffset, which the range check
+      // covers (rows past Kdim and columns past the last row read 0)
+      const int k = kt * BK + a_kc * APT + j;
+      av[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          wr, a_voff + (unsigned)k * (unsigned)ks * 4u, 0, 0));
+    }
+    // the k rows of this wave: (c, kx, ky) of the first by division, then
+    // stepped (all scalar)
+    const int kb = kt * BK + b_kc * BPT;
+    uint32_t c, r, kx, ky;
+    g.div_khkw.divmod((uint32_t)(kb < g.Kdim ? kb : 0), c, r);
+    g.div_kh.divmod(r, kx, ky);
+#pragma unroll
+    for (int e = 0; e < BPT; e++) {
+      const int k = kb + e;
+      const unsigned ko =
+          k < g.Kdim ? (unsigned)((int)c * g.HW + (int)kx * g.H + (int)ky) * 4u : kOob;
+      // the whole offset in voffset (range-checked); a tap outside a padded
+      // map, a column past M or a row past Kdim lands past the range
+      unsigned off = xoff4 + ko;
+      if (PADDED) {
+        const unsigned tap = kx * (uint32_t)g.kh + ky;
+        off = k < g.Kdim ? off | (((nmask >> tap) & 1u) << 31) : kOob;
+      }
+      bv[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, off, 0, 0));
+      if (++ky == (uint32_t)g.kh) {
+        ky = 0;
+        if (++kx == (uint32_t)g.kw) { kx = 0; ++c; }
+      }
+    }
+  };
+  auto store = [&](char *buf) {
+#pragma unroll
+    for (int cc = 0; cc < APT / 8; cc++)
+      put8(buf, PLA, swz(a_row, a_kc * (APT / 8) + cc), &av[8 * cc]);
+#pragma unroll
+    for (int cc = 0; cc < BPT / 8; cc++)
+      put8(buf + 3 * PLA, PLB, swz(b_row, b_kc * (BPT / 8) + cc), &bv[8 * cc]);
+  };
+
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++) acc[i][j] = x6::zero16();
+
+  if (T > 0) {
+    load(0);
+    store(lds);
+    __syncthreads();
+    if (T > 1) load(1);
+  }
+  const int ar = wm * 64 + l, br = wn * 64 + l;
+  for (int t = 0; t < T; t++) {
+    const char *bufA = lds + (t & 1) * BUF;
+    const char *bufB = bufA + 3 * PLA;
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      x6::bf16x8 a[2][3], bb[2][3];
+      const int c = 2 * s + h;
+#pragma unroll
+      for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int pl = 0; pl < 3; pl++) {
+          a[i][pl] = *reinterpret_cast<const x6::bf16x8 *>(bufA + pl * PLA + swz(ar + 32 * i, c));
+          bb[i][pl] = *reinterpret_cast<const x6::bf16x8 *>(bufB + pl * PLB + swz(br + 32 * i, c));
+        }
+#pragma unroll
+      for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) acc[i][j] = x6::mfma6(a[i], bb[j], acc[i][j]);
+    }
+    if (t + 1 < T) {
+      store(lds + ((t + 1) & 1) * BUF);
+      if (t + 2 < T) load(t + 2);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: accumulator r of lane (l, h) is row g0 + wm*64 + 32i +
+  // mfma32_row(r), column m0 + wn*64 + 32j + l; concat layout + bias (+ReLU)
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const int64_t mm = m0 + wn * 64 + 32 * j + l;
+    if (mm >= g.M) continue;
+    uint32_t on, op;
+    g.div_P.divmod((uint32_t)mm, on, op);
+    float *orow = out + (int64_t)on * os + op;
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int gg = g0 + wm * 64 + 32 * i + mfma32_row(r, lane);
+        if (gg >= g.G) continue;
+        float v = acc[i][j][r];
+        if (bias) v = v + bias[gg];
+        if (relu) v = v < 0.0f ? 0.0f : v;  // RectifiedLinear: ApplyFloor(0)
+        orow[(int64_t)gg * g.P] = v;
+      }
+  }
+}
+
+template <int BG, bool PADDED>
+void launch(const ConvGeom &g, unsigned blocks, const float *X, int xs, const float *K, int ks,
+            const float *bias, float *out, int os, int relu, hipStream_t st) {
+  static bool attr = hipFuncSetAttribute(
+      reinterpret_cast<const void *>(&conv_igemm_x6_kernel<BG, PADDED>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 3 * 384 * ROWB) == hipSuccess;
+  (void)attr;
+  hipLaunchKernelGGL((conv_igemm_x6_kernel<BG, PADDED>), dim3(blocks), dim3(NT),
+                     2 * 3 * 384 * ROWB, st, g, X, xs, K, ks, bias, out, os, relu);
+}
+
+}  // namespace
+
+// Conv2D(concat) + bias (+ ReLU) on the bf16 MFMAs; -1 (nothing launched)
+// for shapes outside its addressing limits.  KCNN_IGEMM_X6=0 disables it
+// (the fp32-MFMA conv_igemm2_kernel then runs).
+int kcnn_conv_igemm_x6(const ConvGeom &g, const float *X, int xs, const float *K, int ks,
+                       const float *bias, float *out, int os, int relu, hipStream_t st) {
+  static const int use = [] {
+    const char *e = getenv("KCNN_IGEMM_X6");
+    return e && *e ? atoi(e) : 1;
+  }();
+  if (!use || g.M <= 0 || g.G <= 0 || g.Kdim <= 0) return -1;
+  const bool padded = g.pad_h > 0 || g.pad_w > 0;
+  if (padded && g.kh * g.kw > 31) return -1;
+  if ((int64_t)g.R * xs * 4 >= (int64_t)kOob || (int64_t)g.C * g.HW * 4 >= (int64_t)kOob)
+    return -1;
+  if ((int64_t)(g.Kdim + BK) * ks * 4 >= (int64_t)kOob || g.M >= ((int64_t)1 << 31) ||
+      (int64_t)g.G * g.P >= ((int64_t)1 << 31))
+    return -1;
+  const int BG = g.G <= 128 ? 128 : 256;
+  const int64_t tiles = (int64_t)((g.G + BG - 1) / BG) * ((g.M + (384 - BG) - 1) / (384 - BG));
+  if (tiles >= ((int64_t)1 << 31)) return -1;
+  const unsigned nb = (unsigned)tiles;
+  if (BG == 128) {
+    if (padded) launch<128, true>(g, nb, X, xs, K, ks, bias, out, os, relu, st);
+    else launch<128, false>(g, nb, X, xs, K, ks, bias, out, os, relu, st);
+  } else {
+    if (padded) launch<256, true>(g, nb, X, xs, K, ks, bias, out, os, relu, st);
+    else launch<256, false>(g, nb, X, xs, K, ks, bias, out, os, relu, st);
+  }
+  return (int)hipGetLastError();
+}

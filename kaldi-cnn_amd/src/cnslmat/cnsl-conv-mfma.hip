@@ -1097,8 +1097,12 @@ static int conv2d_impl(const float *in, MatrixDim in_dim, int in_height, int in_
     return kcnn::launch_status();
   }
 
-  // implicit GEMM v2: concat layout, X addressable with 32-bit offsets, tap
-  // masks for padded maps need kh*kw <= 32
+  // the implicit GEMM on the bf16 MFMAs (exact three-way operand splits)
+  if (concat && kcnn_conv_igemm_x6(g, in, in_dim.stride, kernel, kernel_dim.stride, bias,
+                                   out, out_dim.stride, relu, st) == 0)
+    return 0;
+  // implicit GEMM v2 (fp32 MFMA): concat layout, X addressable with 32-bit
+  // offsets, tap masks for padded maps need kh*kw <= 32
   static const int ig2 = [] {
     const char *e = getenv("KCNN_IGEMM2");
     return e && *e ? atoi(e) : 1;

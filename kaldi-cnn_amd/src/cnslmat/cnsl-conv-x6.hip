@@ -43,19 +43,22 @@
 #include <type_traits>
 
 #include "conv-geom.h"
+#include "x6-util.h"
 
 using namespace kcnn;
 
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef __attribute__((address_space(3))) void lds_void_t;
+using x6::bf16x8;
+using x6::split2;
+using x6::split8;
+using x6::mfma6;
+using x6::zero16;
 
 constexpr int NT = 512, NW = NT / 64;
 constexpr int PP = 384;             // positions per image row (768 B)
@@ -83,51 +86,6 @@ __device__ __forceinline__ int yoff(int row, int p) {
 // byte offset of (k, g) in the [32][128] bf16 W image
 __device__ __forceinline__ int woff(int k, int g) {
   return k * WROWB + ((((g >> 3) & 15) ^ swz4(k)) << 4) + ((g & 7) << 1);
-}
-
-__device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
-  f32x2 v = {lo, hi};
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
-}
-// (x0, x1) -> bf16 pairs h, m, l with x = h + m + l exactly (finite x)
-__device__ __forceinline__ void split2(float x0, float x1, uint32_t &h, uint32_t &m,
-                                       uint32_t &l) {
-  h = pack_bf16(x0, x1);
-  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xffff0000u);
-  m = pack_bf16(r0, r1);
-  l = pack_bf16(r0 - __uint_as_float(m << 16), r1 - __uint_as_float(m & 0xffff0000u));
-}
-// eight values -> the three bf16x8 fragments
-__device__ __forceinline__ void split8(const float *v, bf16x8 &h, bf16x8 &m, bf16x8 &l) {
-  uint32_t hh[4], mm[4], ll[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) split2(v[2 * i], v[2 * i + 1], hh[i], mm[i], ll[i]);
-  h = __builtin_bit_cast(bf16x8, make_uint4(hh[0], hh[1], hh[2], hh[3]));
-  m = __builtin_bit_cast(bf16x8, make_uint4(mm[0], mm[1], mm[2], mm[3]));
-  l = __builtin_bit_cast(bf16x8, make_uint4(ll[0], ll[1], ll[2], ll[3]));
-}
-
-__device__ __forceinline__ floatx16 mfma(const bf16x8 &a, const bf16x8 &b,
-                                         const floatx16 &c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-// the six products of a split pair, small to large
-__device__ __forceinline__ floatx16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3],
-                                          floatx16 c) {
-  c = mfma(a[2], b[0], c);
-  c = mfma(a[0], b[2], c);
-  c = mfma(a[1], b[1], c);
-  c = mfma(a[1], b[0], c);
-  c = mfma(a[0], b[1], c);
-  c = mfma(a[0], b[0], c);
-  return c;
-}
-
-__device__ __forceinline__ floatx16 zero16() {
-  floatx16 z;
-#pragma unroll
-  for (int i = 0; i < 16; i++) z[i] = 0.0f;
-  return z;
 }
 
 __host__ __device__ inline int round4(int n) { return (n + 3) & ~3; }
@@ -556,10 +514,6 @@ int kcnn_conv_bwd_x6(const ConvGeom &g, const float *X, int xs, const float *dY,
   // LDS-DMA of dP (16 B per lane) and of the mask (4 B per lane)
   if ((uintptr_t)dY % 16 || dys % 4) return -1;
   if (pc > 0 && ((uintptr_t)pmask % 4 || pms % 4)) return -1;
-  // wgrad k16 steps: each goes to the wave with the fewest MFMAs so far
-  // (a dgrad tile is 12, a step 6); the same table with or without dX would
-  // change the partial sums' split, so the table depends on dX only through
-  // the load, and the result is summed in a fixed order either way
   // wgrad k16 steps dealt round-robin to waves 4-7 (the same table with or
   // without dX: it fixes how the gradient splits over the waves' partials)
   X6Steps tab;

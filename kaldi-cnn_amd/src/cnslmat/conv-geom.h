@@ -13,6 +13,7 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 // G output maps of oh x ow (p = px*oh + py).
 struct ConvGeom {
   int R, H, W, C, pad_h, pad_w, kh, kw, G, oh, ow, P, Kdim, HW;
+  int Gtot;   // the layer's filter count (G is one chunk's when a launch splits G)
   int64_t M;  // R * P
   FastDiv div_P, div_oh, div_khkw, div_kh, div_H, div_HW;
 };
@@ -21,7 +22,7 @@ inline ConvGeom make_geom(int R, int H, int W, int C, int pad_h, int pad_w,
                           int kh, int kw, int G) {
   ConvGeom g;
   g.R = R; g.H = H; g.W = W; g.C = C; g.pad_h = pad_h; g.pad_w = pad_w;
-  g.kh = kh; g.kw = kw; g.G = G;
+  g.kh = kh; g.kw = kw; g.G = G; g.Gtot = G;
   g.oh = H + 2 * pad_h - kh + 1;
   g.ow = W + 2 * pad_w - kw + 1;
   g.P = g.oh * g.ow;
@@ -77,6 +78,11 @@ int kcnn_conv_bwd_x6(const kcnn::ConvGeom &g, const float *X, int xs, const floa
                      int dys, const float *K, int ks, float *dX, int dxs, float *ws_part,
                      int S, int dx_acc, hipStream_t st, const unsigned char *pmask,
                      int pms, int pc);
+// Conv2D(concat) + bias (+ ReLU when relu) as an implicit GEMM on the bf16
+// MFMAs (cnsl-conv-igemm-x6.hip); -1 when the shape is outside its limits.
+int kcnn_conv_igemm_x6(const kcnn::ConvGeom &g, const float *X, int xs, const float *K,
+                       int ks, const float *bias, float *out, int os, int relu,
+                       hipStream_t st);
 size_t kcnn_conv_wgrad_frame_ws(const kcnn::ConvGeom &g);
 int kcnn_conv_wgrad_frame(const kcnn::ConvGeom &g, const float *X, int xs,
                           const float *dY, int dys, float *gW, int gws,

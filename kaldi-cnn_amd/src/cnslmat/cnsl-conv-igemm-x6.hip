@@ -50,7 +50,7 @@ __device__ __forceinline__ void put8(char *img, int pl_bytes, int off, const flo
   *reinterpret_cast<uint4 *>(img + 2 * pl_bytes + off) = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
-template <int BG, bool PADDED>
+template <int BG, bool PADDED, bool STG>
 __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
     ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ Kw, int ks,
     const float *__restrict__ bias, float *__restrict__ out, int os, int relu) {
@@ -168,29 +168,34 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
     if (T > 1) load(1);
   }
   const int ar = wm * 64 + l, br = wn * 64 + l;
-  for (int t = 0; t < T; t++) {
-    const char *bufA = lds + (t & 1) * BUF;
+  // one k16 half of a step: 12 fragment reads, 24 MFMAs
+  auto half_step = [&](const char *bufA, int s) {
     const char *bufB = bufA + 3 * PLA;
+    x6::bf16x8 a[2][3], bb[2][3];
+    const int c = 2 * s + h;
 #pragma unroll
-    for (int s = 0; s < 2; s++) {
-      x6::bf16x8 a[2][3], bb[2][3];
-      const int c = 2 * s + h;
+    for (int i = 0; i < 2; i++)
 #pragma unroll
-      for (int i = 0; i < 2; i++)
+      for (int pl = 0; pl < 3; pl++) {
+        a[i][pl] = *reinterpret_cast<const x6::bf16x8 *>(bufA + pl * PLA + swz(ar + 32 * i, c));
+        bb[i][pl] = *reinterpret_cast<const x6::bf16x8 *>(bufB + pl * PLB + swz(br + 32 * i, c));
+      }
 #pragma unroll
-        for (int pl = 0; pl < 3; pl++) {
-          a[i][pl] = *reinterpret_cast<const x6::bf16x8 *>(bufA + pl * PLA + swz(ar + 32 * i, c));
-          bb[i][pl] = *reinterpret_cast<const x6::bf16x8 *>(bufB + pl * PLB + swz(br + 32 * i, c));
-        }
+    for (int i = 0; i < 2; i++)
 #pragma unroll
-      for (int i = 0; i < 2; i++)
-#pragma unroll
-        for (int j = 0; j < 2; j++) acc[i][j] = x6::mfma6(a[i], bb[j], acc[i][j]);
-    }
-    if (t + 1 < T) {
-      store(lds + ((t + 1) & 1) * BUF);
-      if (t + 2 < T) load(t + 2);
-    }
+      for (int j = 0; j < 2; j++) acc[i][j] = x6::mfma6(a[i], bb[j], acc[i][j]);
+  };
+  // STG: waves 4-7 split the next step's operands between their two MFMA
+  // halves, waves 0-3 after both, so the two waves of a SIMD (w, w + 4)
+  // alternate their vector and matrix phases instead of running them at once
+  const bool late = !STG || wave < 4;
+  for (int t = 0; t < T; t++) {
+    const char *buf = lds + (t & 1) * BUF;
+    half_step(buf, 0);
+    if (!late && t + 1 < T) store(lds + ((t + 1) & 1) * BUF);
+    half_step(buf, 1);
+    if (late && t + 1 < T) store(lds + ((t + 1) & 1) * BUF);
+    if (t + 2 < T) load(t + 2);
     __syncthreads();
   }
 
@@ -217,15 +222,220 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Weight gradient (ConvolutionComponent::Update's TpBlock(X) conv
+// TpInsideBlock(dY) + ModPermuteRow, nnet-component-nnet0.cc:738-765,
+// Appendix A.12) on the bf16 MFMAs:
+//   gW[g][k] = sum_t dY[n][g*P + p] im2col(X)[t][k],  gb[g] = sum_t dY[n][g*P + p]
+// over t = n*P + p of a split's frames: C[g][k] = A[g][t] B[k][t], rows g in
+// a tile of 256, columns k in a tile of 128, the reduction t flattened over
+// the split's frames in steps of 32 (no padding of P to a chunk length).
+// Thread (tp, r) = (tid % 16, tid / 16) loads the t pair 2tp, 2tp + 1 of A
+// rows r + 32j (j < 8) and B rows r + 32j (j < 4): lanes along t, so a wave
+// reads 128-B runs of dY and of the X map; each pair splits into one packed
+// bf16 pair per plane (a 4-B LDS write).  The split's frame range is the
+// range of the two buffer descriptors, so t past the split reads 0.  The
+// k-tile-0 blocks also sum dY for the bias gradient (fixed order).  Partials
+// go to ws[split][g*Kdim + k] (then the G bias entries), reduced in a fixed
+// order by kcnn_reduce_splits_wgrad: deterministic.
+template <bool PADDED, bool STG>
+__global__ __launch_bounds__(NT, 1) void conv_wgrad_x6_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ dY, int dys,
+    float *__restrict__ ws, int fps, int ktiles, int nblocks) {
+  constexpr int BG = 256, BN = 128;
+  constexpr int PLA = BG * ROWB, PLB = BN * ROWB, BUF = 3 * (PLA + PLB);
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  // XCD-aware order: logical ids contiguous per XCD, so the tiles of one
+  // split (the same frames) share an L2
+  const int nb8 = (nblocks + 7) >> 3;
+  const int bid = (int)(blockIdx.x & 7) * nb8 + (int)(blockIdx.x >> 3);
+  if (bid >= nblocks) return;  // whole workgroup: no barrier is skipped
+  const int ntiles = ktiles * ((g.G + BG - 1) / BG);
+  const int split = bid / ntiles, tile = bid - split * ntiles;
+  const int k0 = (tile % ktiles) * BN, g0 = (tile / ktiles) * BG;
+  const int nbeg = split * fps;
+  const int nf = min(g.R, nbeg + fps) - nbeg;  // frames of this split (>= 1)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int l = lane & 31, h = lane >> 5;
+  const int tp = tid & 15, r = tid >> 4;
+
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)(dY + (int64_t)nbeg * dys), (short)0, nf * dys * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)(X + (int64_t)nbeg * xs), (short)0, nf * xs * 4, 0x00020000);
+  // this thread's B rows k = k0 + r + 32j: map offset of the tap, its
+  // (kx, ky) for padded maps; rows past Kdim read 0
+  unsigned koff4[4];
+  int tkx[PADDED ? 4 : 1], tky[PADDED ? 4 : 1];
+  bool kval[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int k = k0 + r + 32 * j;
+    uint32_t c = 0, rr = 0, kx = 0, ky = 0;
+    kval[j] = k < g.Kdim;
+    if (kval[j]) {
+      g.div_khkw.divmod((uint32_t)k, c, rr);
+      g.div_kh.divmod(rr, kx, ky);
+    }
+    koff4[j] = (unsigned)((int)c * g.HW + (int)kx * g.H + (int)ky) * 4u;
+    if (PADDED) { tkx[j] = (int)kx - g.pad_w; tky[j] = (int)ky - g.pad_h; }
+  }
+  const int nsteps = (nf * g.P + BK - 1) / BK;
+
+  float av[8][2], bv[4][2], bsum[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) bsum[j] = 0.0f;
+  const bool do_bias = k0 == 0;
+  auto load = [&](int st) {
+    // t pair (t0, t0 + 1) -> (n, p) and map position (px, py) of each
+    const uint32_t t0 = (uint32_t)(st * BK + 2 * tp);
+    uint32_t n0, p0, px0, py0;
+    g.div_P.divmod(t0, n0, p0);
+    g.div_oh.divmod(p0, px0, py0);
+    uint32_t n1 = n0, p1 = p0 + 1, px1 = px0, py1 = py0 + 1;
+    if (py1 == (uint32_t)g.oh) { py1 = 0; ++px1; }
+    if (p1 == (uint32_t)g.P) { p1 = 0; px1 = 0; py1 = 0; ++n1; }
+    const uint32_t nn[2] = {n0, n1}, pp[2] = {p0, p1}, pxs[2] = {px0, px1}, pys[2] = {py0, py1};
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      // past the split: n >= nf, every offset lands past the range
+      const unsigned a4 = (nn[e] * (unsigned)dys + pp[e]) * 4u;
+#pragma unroll
+      for (int j = 0; j < 8; j++)
+        av[j][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            ar, a4 + (unsigned)((g0 + r + 32 * j) * g.P) * 4u, 0, 0));
+      const int xo = (int)(nn[e] * (unsigned)xs) + ((int)pxs[e] - g.pad_w) * g.H +
+                     (int)pys[e] - g.pad_h;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        unsigned off = (unsigned)xo * 4u + koff4[j];
+        if (PADDED) {
+          const bool in = (unsigned)((int)pxs[e] + tkx[j]) < (unsigned)g.W &&
+                          (unsigned)((int)pys[e] + tky[j]) < (unsigned)g.H;
+          off = in ? off : kOob;
+        }
+        off = kval[j] ? off : kOob;
+        bv[j][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(br, off, 0, 0));
+      }
+    }
+  };
+  auto store = [&](char *buf) {
+    // pair (t0, t0 + 1) of row q: bytes 2*(t0 % 8) of chunk t0 / 8
+    const int tc = (2 * tp) >> 3, tb = ((2 * tp) & 7) * 2;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      uint32_t hh, mm, ll;
+      x6::split2(av[j][0], av[j][1], hh, mm, ll);
+      const int o = swz(r + 32 * j, tc) + tb;
+      *reinterpret_cast<uint32_t *>(buf + o) = hh;
+      *reinterpret_cast<uint32_t *>(buf + PLA + o) = mm;
+      *reinterpret_cast<uint32_t *>(buf + 2 * PLA + o) = ll;
+      if (do_bias) bsum[j] += av[j][0] + av[j][1];
+    }
+    char *bb = buf + 3 * PLA;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      uint32_t hh, mm, ll;
+      x6::split2(bv[j][0], bv[j][1], hh, mm, ll);
+      const int o = swz(r + 32 * j, tc) + tb;
+      *reinterpret_cast<uint32_t *>(bb + o) = hh;
+      *reinterpret_cast<uint32_t *>(bb + PLB + o) = mm;
+      *reinterpret_cast<uint32_t *>(bb + 2 * PLB + o) = ll;
+    }
+  };
+
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++) acc[i][j] = x6::zero16();
+  load(0);
+  store(lds);
+  __syncthreads();
+  if (nsteps > 1) load(1);
+  const int arow = wm * 64 + l, brow = wn * 64 + l;
+  auto half_step = [&](const char *bufA, int s) {
+    const char *bufB = bufA + 3 * PLA;
+    x6::bf16x8 a[2][3], bb[2][3];
+    const int c = 2 * s + h;
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int pl = 0; pl < 3; pl++) {
+        a[i][pl] = *reinterpret_cast<const x6::bf16x8 *>(bufA + pl * PLA + swz(arow + 32 * i, c));
+        bb[i][pl] = *reinterpret_cast<const x6::bf16x8 *>(bufB + pl * PLB + swz(brow + 32 * i, c));
+      }
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) acc[i][j] = x6::mfma6(a[i], bb[j], acc[i][j]);
+  };
+  const bool late = !STG || wave < 4;  // as in conv_igemm_x6_kernel
+  for (int t = 0; t < nsteps; t++) {
+    const char *buf = lds + (t & 1) * BUF;
+    half_step(buf, 0);
+    if (!late && t + 1 < nsteps) store(lds + ((t + 1) & 1) * BUF);
+    half_step(buf, 1);
+    if (late && t + 1 < nsteps) store(lds + ((t + 1) & 1) * BUF);
+    if (t + 2 < nsteps) load(t + 2);
+    __syncthreads();
+  }
+
+  // partials of this split: gW (lanes along k: 128-B runs), then the bias
+  const int64_t E = (int64_t)g.G * g.Kdim + g.G;
+  float *wsp = ws + (int64_t)split * E;
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const int kk = k0 + wn * 64 + 32 * j + l;
+    if (kk >= g.Kdim) continue;
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        const int gg = g0 + wm * 64 + 32 * i + mfma32_row(q, lane);
+        if (gg < g.G) wsp[(int64_t)gg * g.Kdim + kk] = acc[i][j][q];
+      }
+  }
+  if (do_bias) {
+    // row r + 32j's 16 t-lane sums, added in lane order through LDS (the
+    // last barrier of the loop ended every read of the images)
+    float *red = reinterpret_cast<float *>(lds);  // [256][17]
+#pragma unroll
+    for (int j = 0; j < 8; j++) red[(r + 32 * j) * 17 + tp] = bsum[j];
+    __syncthreads();
+    if (tid < BG && g0 + tid < g.G) {
+      float sum = 0.0f;
+      for (int i = 0; i < 16; i++) sum += red[tid * 17 + i];
+      wsp[(int64_t)g.G * g.Kdim + g0 + tid] = sum;
+    }
+  }
+}
+
+int stagger() {
+  static const int v = [] {
+    const char *e = getenv("KCNN_X6_STAGGER");
+    return e && *e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+template <int BG, bool PADDED, bool STG>
+void launch_t(const ConvGeom &g, unsigned blocks, const float *X, int xs, const float *K,
+              int ks, const float *bias, float *out, int os, int relu, hipStream_t st) {
+  static bool attr = hipFuncSetAttribute(
+      reinterpret_cast<const void *>(&conv_igemm_x6_kernel<BG, PADDED, STG>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 3 * 384 * ROWB) == hipSuccess;
+  (void)attr;
+  hipLaunchKernelGGL((conv_igemm_x6_kernel<BG, PADDED, STG>), dim3(blocks), dim3(NT),
+                     2 * 3 * 384 * ROWB, st, g, X, xs, K, ks, bias, out, os, relu);
+}
 template <int BG, bool PADDED>
 void launch(const ConvGeom &g, unsigned blocks, const float *X, int xs, const float *K, int ks,
             const float *bias, float *out, int os, int relu, hipStream_t st) {
-  static bool attr = hipFuncSetAttribute(
-      reinterpret_cast<const void *>(&conv_igemm_x6_kernel<BG, PADDED>),
-      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 3 * 384 * ROWB) == hipSuccess;
-  (void)attr;
-  hipLaunchKernelGGL((conv_igemm_x6_kernel<BG, PADDED>), dim3(blocks), dim3(NT),
-                     2 * 3 * 384 * ROWB, st, g, X, xs, K, ks, bias, out, os, relu);
+  if (stagger()) launch_t<BG, PADDED, true>(g, blocks, X, xs, K, ks, bias, out, os, relu, st);
+  else launch_t<BG, PADDED, false>(g, blocks, X, xs, K, ks, bias, out, os, relu, st);
 }
 
 }  // namespace
@@ -258,5 +468,70 @@ int kcnn_conv_igemm_x6(const ConvGeom &g, const float *X, int xs, const float *K
     if (padded) launch<256, true>(g, nb, X, xs, K, ks, bias, out, os, relu, st);
     else launch<256, false>(g, nb, X, xs, K, ks, bias, out, os, relu, st);
   }
+  return (int)hipGetLastError();
+}
+
+// Weight gradient plan: S frame-range splits, each a whole number of frames,
+// sized so the S x tiles blocks fill whole rounds of 256 (one per CU) and an
+// accumulation chain stays within ~16k terms.
+bool kcnn_conv_wgrad_x6_plan(const ConvGeom &g, int xs, int dys, int &S, int &fps,
+                             size_t &ws_bytes) {
+  static const int use = [] {
+    const char *e = getenv("KCNN_WGRAD_X6");
+    return e && *e ? atoi(e) : 1;
+  }();
+  if (!use || g.R <= 0 || g.G < 32 || g.Kdim < 32) return false;
+  const bool padded = g.pad_h > 0 || g.pad_w > 0;
+  (void)padded;
+  if ((int64_t)g.C * g.HW * 4 >= (int64_t)kOob || (int64_t)g.G * g.P * 4 >= (int64_t)kOob)
+    return false;
+  const int ktiles = (g.Kdim + 127) / 128;
+  const int ntiles = ktiles * ((g.G + 255) / 256);
+  const int64_t chain = (int64_t)g.R * g.P;
+  int s0 = (int)((chain + 16383) / 16384);
+  if (s0 < 1) s0 = 1;
+  if ((int64_t)s0 * ntiles < 256) s0 = (256 + ntiles - 1) / ntiles;
+  if (s0 > g.R) s0 = g.R;
+  int best_s = -1, best_fps = 0;
+  double best_cost = 0;
+  for (int s = s0; s <= 2 * s0 && s <= g.R; s++) {
+    const int f = (g.R + s - 1) / s;
+    const int sa = (g.R + f - 1) / f;
+    const int64_t rounds = ((int64_t)sa * ntiles + 255) / 256;
+    const double cost = (double)rounds * f;
+    if (best_s < 0 || cost < best_cost) { best_s = sa; best_fps = f; best_cost = cost; }
+  }
+  if ((int64_t)best_fps * dys * 4 >= (int64_t)kOob || (int64_t)best_fps * xs * 4 >= (int64_t)kOob)
+    return false;
+  S = best_s;
+  fps = best_fps;
+  const size_t E = (size_t)g.G * g.Kdim + g.G;
+  ws_bytes = (size_t)S * E * sizeof(float) + kcnn_reduce_splits_ws(S, (int)E);
+  return true;
+}
+
+// Partials [S][G*Kdim + G] into ws (kcnn_conv_wgrad_x6_plan's S and fps).
+int kcnn_conv_wgrad_x6(const ConvGeom &g, const float *X, int xs, const float *dY, int dys,
+                       float *ws, int S, int fps, hipStream_t st) {
+  const bool padded = g.pad_h > 0 || g.pad_w > 0;
+  const int ktiles = (g.Kdim + 127) / 128;
+  const int nblocks = S * ktiles * ((g.G + 255) / 256);
+  const dim3 grid((unsigned)(8 * ((nblocks + 7) / 8)));
+  constexpr int lds = 2 * 3 * 384 * ROWB;
+#define KCNN_WX6(P_, S_)                                                                  \
+  do {                                                                                    \
+    static bool attr = hipFuncSetAttribute(                                               \
+        reinterpret_cast<const void *>(&conv_wgrad_x6_kernel<P_, S_>),                    \
+        hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;                    \
+    (void)attr;                                                                           \
+    hipLaunchKernelGGL((conv_wgrad_x6_kernel<P_, S_>), grid, dim3(NT), lds, st, g, X, xs, \
+                       dY, dys, ws, fps, ktiles, nblocks);                                \
+  } while (0)
+  if (padded) {
+    if (stagger()) KCNN_WX6(true, true); else KCNN_WX6(true, false);
+  } else {
+    if (stagger()) KCNN_WX6(false, true); else KCNN_WX6(false, false);
+  }
+#undef KCNN_WX6
   return (int)hipGetLastError();
 }

@@ -1232,6 +1232,11 @@ size_t hipF_conv2d_wgrad_workspace_bytes(MatrixDim in_dim, int in_height,
   if (plan_wgrad2(g, in_dim.stride > 0 ? in_dim.stride : g.HW * in_channel,
                   g.P * group, p2) && p2.ws_bytes > a)
     a = p2.ws_bytes;
+  int xS, xfps;
+  size_t xb;
+  if (kcnn_conv_wgrad_x6_plan(g, in_dim.stride > 0 ? in_dim.stride : g.HW * in_channel,
+                              g.P * group, xS, xfps, xb) && xb > a)
+    a = xb;
   return c > a ? c : a;
 }
 
@@ -1261,6 +1266,22 @@ int hipF_conv2d_wgrad(const float *in, MatrixDim in_dim, int in_height,
                                        grad_W_dim.stride, grad_b, workspace,
                                        workspace_bytes, st) == 0)
     return 0;
+  {
+    // the long-kernel weight gradient on the bf16 MFMAs
+    int xS, xfps;
+    size_t xb;
+    if (g.M > 0 &&
+        kcnn_conv_wgrad_x6_plan(g, in_dim.stride, out_deriv_dim.stride, xS, xfps, xb) &&
+        workspace != nullptr && workspace_bytes >= xb) {
+      const int E = g.G * g.Kdim + g.G;
+      float *part = static_cast<float *>(workspace);
+      int rc = kcnn_conv_wgrad_x6(g, in, in_dim.stride, out_deriv, out_deriv_dim.stride,
+                                  part, xS, xfps, st);
+      if (rc) return rc;
+      return kcnn_reduce_splits_wgrad(part, xS, E, part + (size_t)xS * E, g.G * g.Kdim,
+                                      g.Kdim, grad_W, grad_W_dim.stride, grad_b, st);
+    }
+  }
   Wgrad2Plan p2;
   if (g.M > 0 && plan_wgrad2(g, in_dim.stride, out_deriv_dim.stride, p2) &&
       workspace != nullptr && workspace_bytes >= p2.ws_bytes) {

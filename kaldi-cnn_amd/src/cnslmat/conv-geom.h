@@ -83,6 +83,13 @@ int kcnn_conv_bwd_x6(const kcnn::ConvGeom &g, const float *X, int xs, const floa
 int kcnn_conv_igemm_x6(const kcnn::ConvGeom &g, const float *X, int xs, const float *K,
                        int ks, const float *bias, float *out, int os, int relu,
                        hipStream_t st);
+// Weight gradient on the bf16 MFMAs (cnsl-conv-igemm-x6.hip): the split
+// plan (false = not eligible), then partials [S][G*Kdim + G] into ws for
+// kcnn_reduce_splits_wgrad.
+bool kcnn_conv_wgrad_x6_plan(const kcnn::ConvGeom &g, int xs, int dys, int &S, int &fps,
+                             size_t &ws_bytes);
+int kcnn_conv_wgrad_x6(const kcnn::ConvGeom &g, const float *X, int xs, const float *dY,
+                       int dys, float *ws, int S, int fps, hipStream_t st);
 size_t kcnn_conv_wgrad_frame_ws(const kcnn::ConvGeom &g);
 int kcnn_conv_wgrad_frame(const kcnn::ConvGeom &g, const float *X, int xs,
                           const float *dY, int dys, float *gW, int gws,

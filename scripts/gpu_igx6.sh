@@ -1,5 +1,5 @@
-# x6 implicit GEMM (long-kernel convs): GPU tests, then c5 / nnet benches
-# with KCNN_IGEMM_X6=1 and 0, and a kernel profile of c5
+# x6 long-kernel convs: GPU tests, then c5 / nnet benches
+# with the x6 weight gradient on and off (KCNN_WGRAD_X6), and a c5 profile
 set -o pipefail
 O=${1:-gpurun_out/igx6}
 mkdir -p $O
@@ -9,7 +9,7 @@ tail -3 $O/pytest.log
 [ $rc -ne 0 ] && { grep -E "Error|assert|FAILED" $O/pytest.log | head -30; exit 3; }
 for v in 1 0; do
   for c in c5 nnet; do
-    KCNN_IGEMM_X6=$v timeout -k 10 300 python bench.py --no-cpu-baseline --config $c --json-out $O/b_${c}_$v.json > $O/b_${c}_$v.log 2>&1 || exit 5
+    KCNN_WGRAD_X6=$v timeout -k 10 300 python bench.py --no-cpu-baseline --config $c --json-out $O/b_${c}_$v.json > $O/b_${c}_$v.log 2>&1 || exit 5
     python -c "
 import json;d=json.load(open('$O/b_${c}_$v.json'))
 print('$c x6=$v', d['value'], d['ms_per_step'], d.get('conv'))"

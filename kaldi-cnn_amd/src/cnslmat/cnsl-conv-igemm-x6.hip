@@ -50,7 +50,7 @@ __device__ __forceinline__ void put8(char *img, int pl_bytes, int off, const flo
   *reinterpret_cast<uint4 *>(img + 2 * pl_bytes + off) = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
-template <int BG, bool PADDED, bool STG>
+template <int BG, bool PADDED, bool STG, bool TAB>
 __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
     ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ Kw, int ks,
     const float *__restrict__ bias, float *__restrict__ out, int os, int relu) {
@@ -111,6 +111,23 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       (void *)X, (short)0, (int)((int64_t)g.R * xs * 4), 0x00020000);
 
+  // TAB: per k row the byte offset of its tap in a map (kOob past Kdim: out
+  // of range; tap index 31 for padded maps, which no lane's mask admits)
+  const int KT = T * BK;
+  unsigned *ktab = reinterpret_cast<unsigned *>(lds + 2 * BUF);
+  unsigned char *ttab = reinterpret_cast<unsigned char *>(ktab + (TAB ? KT : 0));
+  if constexpr (TAB) {
+    for (int k = tid; k < KT; k += NT) {
+      uint32_t c = 0, r = 0, kx = 0, ky = 0;
+      if (k < g.Kdim) {
+        g.div_khkw.divmod((uint32_t)k, c, r);
+        g.div_kh.divmod(r, kx, ky);
+      }
+      ktab[k] = k < g.Kdim ? (unsigned)((int)c * g.HW + (int)kx * g.H + (int)ky) * 4u : kOob;
+      if (PADDED) ttab[k] = (unsigned char)(k < g.Kdim ? kx * g.kh + ky : 31);
+    }
+    __syncthreads();
+  }
   float av[APT], bv[BPT];
   auto load = [&](int kt) {
 #pragma unroll
@@ -121,9 +138,37 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
       av[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
           wr, a_voff + (unsigned)k * (unsigned)ks * 4u, 0, 0));
     }
+    const int kb = kt * BK + b_kc * BPT;
+    if constexpr (TAB) {
+      // the wave's k rows from the LDS table (uniform address: broadcast)
+      const int kq = min(kb, KT - BPT);  // a step past T re-reads the last
+      unsigned ko[BPT];
+#pragma unroll
+      for (int q4 = 0; q4 < BPT / 4; q4++) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(ktab + kq + 4 * q4);
+        ko[4 * q4] = v.x; ko[4 * q4 + 1] = v.y; ko[4 * q4 + 2] = v.z; ko[4 * q4 + 3] = v.w;
+      }
+      uint32_t tt[PADDED ? BPT / 4 : 1];
+      if (PADDED) {
+#pragma unroll
+        for (int q4 = 0; q4 < BPT / 8; q4++) {
+          const uint2 v = *reinterpret_cast<const uint2 *>(ttab + kq + 8 * q4);
+          tt[2 * q4] = v.x; tt[2 * q4 + 1] = v.y;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < BPT; e++) {
+        unsigned off = xoff4 + ko[e];
+        if (PADDED) {
+          const unsigned tap = (tt[e >> 2] >> (8 * (e & 3))) & 31u;
+          off |= ((nmask >> tap) & 1u) << 31;  // tap 31 (k past Kdim): never inside
+        }
+        bv[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, off, 0, 0));
+      }
+      return;
+    }
     // the k rows of this wave: (c, kx, ky) of the first by division, then
     // stepped (all scalar)
-    const int kb = kt * BK + b_kc * BPT;
     uint32_t c, r, kx, ky;
     g.div_khkw.divmod((uint32_t)(kb < g.Kdim ? kb : 0), c, r);
     g.div_kh.divmod(r, kx, ky);
@@ -421,21 +466,43 @@ int stagger() {
   return v;
 }
 
-template <int BG, bool PADDED, bool STG>
-void launch_t(const ConvGeom &g, unsigned blocks, const float *X, int xs, const float *K,
-              int ks, const float *bias, float *out, int os, int relu, hipStream_t st) {
+constexpr int kLdsMax = 160 * 1024;
+constexpr int kImgBytes = 2 * 3 * 384 * ROWB;  // the double-buffered plane images
+
+// LDS of the tap table for Kdim (0: it does not fit beside the images)
+int tab_bytes(const ConvGeom &g, bool padded) {
+  static const int use = [] {
+    const char *e = getenv("KCNN_IGX6_TAB");
+    return e && *e ? atoi(e) : 1;
+  }();
+  const int KT = (g.Kdim + BK - 1) / BK * BK;
+  const int b = KT * 4 + (padded ? KT : 0);
+  return use && kImgBytes + b <= kLdsMax ? b : 0;
+}
+
+template <int BG, bool PADDED, bool STG, bool TAB>
+void launch_t(const ConvGeom &g, unsigned blocks, int lds, const float *X, int xs,
+              const float *K, int ks, const float *bias, float *out, int os, int relu,
+              hipStream_t st) {
   static bool attr = hipFuncSetAttribute(
-      reinterpret_cast<const void *>(&conv_igemm_x6_kernel<BG, PADDED, STG>),
-      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 3 * 384 * ROWB) == hipSuccess;
+      reinterpret_cast<const void *>(&conv_igemm_x6_kernel<BG, PADDED, STG, TAB>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax) == hipSuccess;
   (void)attr;
-  hipLaunchKernelGGL((conv_igemm_x6_kernel<BG, PADDED, STG>), dim3(blocks), dim3(NT),
-                     2 * 3 * 384 * ROWB, st, g, X, xs, K, ks, bias, out, os, relu);
+  hipLaunchKernelGGL((conv_igemm_x6_kernel<BG, PADDED, STG, TAB>), dim3(blocks), dim3(NT),
+                     lds, st, g, X, xs, K, ks, bias, out, os, relu);
 }
 template <int BG, bool PADDED>
 void launch(const ConvGeom &g, unsigned blocks, const float *X, int xs, const float *K, int ks,
             const float *bias, float *out, int os, int relu, hipStream_t st) {
-  if (stagger()) launch_t<BG, PADDED, true>(g, blocks, X, xs, K, ks, bias, out, os, relu, st);
-  else launch_t<BG, PADDED, false>(g, blocks, X, xs, K, ks, bias, out, os, relu, st);
+  const int tb = tab_bytes(g, PADDED);
+  const int lds = kImgBytes + tb;
+  if (tb) {
+    if (stagger()) launch_t<BG, PADDED, true, true>(g, blocks, lds, X, xs, K, ks, bias, out, os, relu, st);
+    else launch_t<BG, PADDED, false, true>(g, blocks, lds, X, xs, K, ks, bias, out, os, relu, st);
+  } else {
+    if (stagger()) launch_t<BG, PADDED, true, false>(g, blocks, lds, X, xs, K, ks, bias, out, os, relu, st);
+    else launch_t<BG, PADDED, false, false>(g, blocks, lds, X, xs, K, ks, bias, out, os, relu, st);
+  }
 }
 
 }  // namespace

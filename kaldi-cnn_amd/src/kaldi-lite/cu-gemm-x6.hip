@@ -70,21 +70,46 @@ __device__ __forceinline__ int swz(int r, int c) {
   return r * ROWB + ((c ^ ((r >> 2) & 3)) << 4);
 }
 
+__device__ __forceinline__ uint32_t pack_hi(float lo, float hi) {
+  // two rounded bf16 halves of one u32 (v_cvt_pk_bf16_f32)
+  f32x2 v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+__device__ __forceinline__ f32x2 unpack2(uint32_t u) {
+  f32x2 r;
+  r[0] = __uint_as_float(u << 16);
+  r[1] = __uint_as_float(u & 0xffff0000u);
+  return r;
+}
+// (x0, x1) -> the h, m, l bf16 pairs (x = h + m + l exactly, finite x)
+__device__ __forceinline__ void split2(float x0, float x1, uint32_t &h, uint32_t &m,
+                                       uint32_t &l) {
+#ifdef KCNN_X6_TRUNC
+  // truncating split: h, m, l are the three bytes of the significand
+  const uint32_t b0 = __float_as_uint(x0), b1 = __float_as_uint(x1);
+  const float h0 = __uint_as_float(b0 & 0xffff0000u), h1 = __uint_as_float(b1 & 0xffff0000u);
+  const float r0 = x0 - h0, r1 = x1 - h1;
+  const uint32_t c0 = __float_as_uint(r0), c1 = __float_as_uint(r1);
+  const float m0 = __uint_as_float(c0 & 0xffff0000u), m1 = __uint_as_float(c1 & 0xffff0000u);
+  const float l0 = r0 - m0, l1 = r1 - m1;
+  h = __builtin_amdgcn_perm(b1, b0, 0x07060302u);
+  m = __builtin_amdgcn_perm(c1, c0, 0x07060302u);
+  l = __builtin_amdgcn_perm(__float_as_uint(l1), __float_as_uint(l0), 0x07060302u);
+#else
+  h = pack_hi(x0, x1);
+  const f32x2 hf = unpack2(h);
+  const float r0 = x0 - hf[0], r1 = x1 - hf[1];
+  m = pack_hi(r0, r1);
+  const f32x2 mf = unpack2(m);
+  l = pack_hi(r0 - mf[0], r1 - mf[1]);
+#endif
+}
+
 // 8 fp32 -> three bf16x8 planes, x = h + m + l exactly for finite x
 __device__ __forceinline__ void split8(const float *x, uint4 &h, uint4 &m, uint4 &l) {
   uint32_t hv[4], mv[4], lv[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    f32x2 v = {x[2 * i], x[2 * i + 1]};
-    bf16x2 a = __builtin_convertvector(v, bf16x2);
-    f32x2 r = v - __builtin_convertvector(a, f32x2);
-    bf16x2 b = __builtin_convertvector(r, bf16x2);
-    f32x2 r2 = r - __builtin_convertvector(b, f32x2);
-    bf16x2 c = __builtin_convertvector(r2, bf16x2);
-    hv[i] = __builtin_bit_cast(uint32_t, a);
-    mv[i] = __builtin_bit_cast(uint32_t, b);
-    lv[i] = __builtin_bit_cast(uint32_t, c);
-  }
+  for (int i = 0; i < 4; ++i) split2(x[2 * i], x[2 * i + 1], hv[i], mv[i], lv[i]);
   h = make_uint4(hv[0], hv[1], hv[2], hv[3]);
   m = make_uint4(mv[0], mv[1], mv[2], mv[3]);
   l = make_uint4(lv[0], lv[1], lv[2], lv[3]);
@@ -337,41 +362,6 @@ __global__ void gemm_x6_reduce_scalar_kernel(const float *__restrict__ part, int
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
-__device__ __forceinline__ uint32_t pack_hi(float lo, float hi) {
-  // two rounded bf16 halves of one u32 (v_cvt_pk_bf16_f32)
-  f32x2 v = {lo, hi};
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
-}
-__device__ __forceinline__ f32x2 unpack2(uint32_t u) {
-  f32x2 r;
-  r[0] = __uint_as_float(u << 16);
-  r[1] = __uint_as_float(u & 0xffff0000u);
-  return r;
-}
-// (x0, x1) -> the h, m, l bf16 pairs (x = h + m + l exactly, finite x)
-__device__ __forceinline__ void split2(float x0, float x1, uint32_t &h, uint32_t &m,
-                                       uint32_t &l) {
-#ifdef KCNN_X6_TRUNC
-  // truncating split: h, m, l are the three bytes of the significand
-  const uint32_t b0 = __float_as_uint(x0), b1 = __float_as_uint(x1);
-  const float h0 = __uint_as_float(b0 & 0xffff0000u), h1 = __uint_as_float(b1 & 0xffff0000u);
-  const float r0 = x0 - h0, r1 = x1 - h1;
-  const uint32_t c0 = __float_as_uint(r0), c1 = __float_as_uint(r1);
-  const float m0 = __uint_as_float(c0 & 0xffff0000u), m1 = __uint_as_float(c1 & 0xffff0000u);
-  const float l0 = r0 - m0, l1 = r1 - m1;
-  h = __builtin_amdgcn_perm(b1, b0, 0x07060302u);
-  m = __builtin_amdgcn_perm(c1, c0, 0x07060302u);
-  l = __builtin_amdgcn_perm(__float_as_uint(l1), __float_as_uint(l0), 0x07060302u);
-#else
-  h = pack_hi(x0, x1);
-  const f32x2 hf = unpack2(h);
-  const float r0 = x0 - hf[0], r1 = x1 - hf[1];
-  m = pack_hi(r0, r1);
-  const f32x2 mf = unpack2(m);
-  l = pack_hi(r0 - mf[0], r1 - mf[1]);
-#endif
-}
 
 // offset of (k, col) in a [k][R] transposed image, 16-B chunks swizzled
 template <int R>

@@ -458,10 +458,14 @@ __global__ __launch_bounds__(NT, 1) void conv_wgrad_x6_kernel(
   }
 }
 
+// KCNN_CONV_X6_STAGGER=1: the wave-pair stagger (STG).  It gained 4 % on
+// c5 while the split subtractions were packed into v_pk_add_f32; built
+// without SLP vectorization (Makefile) the kernels measure the same or
+// 0.6 % slower with it, so it is off by default.
 int stagger() {
   static const int v = [] {
-    const char *e = getenv("KCNN_X6_STAGGER");
-    return e && *e ? atoi(e) : 1;
+    const char *e = getenv("KCNN_CONV_X6_STAGGER");
+    return e && *e ? atoi(e) : 0;
   }();
   return v;
 }

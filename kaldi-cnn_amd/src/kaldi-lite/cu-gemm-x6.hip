@@ -198,11 +198,11 @@ __device__ __forceinline__ f32x16 mfma(const bf16x8 &a, const bf16x8 &b, const f
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-template <bool A_KC, bool B_KC>
+template <bool A_KC, bool B_KC, bool STG>
 __global__ __launch_bounds__(NT, 1) void gemm_x6_kernel(GemmX6Args p) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
 
   // XCD-aware order: consecutive logical ids run on one XCD (blocks are
@@ -242,42 +242,50 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6_kernel(GemmX6Args p) {
 
   const int ar = wm * 64 + (lane & 31), br = wn * 64 + (lane & 31);
   const int half = lane >> 5;
-  for (int t = 0; t < T; ++t) {
-    const char *bufA = lds + (t & 1) * BUF;
+  // one k16 half of a step: 12 fragment reads, 24 MFMAs
+  auto half_step = [&](const char *bufA, int s) {
     const char *bufB = bufA + 3 * A_PLANE;
+    bf16x8 a[2][3], bb[2][3];
+    const int c = 2 * s + half;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 a[2][3], bb[2][3];
-      const int c = 2 * s + half;
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-          a[i][pl] = *reinterpret_cast<const bf16x8 *>(bufA + pl * A_PLANE + swz(ar + 32 * i, c));
-          bb[i][pl] = *reinterpret_cast<const bf16x8 *>(bufB + pl * B_PLANE + swz(br + 32 * i, c));
-        }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          f32x16 x = acc[i][j];
-          x = mfma(a[i][2], bb[j][0], x);  // lh
-          x = mfma(a[i][0], bb[j][2], x);  // hl
-          x = mfma(a[i][1], bb[j][1], x);  // mm
-          x = mfma(a[i][1], bb[j][0], x);  // mh
-          x = mfma(a[i][0], bb[j][1], x);  // hm
-          x = mfma(a[i][0], bb[j][0], x);  // hh
-          acc[i][j] = x;
-        }
-    }
-    if (t + 1 < T) {
-      char *nA = lds + ((t + 1) & 1) * BUF;
-      la.template store<A_PLANE>(nA, tid);
-      lb.template store<B_PLANE>(nA + 3 * A_PLANE, tid);
-      if (t + 2 < T) {
-        la.load(p.A, p.lda, row0, p.M, kbeg + (t + 2) * BK, kend, tid);
-        lb.load(p.B, p.ldb, col0, p.N, kbeg + (t + 2) * BK, kend, tid);
+      for (int pl = 0; pl < 3; ++pl) {
+        a[i][pl] = *reinterpret_cast<const bf16x8 *>(bufA + pl * A_PLANE + swz(ar + 32 * i, c));
+        bb[i][pl] = *reinterpret_cast<const bf16x8 *>(bufB + pl * B_PLANE + swz(br + 32 * i, c));
       }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x16 x = acc[i][j];
+        x = mfma(a[i][2], bb[j][0], x);  // lh
+        x = mfma(a[i][0], bb[j][2], x);  // hl
+        x = mfma(a[i][1], bb[j][1], x);  // mm
+        x = mfma(a[i][1], bb[j][0], x);  // mh
+        x = mfma(a[i][0], bb[j][1], x);  // hm
+        x = mfma(a[i][0], bb[j][0], x);  // hh
+        acc[i][j] = x;
+      }
+  };
+  auto split_next = [&](int t) {
+    char *nA = lds + ((t + 1) & 1) * BUF;
+    la.template store<A_PLANE>(nA, tid);
+    lb.template store<B_PLANE>(nA + 3 * A_PLANE, tid);
+  };
+  // STG: waves 4-7 split the next step's operands between their two MFMA
+  // halves, waves 0-3 after both, so the two waves of a SIMD (w, w + 4)
+  // alternate their vector and matrix phases
+  const bool late = !STG || wave < 4;
+  for (int t = 0; t < T; ++t) {
+    const char *buf = lds + (t & 1) * BUF;
+    half_step(buf, 0);
+    if (!late && t + 1 < T) split_next(t);
+    half_step(buf, 1);
+    if (late && t + 1 < T) split_next(t);
+    if (t + 2 < T) {
+      la.load(p.A, p.lda, row0, p.M, kbeg + (t + 2) * BK, kend, tid);
+      lb.load(p.B, p.ldb, col0, p.N, kbeg + (t + 2) * BK, kend, tid);
     }
     __syncthreads();
   }
@@ -951,16 +959,26 @@ __global__ void split_planes_kernel(const float *__restrict__ src, int rows, int
   }
 }
 
-template <bool A_KC, bool B_KC>
-void launch_x6(const GemmX6Args &a, unsigned blocks, hipStream_t st) {
+template <bool A_KC, bool B_KC, bool STG>
+void launch_x6_t(const GemmX6Args &a, unsigned blocks, hipStream_t st) {
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_x6_kernel<A_KC, B_KC>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                               LDS_BYTES) == hipSuccess;
+    return hipFuncSetAttribute(
+               reinterpret_cast<const void *>(&gemm_x6_kernel<A_KC, B_KC, STG>),
+               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_x6_kernel<A_KC, B_KC>), dim3(blocks), dim3(NT), LDS_BYTES,
+  hipLaunchKernelGGL((gemm_x6_kernel<A_KC, B_KC, STG>), dim3(blocks), dim3(NT), LDS_BYTES,
                      st, a);
+}
+// KCNN_X6_STAGGER=0: no wave-pair stagger (c2 FC GEMMs 1.655 -> 1.636 ms with it)
+template <bool A_KC, bool B_KC>
+void launch_x6(const GemmX6Args &a, unsigned blocks, hipStream_t st) {
+  static const int stg = [] {
+    const char *e = getenv("KCNN_X6_STAGGER");
+    return e && *e ? atoi(e) : 1;
+  }();
+  if (stg) launch_x6_t<A_KC, B_KC, true>(a, blocks, st);
+  else launch_x6_t<A_KC, B_KC, false>(a, blocks, st);
 }
 
 // K splits for a tile count: the fraction of the last wave of workgroups

@@ -12,6 +12,7 @@ for v in ${VALS:-1 0 1 0}; do
     env $VAR=$v timeout -k 10 300 python bench.py --no-cpu-baseline --config $c --json-out $O/b.json > $O/b.log 2>&1 || exit 5
     python -c "
 import json;d=json.load(open('$O/b.json'));s=d.get('scopes_ms_per_step') or {}
-print('$c $VAR=$v', d['value'], d['ms_per_step'], {k.split('::')[1]:v for k,v in s.items() if k.startswith('Conv')})"
+k=d.get('kernels') or {}
+print('$c $VAR=$v', d['value'], d['ms_per_step'], {n:v.get('ms', v.get('ms_per_step')) for n,v in k.items()} if k else {k.split('::')[1]:v for k,v in s.items() if k.startswith('Conv')})" | tee -a $O/summary.txt
   done
 done

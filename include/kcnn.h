@@ -236,7 +236,10 @@ int kcnn_nnet_input_deriv(const kcnn_nnet *n, int i, const float **data,
  * previous call (or `out_deriv` for the last component).  mode 0: reference
  * (update in place); 1: write the gradient into grad (device, length
  * kcnn_component_num_gradient_params) without updating; 2: data gradient
- * only.  The data gradient of component 0 is skipped when skip_first_dx. */
+ * only; 3: the gradient only, for an updatable component that is not half
+ * of a fused Conv -> Maxpool pair (a mode 2 call then adds its data
+ * gradient; data parallelism starts the gradient's all-reduce in between).
+ * The data gradient of component 0 is skipped when skip_first_dx. */
 int kcnn_nnet_backprop_component(kcnn_nnet *n, int i, const float *out_deriv,
                                  MatrixDim od_dim, int mode, float *grad,
                                  int skip_first_dx);

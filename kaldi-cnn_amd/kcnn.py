@@ -375,6 +375,12 @@ class Component:
         check(fn(self._h, buf, len(buf)))
         return buf.value.decode()
 
+    def SplitGradient(self) -> bool:
+        """Whether kcnn_dp may compute this layer's gradient apart from its
+        data gradient (mode 3 then mode 2): not for a convolution, whose
+        fused backward makes both from one pass over its output derivative."""
+        return self.Type() != "ConvolutionComponent"
+
     def Type(self) -> str:
         return self._str(lib().kcnn_component_type)
 

@@ -772,6 +772,17 @@ int kcnn_nnet_backprop_component(kcnn_nnet *n, int i, const float *out_deriv,
     auto *u = dynamic_cast<UpdatableComponent *>(c);
     CuMatrix<BaseFloat> *dx = &n->deriv[i];
     if (i == 0 && skip_first_dx && u) dx = nullptr;
+    if (mode == 3) {  // the parameter gradient alone (a later mode 2 call adds dX)
+      KALDI_ASSERT(u != NULL && grad != NULL &&
+                   !(i + 1 < nc && n->deriv_deferred[i + 1]) && !n->mask_valid[i]);
+      CuSubMatrix<BaseFloat> od = (i == nc - 1)
+          ? view(out_deriv, od_dim)
+          : CuSubMatrix<BaseFloat>(n->deriv[i + 1].Data(), n->deriv[i + 1].NumRows(),
+                                   n->deriv[i + 1].NumCols(), n->deriv[i + 1].Stride());
+      u->BackpropGradient(nnet_in_info(n, i), nnet_out_info(n, i), n->fwd[i], n->fwd[i + 1],
+                          od, nullptr, grad);
+      return;
+    }
     if (i + 1 < nc && n->deriv_deferred[i + 1]) {  // pool above left its Backprop here
       auto *conv = dynamic_cast<cnsl::nnet0::ConvolutionComponent *>(c);
       auto *pool = dynamic_cast<cnsl::nnet0::MaxpoolComponent *>(n->comps[i + 1]);

@@ -71,8 +71,9 @@ class OracleNet:
             if isinstance(oc, O.Pool):
                 self.deriv[i] = oc.backprop(self.fwd[i], self.fwd[i + 1], od)
                 return
-            self.deriv[i] = oc.backprop(self.fwd[i], od, update=False)
-            if mode == 1:
+            if mode != 3:  # mode 3: the gradient only
+                self.deriv[i] = oc.backprop(self.fwd[i], od, update=False)
+            if mode in (1, 3):
                 gW, gb = oc.gradient(self.fwd[i], od)
                 grad.copy_(torch.from_numpy(np.concatenate([gW.ravel(), gb])))
 
@@ -90,7 +91,8 @@ def _params(net):
             if not isinstance(c.oc, O.Pool)]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, split):
+    kcnn_dp.SPLIT_GRADIENT_PARAMS = split
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     net = OracleNet(seed=5)                              # identical replicas
@@ -122,7 +124,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_dp_two_ranks_equal_one_process():
+@pytest.mark.parametrize("split", [1 << 20, 1])
+def test_dp_two_ranks_equal_one_process(split):
+    """split = 1: every gradient on its own (mode 3) with its all-reduce
+    started before the layer's data gradient (mode 2)."""
+    kcnn_dp.SPLIT_GRADIENT_PARAMS = split
     ref = OracleNet(seed=5)
     grads = kcnn_dp.gradient_buffers(ref, lambda n: torch.empty(n))
     for x, dy in zip(*_data()):
@@ -133,13 +139,14 @@ def test_dp_two_ranks_equal_one_process():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, split)) for r in range(2)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=240) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    kcnn_dp.SPLIT_GRADIENT_PARAMS = 1 << 20
     for r in range(2):
         for a, b in zip(got[r], want):
             # same math up to the fp32 rounding of a 2-way split of each sum

@@ -38,6 +38,12 @@ CONVS = {
     "ig2_tail_g128": (5, 6, 11, 3, 3, 128, 1, 0),       # Kdim 99, pad on one axis
     # scatter-form data gradient (HW >= 1.25 P) on a padded map
     "scatter_pad": (12, 10, 4, 5, 5, 32, 1, 1),          # HW 120, P 80, Kdim 100
+    # bf16x6 implicit GEMM / weight gradient edges: partial filter tiles of
+    # both tile shapes, Kdim off the 32-step, 5x5 taps on a padded map, P = 2
+    "x6_g320_pad": (6, 7, 8, 3, 3, 320, 1, 1),          # 256 + 64 filters, Kdim 72
+    "x6_g96_k75": (9, 10, 5, 3, 5, 96, 0, 0),           # 128-row tile, 96 used
+    "x6_5x5_pad2": (7, 7, 4, 5, 5, 64, 2, 2),           # 25 taps, pad 2
+    "x6_p2": (1, 4, 40, 1, 3, 64, 0, 0),                # P = 2, Kdim 120
 }
 
 

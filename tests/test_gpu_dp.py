@@ -23,14 +23,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("stack,n_params", [("c2", 6), ("long", 9)])
-def test_dp_two_ranks_match_single_process(tmp_path, stack, n_params):
+@pytest.mark.parametrize("stack,n_params,split", [("c2", 6, None), ("long", 9, None),
+                                                  ("c2", 6, "1")])
+def test_dp_two_ranks_match_single_process(tmp_path, stack, n_params, split):
+    """split "1": every non-conv gradient computed on its own (mode 3) and
+    all-reduced while the layer's data gradient (mode 2) runs."""
     steps, n_global = 2, 48
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(HERE, "dp_gpu_worker.py"), str(tmp_path), str(steps), str(n_global),
            stack]
     env = dict(os.environ, OMP_NUM_THREADS="2")
+    if split:
+        env["KCNN_DP_SPLIT_PARAMS"] = split
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     a, b = np.load(tmp_path / "rank0.npz"), np.load(tmp_path / "rank1.npz")

@@ -380,6 +380,11 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
         // the pooling of item i - 1, so that VALU work runs under the chain
         constexpr int NI = 4 * FT;
         floatx16 accp[2];
+        const int npool = g.G / PC * g.P;  // pooled values of one frame row
+        const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(pool + (int64_t)n * ps), (short)0, npool * 4, 0x00020000);
+        const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(mask + (int64_t)n * ms), (short)0, npool, 0x00020000);
         auto valid = [&](int i) { return i / FT < NG && wave + 4 * (i % FT) < ntile; };
 #pragma unroll
         for (int i = 0; i <= NI; i++) {
@@ -394,16 +399,20 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
           const int gb = (i - 1) / FT, t = (i - 1) % FT;
           const floatx16 &acc = accp[(i - 1) & 1];
           const int p = (wave + 4 * t) * 32 + l_f;
-          if (p >= g.P) continue;
           // accumulator r = 4k + i of lane (l, h) is filter 8k + 4h + i at
           // position p: a pool group is PC consecutive registers (the
-          // compares and order of the LDS epilogue, so the same bits)
-          float *pd = pool + (int64_t)n * ps + p;
-          unsigned char *md = mask + (int64_t)n * ms + p;
+          // compares and order of the LDS epilogue, so the same bits).  Its
+          // pooled row is U + h * 4 / PC with U uniform: buffer stores take
+          // the lane part as voffset and U as soffset (no vector address
+          // arithmetic).  Positions past P, and rows past G (G not a
+          // multiple of 32), get a voffset past the descriptors' ranges and
+          // are dropped (the range check covers voffset, not soffset).
+          const unsigned vo = p < g.P ? (unsigned)(h_f * (4 / PC) * g.P + p) : 0x3ffffff0u;
 #pragma unroll
           for (int r0 = 0; r0 < 16; r0 += PC) {
-            const int row = gb * 32 + mfma32_row(r0, lane_f);
-            if (row >= g.G) continue;
+            const int U = (gb * 32 + (r0 & 3) + 8 * (r0 >> 2)) / PC;
+            const unsigned vv =
+                g.G % 32 == 0 || U + h_f * (4 / PC) < g.G / PC ? vo : 0x3ffffff0u;
             float mx = -1e20f;
 #pragma unroll
             for (int c = 0; c < PC; c++)
@@ -411,9 +420,10 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
             unsigned m = 0;
 #pragma unroll
             for (int c = 0; c < PC; c++) m |= (acc[r0 + c] == mx ? 1u : 0u) << c;
-            const int64_t off = (int64_t)(row / PC) * g.P;
-            pd[off] = mx;
-            md[off] = (unsigned char)m;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mx), prs, vv * 4u,
+                                                  (unsigned)(U * g.P) * 4u, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((unsigned char)m, mrs, vv,
+                                                 (unsigned)(U * g.P), 0);
           }
         }
         KCNN_TMARK(2)

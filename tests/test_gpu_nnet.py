@@ -40,6 +40,7 @@ STACKS = {
     "pc2_G96": (12, 7, 2, 3, 2, 96, 2, 32, 0, 0),
     "pc8_G64": (9, 5, 1, 2, 2, 64, 8, 16, 0, 0),
     "G48_pad": (6, 5, 2, 3, 3, 48, 4, 8, 1, 1),     # last filter group of 16 maps
+    "G40_pc4": (10, 6, 2, 3, 2, 40, 4, 8, 0, 0),    # bf16x6 forward: pooled rows past G
     "pc3_unfused": (8, 6, 1, 3, 1, 30, 3, 8, 0, 0),  # not fusable: plain path
     "G256_pc4": (12, 6, 2, 4, 2, 256, 4, 16, 0, 0),  # 2 filter chunks of 128
     # 3-D windows (qh x qw x pc, 16-bit routing mask): (..., pad_h, pad_w, qh, qw)

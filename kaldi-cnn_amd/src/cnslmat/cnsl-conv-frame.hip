@@ -1042,8 +1042,11 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
     float ain[2][16];
 #pragma unroll
     for (int ch = 0; ch < NCH; ch++) {
-      // slab (n, ch) landed; the other buffer's readers are done
+      // slab (n, ch) landed; the other buffer's readers are done.  The
+      // explicit vmcnt(0): an LDS-DMA writes LDS, not VGPRs, so no wait of
+      // the compiler's covers another wave's reads of it
       KCNN_TMARK(6)
+      x6::wait_dma();
       __syncthreads();
       KCNN_TMARK(0)
       {

@@ -200,6 +200,21 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
                                                  (uint32_t)(ch * NJ * P + q * 256), 0, 0);
     }
   };
+  // PCM > 0: this thread's split units (pooled row j, position quad p0) are
+  // the same in every slab: their image offsets are computed once.  yoff(row,
+  // p0) for row = PCM*j + c is ubase + c*ROWB + ((ux[c >> 2] ^ ((c & 3) << 2)) << 4)
+  int uj[MAXU], up0[MAXU], ubase[MAXU], ux[MAXU][2];
+#pragma unroll
+  for (int i = 0; i < MAXU; ++i) {
+    const int u = min(tid + NT * i, NU - 1);
+    uj[i] = u / NPQ;
+    up0[i] = (u - uj[i] * NPQ) * 4;
+    const int r0 = (PCM > 0 ? PCM : 4) * uj[i];
+    ubase[i] = r0 * ROWB + ((up0[i] >> 7) << 8) + ((up0[i] & 7) << 1);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+      ux[i][hh] = ((up0[i] >> 3) & 15) ^ ((((r0 >> 2) + hh)) & 3);
+  }
   auto split_slab = [&](int ch) {
 #pragma unroll
     for (int i = 0; i < MAXU; ++i) {
@@ -208,15 +223,17 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
       if constexpr (PCM > 0) {
         // split the pooled values once, then gate the planes per map: map c
         // of the pool group gets the value where bit c of the mask byte is
-        // set (the in_value == out_value test of Maxpool_backprop), +0 else
-        const int j = u / NPQ, p0 = (u - j * NPQ) * 4;
+        // set (the in_value == out_value test of Maxpool_backprop), +0 else.
+        // Positions past P get mask 0, so their values (the next row's, or
+        // the staging tail) never reach the image: the AND writes +0.
+        const int j = uj[i], p0 = up0[i];
+        const int sj = j * P + p0;
         float x[4];
         unsigned mk[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const bool in = p0 + q < P;
-          x[q] = in ? Sdp[j * P + p0 + q] : 0.0f;
-          mk[q] = in ? (unsigned)Smk[j * P + p0 + q] : 0u;
+          x[q] = Sdp[sj + q];
+          mk[q] = p0 + q < P ? (unsigned)Smk[sj + q] : 0u;
         }
         uint32_t h01, m01, l01, h23, m23, l23;
         split2(x[0], x[1], h01, m01, l01);
@@ -229,7 +246,8 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
           const s16x2 sh = {(short)(15 - c), (short)(15 - c)}, k15 = {15, 15};
           const uint32_t s01 = __builtin_bit_cast(uint32_t, (s16x2)((w01 << sh) >> k15));
           const uint32_t s23 = __builtin_bit_cast(uint32_t, (s16x2)((w23 << sh) >> k15));
-          const int o = yoff(j * PCM + c, p0);
+          // yoff(j * PCM + c, p0) from the unit's precomputed parts
+          const int o = ubase[i] + c * ROWB + ((ux[i][c >> 2] ^ ((c & 3) << 2)) << 4);
           *reinterpret_cast<uint2 *>(Yp + o) = make_uint2(h01 & s01, h23 & s23);
           *reinterpret_cast<uint2 *>(Yp + YPL + o) = make_uint2(m01 & s01, m23 & s23);
           *reinterpret_cast<uint2 *>(Yp + 2 * YPL + o) = make_uint2(l01 & s01, l23 & s23);
@@ -344,6 +362,7 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
       for (int t = 0; t < (RD ? MAXT : 1); ++t) zacc[t] = zero16();
 #pragma unroll
       for (int ch = 0; ch < NCH; ch++) {
+        x6::wait_dma();   // this wave's LDS-DMA of the slab (and map) has landed
         __syncthreads();  // B1: the image's readers are done; last frame's Z is in LDS
         if (ch == 0) {
           if (WG) commit_x();

@@ -62,6 +62,13 @@ __device__ __forceinline__ floatx16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b
   return c;
 }
 
+// Wait for this wave's outstanding vector-memory loads, LDS-DMA included
+// (s_waitcnt vmcnt(0); gfx9 encoding: expcnt and lgkmcnt fields at their
+// no-wait maxima).  An LDS-DMA load writes LDS, not VGPRs, so the compiler's
+// own waits (placed before uses of loaded VGPRs) do not cover the LDS
+// readers of another wave: put this before the barrier that publishes it.
+__device__ __forceinline__ void wait_dma() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 __device__ __forceinline__ floatx16 zero16() {
   floatx16 z;
 #pragma unroll

@@ -863,7 +863,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_planes_kernel(GemmPlanesArgs p) {
   if (T > 0) {
     dma(0, 0);
     dma(min(1, T - 1), 1);
-    __syncthreads();  // vmcnt(0): both tiles landed
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA of both tiles
+    __syncthreads();                      // landed, for every wave
 #pragma unroll
     for (int r = 0; r < 12; ++r) read_frag(lds, 0, r, fa0, fb0);
   }
@@ -879,7 +880,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_planes_kernel(GemmPlanesArgs p) {
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();  // tile t+1 landed; buffer t & 1 fully read
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the DMA of tile t+1 (an LDS
+    __syncthreads();  // write the compiler does not track); buffer t & 1 fully read
 #pragma unroll
     for (int n = 0; n < 24; ++n) {
       mfma_n(n, fa1, fb1);

@@ -458,6 +458,183 @@ __global__ __launch_bounds__(NT, 1) void conv_wgrad_x6_kernel(
   }
 }
 
+// Weight gradient, wide tiles: 256 (g) x 256 (k) per workgroup and t steps
+// of 16, so each dY value a workgroup loads and splits feeds twice the MFMAs
+// of conv_wgrad_x6_kernel (the split's vector work per MFMA drops by a
+// third).  Images of 32-B rows (16 t), the two 16-B chunks of a row swapped
+// on rows 8-15 of every 16 (conflict-free fragment reads), 2 x 48 KB.  Waves
+// 4 (g) x 2 (k), each 64 x 128: 2 x 4 accumulators.  Thread (tp, r) = (tid %
+// 8, tid / 8) loads the t pair (2tp, 2tp + 1) of A and B rows r + 64j.
+// Same split plan, partial layout, bias sums and fixed-order reduction as
+// conv_wgrad_x6_kernel.
+constexpr int WROW = 32;  // bytes per image row (16 bf16)
+__device__ __forceinline__ int swz32(int r, int c) {
+  return r * WROW + ((c ^ ((r >> 3) & 1)) << 4);
+}
+
+template <bool PADDED>
+__global__ __launch_bounds__(NT, 1) void conv_wgrad_x6w_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ dY, int dys,
+    float *__restrict__ ws, int fps, int ktiles, int nblocks) {
+  constexpr int BG = 256, BN = 256, BT = 16;
+  constexpr int PLA = BG * WROW, PLB = BN * WROW, BUF = 3 * (PLA + PLB);
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int nb8 = (nblocks + 7) >> 3;
+  const int bid = (int)(blockIdx.x & 7) * nb8 + (int)(blockIdx.x >> 3);
+  if (bid >= nblocks) return;  // whole workgroup: no barrier is skipped
+  const int ntiles = ktiles * ((g.G + BG - 1) / BG);
+  const int split = bid / ntiles, tile = bid - split * ntiles;
+  const int k0 = (tile % ktiles) * BN, g0 = (tile / ktiles) * BG;
+  const int nbeg = split * fps;
+  const int nf = min(g.R, nbeg + fps) - nbeg;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int l = lane & 31, h = lane >> 5;
+  const int tp = tid & 7, r = tid >> 3;
+
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)(dY + (int64_t)nbeg * dys), (short)0, nf * dys * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)(X + (int64_t)nbeg * xs), (short)0, nf * xs * 4, 0x00020000);
+  unsigned koff4[4];
+  int tkx[PADDED ? 4 : 1], tky[PADDED ? 4 : 1];
+  bool kval[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int k = k0 + r + 64 * j;
+    uint32_t c = 0, rr = 0, kx = 0, ky = 0;
+    kval[j] = k < g.Kdim;
+    if (kval[j]) {
+      g.div_khkw.divmod((uint32_t)k, c, rr);
+      g.div_kh.divmod(rr, kx, ky);
+    }
+    koff4[j] = (unsigned)((int)c * g.HW + (int)kx * g.H + (int)ky) * 4u;
+    if (PADDED) { tkx[j] = (int)kx - g.pad_w; tky[j] = (int)ky - g.pad_h; }
+  }
+  const int nsteps = (nf * g.P + BT - 1) / BT;
+
+  float av[4][2], bv[4][2], bsum[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) bsum[j] = 0.0f;
+  const bool do_bias = k0 == 0;
+  auto load = [&](int st) {
+    const uint32_t t0 = (uint32_t)(st * BT + 2 * tp);
+    uint32_t n0, p0, px0, py0;
+    g.div_P.divmod(t0, n0, p0);
+    g.div_oh.divmod(p0, px0, py0);
+    uint32_t n1 = n0, p1 = p0 + 1, px1 = px0, py1 = py0 + 1;
+    if (py1 == (uint32_t)g.oh) { py1 = 0; ++px1; }
+    if (p1 == (uint32_t)g.P) { p1 = 0; px1 = 0; py1 = 0; ++n1; }
+    const uint32_t nn[2] = {n0, n1}, pp[2] = {p0, p1}, pxs[2] = {px0, px1}, pys[2] = {py0, py1};
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const unsigned a4 = (nn[e] * (unsigned)dys + pp[e]) * 4u;
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        av[j][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            ar, a4 + (unsigned)((g0 + r + 64 * j) * g.P) * 4u, 0, 0));
+      const int xo = (int)(nn[e] * (unsigned)xs) + ((int)pxs[e] - g.pad_w) * g.H +
+                     (int)pys[e] - g.pad_h;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        unsigned off = (unsigned)xo * 4u + koff4[j];
+        if (PADDED) {
+          const bool in = (unsigned)((int)pxs[e] + tkx[j]) < (unsigned)g.W &&
+                          (unsigned)((int)pys[e] + tky[j]) < (unsigned)g.H;
+          off = in ? off : kOob;
+        }
+        off = kval[j] ? off : kOob;
+        bv[j][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(br, off, 0, 0));
+      }
+    }
+  };
+  const int tc = tp >> 2, tb = (tp & 3) * 4;  // pair (2tp, 2tp+1): chunk, byte
+  auto store = [&](char *buf) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      uint32_t hh, mm, ll;
+      x6::split2(av[j][0], av[j][1], hh, mm, ll);
+      const int o = swz32(r + 64 * j, tc) + tb;
+      *reinterpret_cast<uint32_t *>(buf + o) = hh;
+      *reinterpret_cast<uint32_t *>(buf + PLA + o) = mm;
+      *reinterpret_cast<uint32_t *>(buf + 2 * PLA + o) = ll;
+      if (do_bias) bsum[j] += av[j][0] + av[j][1];
+    }
+    char *bb = buf + 3 * PLA;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      uint32_t hh, mm, ll;
+      x6::split2(bv[j][0], bv[j][1], hh, mm, ll);
+      const int o = swz32(r + 64 * j, tc) + tb;
+      *reinterpret_cast<uint32_t *>(bb + o) = hh;
+      *reinterpret_cast<uint32_t *>(bb + PLB + o) = mm;
+      *reinterpret_cast<uint32_t *>(bb + 2 * PLB + o) = ll;
+    }
+  };
+
+  floatx16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) acc[i][j] = x6::zero16();
+  load(0);
+  store(lds);
+  __syncthreads();
+  if (nsteps > 1) load(1);
+  const int arow = wm * 64 + l, brow = wn * 128 + l;
+  for (int t = 0; t < nsteps; t++) {
+    const char *bufA = lds + (t & 1) * BUF;
+    const char *bufB = bufA + 3 * PLA;
+    x6::bf16x8 a[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int pl = 0; pl < 3; pl++)
+        a[i][pl] = *reinterpret_cast<const x6::bf16x8 *>(bufA + pl * PLA + swz32(arow + 32 * i, h));
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      x6::bf16x8 bb[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; pl++)
+        bb[pl] = *reinterpret_cast<const x6::bf16x8 *>(bufB + pl * PLB + swz32(brow + 32 * j, h));
+#pragma unroll
+      for (int i = 0; i < 2; i++) acc[i][j] = x6::mfma6(a[i], bb, acc[i][j]);
+    }
+    if (t + 1 < nsteps) {
+      store(lds + ((t + 1) & 1) * BUF);
+      if (t + 2 < nsteps) load(t + 2);
+    }
+    __syncthreads();
+  }
+
+  const int64_t E = (int64_t)g.G * g.Kdim + g.G;
+  float *wsp = ws + (int64_t)split * E;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int kk = k0 + wn * 128 + 32 * j + l;
+    if (kk >= g.Kdim) continue;
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        const int gg = g0 + wm * 64 + 32 * i + mfma32_row(q, lane);
+        if (gg < g.G) wsp[(int64_t)gg * g.Kdim + kk] = acc[i][j][q];
+      }
+  }
+  if (do_bias) {
+    float *red = reinterpret_cast<float *>(lds);  // [256][9]
+#pragma unroll
+    for (int j = 0; j < 4; j++) red[(r + 64 * j) * 9 + tp] = bsum[j];
+    __syncthreads();
+    if (tid < BG && g0 + tid < g.G) {
+      float sum = 0.0f;
+      for (int i = 0; i < 8; i++) sum += red[tid * 9 + i];
+      wsp[(int64_t)g.G * g.Kdim + g0 + tid] = sum;
+    }
+  }
+}
+
 // KCNN_CONV_X6_STAGGER=1: the wave-pair stagger (STG).  It gained 4 % on
 // c5 while the split subtractions were packed into v_pk_add_f32; built
 // without SLP vectorization (Makefile) the kernels measure the same or
@@ -545,18 +722,23 @@ int kcnn_conv_igemm_x6(const ConvGeom &g, const float *X, int xs, const float *K
 // Weight gradient plan: S frame-range splits, each a whole number of frames,
 // sized so the S x tiles blocks fill whole rounds of 256 (one per CU) and an
 // accumulation chain stays within ~16k terms.
+// KCNN_WGRAD_X6: 0 off, 1 the 128-wide k tiles, 2 the wide (256) k tiles
+static int wgrad_x6_mode() {
+  static const int v = [] {
+    const char *e = getenv("KCNN_WGRAD_X6");
+    return e && *e ? atoi(e) : 2;
+  }();
+  return v;
+}
+static int wgrad_kwidth() { return wgrad_x6_mode() == 2 ? 256 : 128; }
+
 bool kcnn_conv_wgrad_x6_plan(const ConvGeom &g, int xs, int dys, int &S, int &fps,
                              size_t &ws_bytes) {
-  static const int use = [] {
-    const char *e = getenv("KCNN_WGRAD_X6");
-    return e && *e ? atoi(e) : 1;
-  }();
+  const int use = wgrad_x6_mode();
   if (!use || g.R <= 0 || g.G < 32 || g.Kdim < 32) return false;
-  const bool padded = g.pad_h > 0 || g.pad_w > 0;
-  (void)padded;
   if ((int64_t)g.C * g.HW * 4 >= (int64_t)kOob || (int64_t)g.G * g.P * 4 >= (int64_t)kOob)
     return false;
-  const int ktiles = (g.Kdim + 127) / 128;
+  const int ktiles = (g.Kdim + wgrad_kwidth() - 1) / wgrad_kwidth();
   const int ntiles = ktiles * ((g.G + 255) / 256);
   const int64_t chain = (int64_t)g.R * g.P;
   int s0 = (int)((chain + 16383) / 16384);
@@ -585,9 +767,25 @@ bool kcnn_conv_wgrad_x6_plan(const ConvGeom &g, int xs, int dys, int &S, int &fp
 int kcnn_conv_wgrad_x6(const ConvGeom &g, const float *X, int xs, const float *dY, int dys,
                        float *ws, int S, int fps, hipStream_t st) {
   const bool padded = g.pad_h > 0 || g.pad_w > 0;
-  const int ktiles = (g.Kdim + 127) / 128;
+  const int ktiles = (g.Kdim + wgrad_kwidth() - 1) / wgrad_kwidth();
   const int nblocks = S * ktiles * ((g.G + 255) / 256);
   const dim3 grid((unsigned)(8 * ((nblocks + 7) / 8)));
+  if (wgrad_kwidth() == 256) {
+    constexpr int wl = 2 * 3 * 512 * WROW;
+#define KCNN_WX6W(P_)                                                                      \
+  do {                                                                                     \
+    static bool attr = hipFuncSetAttribute(                                                \
+        reinterpret_cast<const void *>(&conv_wgrad_x6w_kernel<P_>),                        \
+        hipFuncAttributeMaxDynamicSharedMemorySize, wl) == hipSuccess;                      \
+    (void)attr;                                                                            \
+    hipLaunchKernelGGL((conv_wgrad_x6w_kernel<P_>), grid, dim3(NT), wl, st, g, X, xs, dY, \
+                       dys, ws, fps, ktiles, nblocks);                                     \
+  } while (0)
+    if (padded) KCNN_WX6W(true);
+    else KCNN_WX6W(false);
+#undef KCNN_WX6W
+    return (int)hipGetLastError();
+  }
   constexpr int lds = 2 * 3 * 384 * ROWB;
 #define KCNN_WX6(P_, S_)                                                                  \
   do {                                                                                    \

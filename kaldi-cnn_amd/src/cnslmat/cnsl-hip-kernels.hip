@@ -311,6 +311,19 @@ struct BiasUpdate {
   __device__ void operator()(int64_t, int j) const { b[j] = a_g * gb[j] + b[j]; }
 };
 
+// Both in one launch: rows [0, rows) of W as MomentumUpdate, the extra row
+// `rows` as BiasUpdate over its first b_dim columns (b_dim <= W's columns),
+// one kernel instead of two for the step's few-KB bias.
+struct MomentumBiasUpdate {
+  MomentumUpdate w;
+  BiasUpdate b;
+  int rows, b_dim;
+  __device__ void operator()(int64_t i, int j) const {
+    if (i < rows) w(i, j);
+    else if (j < b_dim) b(0, j);
+  }
+};
+
 // ---------------------------------------------------------------------------
 // Channel-group pooling (non-overlap, ph = pw = 1: the c2 1x1x4 intermap pool).
 // The pc maps of one pool group are a contiguous run of a row (pc*plane
@@ -1389,8 +1402,13 @@ int hipF_momentum_update(float *W, MatrixDim W_dim, float *prev,
                          kcnn_stream_t stream) {
   hipStream_t st = kcnn::as_stream(stream);
   MomentumUpdate f{W, W_dim, prev, prev_dim, grad, grad_dim, momentum, a_wd, a_g};
+  const bool bias = b != nullptr && grad_b != nullptr && b_dim > 0;
+  if (bias && b_dim <= W_dim.cols) {
+    MomentumBiasUpdate fw{f, BiasUpdate{b, grad_b, a_g}, W_dim.rows, b_dim};
+    return launch_elem2d(W_dim.rows + 1, W_dim.cols, fw, st);
+  }
   int rc = launch_elem2d(W_dim.rows, W_dim.cols, f, st);
-  if (rc == 0 && b != nullptr && grad_b != nullptr && b_dim > 0) {
+  if (rc == 0 && bias) {
     BiasUpdate fb{b, grad_b, a_g};
     rc = launch_elem2d(1, b_dim, fb, st);
   }

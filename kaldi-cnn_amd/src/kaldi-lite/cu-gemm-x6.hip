@@ -697,25 +697,26 @@ void launch_fast_d(const GemmFastArgs &a, unsigned blocks, hipStream_t st) {
                      LDS_BYTES, st, a);
 }
 
-// KCNN_X6_DBG (timing experiments only; results are wrong): 1 no split
-// stores, 2 no HBM loads, 4 no MFMAs, 8 no barrier, 16 no fragment reads
+// the DBG template argument (timing experiments that skip work, so the
+// results are wrong: 1 no split stores, 2 no HBM loads, 4 no MFMAs, 8 no
+// barrier, 16 no fragment reads) is selectable by KCNN_X6_DBG only in the
+// phase-timing build (make timing), never in libkcnn.so
 template <bool A_KC, bool B_KC>
 void launch_fast(const GemmFastArgs &a, unsigned blocks, hipStream_t st) {
+#ifdef KCNN_PHASE_TIMING
   static const int dbg = [] {
     const char *e = getenv("KCNN_X6_DBG");
     return e ? atoi(e) : 0;
   }();
   switch (dbg) {
-    case 1: launch_fast_d<A_KC, B_KC, 1>(a, blocks, st); break;
-    case 2: launch_fast_d<A_KC, B_KC, 2>(a, blocks, st); break;
-    case 3: launch_fast_d<A_KC, B_KC, 3>(a, blocks, st); break;
-    case 4: launch_fast_d<A_KC, B_KC, 4>(a, blocks, st); break;
-    case 6: launch_fast_d<A_KC, B_KC, 6>(a, blocks, st); break;
-    case 11: launch_fast_d<A_KC, B_KC, 11>(a, blocks, st); break;
-    case 27: launch_fast_d<A_KC, B_KC, 27>(a, blocks, st); break;
-    case 9: launch_fast_d<A_KC, B_KC, 9>(a, blocks, st); break;
-    default: launch_fast_d<A_KC, B_KC, 0>(a, blocks, st); break;
+    case 1: launch_fast_d<A_KC, B_KC, 1>(a, blocks, st); return;
+    case 2: launch_fast_d<A_KC, B_KC, 2>(a, blocks, st); return;
+    case 4: launch_fast_d<A_KC, B_KC, 4>(a, blocks, st); return;
+    case 16: launch_fast_d<A_KC, B_KC, 16>(a, blocks, st); return;
+    default: break;
   }
+#endif
+  launch_fast_d<A_KC, B_KC, 0>(a, blocks, st);
 }
 
 // KCNN_X6_FAST=1 selects the one-block-per-step kernel above.  It is not the

@@ -433,10 +433,15 @@ def main():
         # FullyConnectedComponent's three GEMMs (CuMatrixBase::AddMatMat):
         # the in-house bf16x6 kernel (kaldi-lite/cu-gemm-x6.hip) by default,
         # rocBLAS sgemm with KCNN_GEMM=0
+        fc_tf = FC_FLOP * B / (k_fc[0] / args.steps) / 1e9
         kernels["fc_gemms"] = {
             "engine": "bf16x6 (cu-gemm-x6.hip)" if gemm_x6 else "rocBLAS sgemm",
             "ms_per_step": round(k_fc[0] / args.steps, 4),
-            "TFLOP/s": round(FC_FLOP * B / (k_fc[0] / args.steps) / 1e9, 2)}
+            "TFLOP/s": round(fc_tf, 2),
+            "mfma_frac": round(fc_tf / PEAK_FP32_MFMA_TFLOPS, 4),
+            # six bf16 products per fp32 product: the share of the bf16 engine
+            "frac_of_bf16_peak": round(6 * fc_tf / PEAK_BF16_MFMA_TFLOPS, 4) if gemm_x6
+            else None}
 
     # Dominant hand-written hot-path kernel by time.
     dom = max((k for k in kernels if not k.startswith("fc_")),

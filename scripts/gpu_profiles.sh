@@ -14,6 +14,9 @@ timeout -k 10 300 python bench.py --no-cpu-baseline --no-fusion --json-out $O/be
 timeout -k 10 300 python bench.py --no-cpu-baseline --store-conv-out --json-out $O/bench_store.json > $O/bench_store.log 2>&1 || exit 5
 timeout -k 10 300 python bench.py --config c5 --json-out $O/bench_c5.json > $O/bench_c5.log 2>&1 || exit 5
 timeout -k 10 300 python bench.py --config nnet --json-out $O/bench_nnet.json > $O/bench_nnet.log 2>&1 || exit 5
+# c3 (65536 frames on one GPU) and one rank's c4 shard (16384 frames)
+timeout -k 10 300 python bench.py --no-cpu-baseline --frames-per-gpu 65536 --json-out $O/bench_c3.json > $O/bench_c3.log 2>&1 || exit 5
+timeout -k 10 300 python bench.py --no-cpu-baseline --frames-per-gpu 16384 --json-out $O/bench_c4shard.json > $O/bench_c4shard.log 2>&1 || exit 5
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c2/prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/c2.prof.log 2>&1 || exit 6
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $O/c2/pmc_$c -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/c2.pmc_$c.log 2>&1 || exit 7

@@ -276,6 +276,24 @@ int hipF_conv2d_backward_pooled(const float *in, MatrixDim in_dim, int in_height
                                 MatrixDim grad_W_dim, float *grad_b, void *workspace,
                                 size_t workspace_bytes, kcnn_stream_t stream);
 
+/* The same for a 3-D window pool_height_dim x 1 x pool_channel_dim
+ * (pool_height_dim in {2, 3} dividing the conv's out-height, pool_channel_dim
+ * in {4, 8}, at most 16 window elements: c5's P1 3 x 1 x 4) from the 16-bit
+ * routing mask of hipF_conv2d_maxpool3d (mask_stride in elements):
+ * MaxpoolComponent::Backprop (hipF_maxpool_backprop_mask3d) folded into
+ * ConvolutionComponent::Backprop.  -1 without launching when not covered. */
+int hipF_conv2d_backward_pooled3d(const float *in, MatrixDim in_dim, int in_height,
+                                  int in_width, int in_channel, int pad_h, int pad_w,
+                                  const unsigned short *mask, int mask_stride,
+                                  const float *pool_deriv, MatrixDim pool_deriv_dim,
+                                  int pool_height_dim, int pool_width_dim,
+                                  int pool_channel_dim, const float *kernel,
+                                  MatrixDim kernel_dim, int kernel_height,
+                                  int kernel_width, int group, float *in_deriv,
+                                  MatrixDim in_deriv_dim, float *grad_W,
+                                  MatrixDim grad_W_dim, float *grad_b, void *workspace,
+                                  size_t workspace_bytes, kcnn_stream_t stream);
+
 /* Momentum / weight-decay step of ConvolutionComponent::Update
  * (nnet-component-nnet0.cc:769-775) and FullyConnectedComponent::UpdateSimple
  * (:1137-1142), one pass:  prev = momentum*prev + a_wd*W + a_g*grad;

@@ -808,8 +808,7 @@ int kcnn_nnet_backprop_component(kcnn_nnet *n, int i, const float *out_deriv,
       KALDI_ASSERT(pool != NULL);
       // mode 1, not the last component: left to the conv below, which
       // builds its out_deriv from od and the mask slab by slab
-      if (g_fusion == 1 && i < nc - 1 && (pool->FusableChannelPool() == 4 ||
-                                          pool->FusableChannelPool() == 8)) {
+      if (g_fusion == 1 && i < nc - 1 && pool->FoldsIntoConvBackprop()) {
         n->deriv_deferred[i] = 1;
         return;
       }

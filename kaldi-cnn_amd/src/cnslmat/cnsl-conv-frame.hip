@@ -1706,7 +1706,8 @@ static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
                            const float *dY, int dys, const float *K, int ks,
                            float *dX, int dxs, float *gW, int gws, float *gb,
                            void *ws, size_t ws_bytes, int dx_acc, hipStream_t st,
-                           const unsigned char *pmask = nullptr, int pms = 0, int pc = 0) {
+                           const unsigned char *pmask = nullptr, int pms = 0, int pc = 0,
+                           int ph = 1) {
   static const int enabled = env_int("KCNN_FUSED_BWD", 1);
   static const int variant = env_int("KCNN_BWD_VARIANT", 3);  // 1: register-staged
   static const int bdbg = env_int("KCNN_BWD_DEBUG", 0);
@@ -1715,7 +1716,7 @@ static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
   // the bf16x6 kernel (cnsl-conv-x6.hip) where the shape allows; KCNN_BWD_X6=0
   // keeps the fp32-MFMA kernels below
   static const int use_x6 = env_int("KCNN_BWD_X6", 1);
-  if (use_x6 && variant == 3 && kcnn_conv_bwd_x6_eligible(g, dX != nullptr, pc)) {
+  if (use_x6 && variant == 3 && kcnn_conv_bwd_x6_eligible(g, dX != nullptr, pc, ph)) {
     const int S = (int)frame_grid(g, 1);
     const int E = (g.Kdim + 1) * g.G;
     float *part = static_cast<float *>(ws);
@@ -1724,12 +1725,13 @@ static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
       if (need == 0 || ws == nullptr || ws_bytes < need) return -1;
     }
     int rc = kcnn_conv_bwd_x6(g, X, xs, dY, dys, K, ks, dX, dxs, gW ? part : nullptr, S,
-                              dx_acc, st, pmask, pms, pc);
+                              dx_acc, st, pmask, pms, pc, ph);
     if (rc || gW == nullptr) return rc;
     hipLaunchKernelGGL(reduce_splits_kernel, dim3((E + 63) / 64), dim3(256), 0, st, part, S,
                        E, g.Kdim * g.G, g.G, 0, gW, gws, gb);
     return (int)hipGetLastError();
   }
+  if (ph != 1) return -1;  // 3-D windows: the bf16x6 kernel only
   if (g.P < 16 || g.P > 32 * BWD_WAVES * BWD_MAXT || 8 * g.P > BWD_THREADS * BWD_MAXV)
     return -1;
   if (pc == 0 && ((uintptr_t)dY % 16 != 0 || dys % 4 != 0)) return -1;  // 16-B slab loads
@@ -1837,21 +1839,23 @@ int kcnn_conv_bwd_frame(const ConvGeom &g, const float *X, int xs,
                         const float *dY, int dys, const float *K, int ks,
                         float *dX, int dxs, float *gW, int gws, float *gb,
                         void *ws, size_t ws_bytes, hipStream_t st,
-                        const unsigned char *pmask, int pms, int pc) {
+                        const unsigned char *pmask, int pms, int pc, int ph) {
   if (g.G <= 128)
     return bwd_frame_chunk(g, X, xs, dY, dys, K, ks, dX, dxs, gW, gws, gb, ws,
-                           ws_bytes, 0, st, pmask, pms, pc);
+                           ws_bytes, 0, st, pmask, pms, pc, ph);
   if (g.G % 32 != 0 || (int64_t)g.G * g.P * 4 % 16 != 0) return -1;
   static const int variant = env_int("KCNN_BWD_VARIANT", 3);
   if (variant != 3 && dX != nullptr) return -1;  // chunking needs dX accumulation
   for (int g0 = 0; g0 < g.G; g0 += 128) {
     ConvGeom gc = g;
     gc.G = g.G - g0 < 128 ? g.G - g0 : 128;
-    const int64_t dofs = (int64_t)(pc ? g0 / pc : g0) * g.P;  // pooled rows when pc
+    // pooled rows of P / ph values when pc, masks of 1 (ph == 1) or 2 bytes
+    const int64_t dofs = pc ? (int64_t)(g0 / pc) * (g.P / ph) : (int64_t)g0 * g.P;
+    const int64_t mofs = dofs * (ph > 1 ? 2 : 1);
     const int rc = bwd_frame_chunk(
         gc, X, xs, dY + dofs, dys, K + g0, ks, dX, dxs, gW ? gW + g0 : nullptr, gws,
-        gb ? gb + g0 : nullptr, ws, ws_bytes, g0 > 0, st, pmask ? pmask + dofs : nullptr,
-        pms, pc);
+        gb ? gb + g0 : nullptr, ws, ws_bytes, g0 > 0, st, pmask ? pmask + mofs : nullptr,
+        pms, pc, ph);
     if (rc) {
       // only the first chunk may decline (nothing written yet); a later
       // failure is a launch error

@@ -1415,6 +1415,45 @@ size_t hipF_conv2d_backward_workspace_bytes(MatrixDim in_dim, int in_height,
   return c > a ? c : a;
 }
 
+// The pooled backward of a ph x 1 x pc window (ph == 1: channel-only, 1-byte
+// mask; else a 2-byte mask), mask_bytes = the mask's row pitch in bytes.
+static int conv2d_backward_pooled(const float *in, MatrixDim in_dim, int in_height,
+                                  int in_width, int in_channel, int pad_h, int pad_w,
+                                  const unsigned char *mask, int64_t mask_pitch,
+                                  int64_t mask_cols, const float *pool_deriv,
+                                  MatrixDim pool_deriv_dim, int ph, int pc,
+                                  const float *kernel, MatrixDim kernel_dim,
+                                  int kernel_height, int kernel_width, int group,
+                                  float *in_deriv, MatrixDim in_deriv_dim, float *grad_W,
+                                  MatrixDim grad_W_dim, float *grad_b, void *workspace,
+                                  size_t workspace_bytes, hipStream_t st) {
+  ConvGeom g = make_geom(in_dim.rows, in_height, in_width, in_channel, pad_h,
+                         pad_w, kernel_height, kernel_width, group);
+  if (g.oh <= 0 || g.ow <= 0 || in_dim.cols != g.HW * in_channel ||
+      !(pc == 2 || pc == 4 || pc == 8) || group % pc != 0 ||  // pc = 2: declined below
+      ph < 1 || g.oh % ph != 0 ||
+      pool_deriv_dim.rows != g.R ||
+      (int64_t)pool_deriv_dim.cols * pc * ph != (int64_t)g.P * group ||
+      mask == nullptr || mask_cols < pool_deriv_dim.cols ||
+      kernel_dim.rows != g.Kdim || kernel_dim.cols != group ||
+      (grad_W == nullptr && in_deriv == nullptr) ||
+      (grad_W != nullptr && (grad_W_dim.rows != g.Kdim || grad_W_dim.cols != group)))
+    return (int)hipErrorInvalidValue;
+  if (in_deriv != nullptr &&
+      (in_deriv_dim.rows != g.R || in_deriv_dim.cols != g.HW * in_channel ||
+       pad_h > kernel_height - 1 || pad_w > kernel_width - 1))
+    return (int)hipErrorInvalidValue;
+  if (g.M >= ((int64_t)1 << 31) || mask_pitch >= ((int64_t)1 << 31))
+    return (int)hipErrorInvalidValue;
+  if (g.R == 0) return 0;
+  return kcnn_conv_bwd_frame(g, in, in_dim.stride, pool_deriv, pool_deriv_dim.stride,
+                             kernel, kernel_dim.stride, in_deriv,
+                             in_deriv ? in_deriv_dim.stride : 0, grad_W,
+                             grad_W ? grad_W_dim.stride : 0, grad_b, workspace,
+                             workspace_bytes, st, mask, (int)mask_pitch, pc,
+                             ph);  // -1: declined, > 0: HIP error
+}
+
 int hipF_conv2d_backward_pooled(const float *in, MatrixDim in_dim, int in_height,
                                 int in_width, int in_channel, int pad_h, int pad_w,
                                 const unsigned char *mask, int mask_stride,
@@ -1425,29 +1464,33 @@ int hipF_conv2d_backward_pooled(const float *in, MatrixDim in_dim, int in_height
                                 MatrixDim in_deriv_dim, float *grad_W,
                                 MatrixDim grad_W_dim, float *grad_b, void *workspace,
                                 size_t workspace_bytes, kcnn_stream_t stream) {
-  ConvGeom g = make_geom(in_dim.rows, in_height, in_width, in_channel, pad_h,
-                         pad_w, kernel_height, kernel_width, group);
-  const int pc = pool_channel_dim;
-  if (g.oh <= 0 || g.ow <= 0 || in_dim.cols != g.HW * in_channel ||
-      !(pc == 2 || pc == 4 || pc == 8) || group % pc != 0 ||  // pc = 2: declined below
-      pool_deriv_dim.rows != g.R || (int64_t)pool_deriv_dim.cols * pc != (int64_t)g.P * group ||
-      mask == nullptr || mask_stride < pool_deriv_dim.cols ||
-      kernel_dim.rows != g.Kdim || kernel_dim.cols != group ||
-      (grad_W == nullptr && in_deriv == nullptr) ||
-      (grad_W != nullptr && (grad_W_dim.rows != g.Kdim || grad_W_dim.cols != group)))
-    return (int)hipErrorInvalidValue;
-  if (in_deriv != nullptr &&
-      (in_deriv_dim.rows != g.R || in_deriv_dim.cols != g.HW * in_channel ||
-       pad_h > kernel_height - 1 || pad_w > kernel_width - 1))
-    return (int)hipErrorInvalidValue;
-  if (g.M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
-  if (g.R == 0) return 0;
-  return kcnn_conv_bwd_frame(g, in, in_dim.stride, pool_deriv, pool_deriv_dim.stride,
-                             kernel, kernel_dim.stride, in_deriv,
-                             in_deriv ? in_deriv_dim.stride : 0, grad_W,
-                             grad_W ? grad_W_dim.stride : 0, grad_b, workspace,
-                             workspace_bytes, kcnn::as_stream(stream), mask,
-                             mask_stride, pc);  // -1: declined, > 0: HIP error
+  return conv2d_backward_pooled(in, in_dim, in_height, in_width, in_channel, pad_h, pad_w,
+                                mask, mask_stride, mask_stride, pool_deriv, pool_deriv_dim,
+                                1, pool_channel_dim, kernel, kernel_dim, kernel_height,
+                                kernel_width, group, in_deriv, in_deriv_dim, grad_W,
+                                grad_W_dim, grad_b, workspace, workspace_bytes,
+                                kcnn::as_stream(stream));
+}
+
+int hipF_conv2d_backward_pooled3d(const float *in, MatrixDim in_dim, int in_height,
+                                  int in_width, int in_channel, int pad_h, int pad_w,
+                                  const unsigned short *mask, int mask_stride,
+                                  const float *pool_deriv, MatrixDim pool_deriv_dim,
+                                  int pool_height_dim, int pool_width_dim,
+                                  int pool_channel_dim, const float *kernel,
+                                  MatrixDim kernel_dim, int kernel_height,
+                                  int kernel_width, int group, float *in_deriv,
+                                  MatrixDim in_deriv_dim, float *grad_W,
+                                  MatrixDim grad_W_dim, float *grad_b, void *workspace,
+                                  size_t workspace_bytes, kcnn_stream_t stream) {
+  if (pool_width_dim != 1 || pool_height_dim < 2) return -1;  // not covered
+  return conv2d_backward_pooled(in, in_dim, in_height, in_width, in_channel, pad_h, pad_w,
+                                reinterpret_cast<const unsigned char *>(mask),
+                                (int64_t)mask_stride * 2, mask_stride, pool_deriv,
+                                pool_deriv_dim, pool_height_dim, pool_channel_dim, kernel,
+                                kernel_dim, kernel_height, kernel_width, group, in_deriv,
+                                in_deriv_dim, grad_W, grad_W_dim, grad_b, workspace,
+                                workspace_bytes, kcnn::as_stream(stream));
 }
 
 int hipF_conv2d_backward(const float *in, MatrixDim in_dim, int in_height,

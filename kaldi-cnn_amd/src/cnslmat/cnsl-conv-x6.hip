@@ -18,7 +18,7 @@
 // One workgroup (512 threads) per CU walks frames; per frame and 32-filter
 // slab of dY:
 //   split   the slab's dY (PCM > 0: built from the pooled derivative dP and
-//           the 1-byte routing mask of a fused 1 x 1 x PCM Maxpool, i.e.
+//           the routing mask of a fused PH x 1 x PCM Maxpool, i.e.
 //           MaxpoolComponent::Backprop folded in) is gated, split and written
 //           as three bf16 planes of a [g][p] LDS image (768-B rows, 16-B
 //           chunks XOR-swizzled per 256-B segment, so that 32-lane row reads
@@ -89,19 +89,25 @@ __device__ __forceinline__ int woff(int k, int g) {
 }
 
 __host__ __device__ inline int round4(int n) { return (n + 3) & ~3; }
-// staging floats for one slab's dP rows (whole 1-KiB DMA chunks), and bytes
-// for its mask (whole 256-B chunks)
-__host__ __device__ inline int x6_stage_floats(int P, int pcm) {
-  return (((pcm > 0 ? 32 / pcm : 32) * P * 4 + 1023) & ~1023) / 4;
+// staging floats for one slab's dP rows and bytes for its mask: whole DMA
+// chunks (1 KiB, 256 B) and room for the split's reads past the last row (up
+// to 16 values, masked off); ph > 1: P / ph pooled positions per row, 2-byte
+// mask
+__host__ __device__ inline int x6_stage_floats(int P, int pcm, int ph) {
+  return (((pcm > 0 ? 32 / pcm : 32) * (P / ph) * 4 + 64 + 1023) & ~1023) / 4;
 }
-__host__ __device__ inline int x6_stage_mask_bytes(int P, int pcm) {
-  return pcm > 0 ? (((32 / pcm) * P + 255) & ~255) : 0;
+__host__ __device__ inline int x6_stage_mask_bytes(int P, int pcm, int ph) {
+  return pcm > 0 ? (((32 / pcm) * (P / ph) * (ph > 1 ? 2 : 1) + 32 + 255) & ~255) : 0;
 }
 
-// PCM > 0: dY / dys are the pooled derivative dP of a 1 x 1 x PCM Maxpool,
-// pmask / pms its routing mask: dY[g][p] = bit g % PCM of mask[g / PCM][p] ?
-// dP[g / PCM][p] : +0 (hipF_maxpool_backprop_mask).
-template <int NCH, bool DX, bool WG, int PCM>
+// PCM > 0: dY / dys are the pooled derivative dP of a PH x 1 x PCM Maxpool
+// (PH = 1: channel-only; PH > 1 divides oh, so map position p = x*oh + y
+// pools into p / PH), pmask / pms (bytes) its routing mask, 1 byte (PH = 1)
+// or 2 (PH > 1) per pooled value:
+//   dY[g][p] = bit (g % PCM)*PH + p % PH of mask[g / PCM][p / PH] ?
+//              dP[g / PCM][p / PH] : +0
+// (hipF_maxpool_backprop_mask, hipF_maxpool_backprop_mask3d with pw = 1).
+template <int NCH, bool DX, bool WG, int PCM, int PH>
 __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
     ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ dY, int dys,
     const float *__restrict__ K, int ks, float *__restrict__ dX, int dxs,
@@ -116,6 +122,8 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
   // raw dY slab (46 KB at c2), so Z goes to the image at the frame's end and
   // is col2im'ed there, between two more barriers.
   constexpr bool DEFER = PCM > 0;
+  using MaskT = typename std::conditional<(PH > 1), unsigned short, unsigned char>::type;
+  const int Q = P / PH;  // pooled positions per dP row
   char *Yp = smem;                                   // [3][32][384] bf16
   char *Wimg = Yp + 3 * YPL;                         // [3][32][128] bf16
   float *Zs = DEFER ? reinterpret_cast<float *>(Wimg + (DX ? 3 * WPL : 0))  // [P][ZZ]
@@ -127,7 +135,7 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
   // mask bytes, PCM == 0 its 32 rows of dY
   constexpr int NJ = PCM > 0 ? 32 / PCM : 32;
   float *Sdp = reinterpret_cast<float *>(qtab + PP);          // [NJ][P] (+ DMA tail)
-  unsigned char *Smk = reinterpret_cast<unsigned char *>(Sdp + x6_stage_floats(P, PCM));
+  MaskT *Smk = reinterpret_cast<MaskT *>(Sdp + x6_stage_floats(P, PCM, PH));
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = lane & 31, hf = lane >> 5;
@@ -182,22 +190,23 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
   // dP and of the mask, unit u = (pooled row j, position quad pq); PCM == 0:
   // its 32 rows of dY, unit u = (filter quad gq, position quad pq).
   auto load_slab = [&](int n, int ch) {
-    const int rowf = (PCM > 0 ? g.G / PCM : g.G) * P;  // values per frame row
+    const int rowf = (PCM > 0 ? g.G / PCM : g.G) * Q;  // values per frame row
     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(dY + (int64_t)n * dys), (short)0, rowf * 4, 0x00020000);
-    const int nq = (NJ * P * 4 + 1023) >> 10;
+    const int nq = (NJ * Q * 4 + 1023) >> 10;
     for (int q = wave; q < nq; q += NW)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rd, (lds_void_t *)(Sdp + q * 256), 16,
                                                (uint32_t)lane * 16u,
-                                               (uint32_t)(ch * NJ * P * 4 + q * 1024), 0, 0);
+                                               (uint32_t)(ch * NJ * Q * 4 + q * 1024), 0, 0);
     if constexpr (PCM > 0) {
+      constexpr int MB = (int)sizeof(MaskT);
       const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(
-          (void *)(pmask + (int64_t)n * pms), (short)0, rowf, 0x00020000);
-      const int nm = (NJ * P + 255) >> 8;
+          (void *)(pmask + (int64_t)n * pms), (short)0, rowf * MB, 0x00020000);
+      const int nm = (NJ * Q * MB + 255) >> 8;
       for (int q = wave; q < nm; q += NW)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, (lds_void_t *)(Smk + q * 256), 4,
-                                                 (uint32_t)lane * 4u,
-                                                 (uint32_t)(ch * NJ * P + q * 256), 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rm, (lds_void_t *)(reinterpret_cast<char *>(Smk) + q * 256), 4,
+            (uint32_t)lane * 4u, (uint32_t)(ch * NJ * Q * MB + q * 256), 0, 0);
     }
   };
   // PCM > 0: this thread's split units (pooled row j, position quad p0) are
@@ -222,30 +231,48 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
       if (u >= NU) break;
       if constexpr (PCM > 0) {
         // split the pooled values once, then gate the planes per map: map c
-        // of the pool group gets the value where bit c of the mask byte is
-        // set (the in_value == out_value test of Maxpool_backprop), +0 else.
+        // of the pool group gets the value where its mask bit is set (the
+        // in_value == out_value test of Maxpool_backprop), +0 else.
         // Positions past P get mask 0, so their values (the next row's, or
         // the staging tail) never reach the image: the AND writes +0.
         const int j = uj[i], p0 = up0[i];
-        const int sj = j * P + p0;
         float x[4];
         unsigned mk[4];
+        short rq[4];  // p % PH: the window row, the low part of the mask bit
+        if constexpr (PH > 1) {
+          // the quad's 4 positions fall in 2 windows (p0 % 4 == 0, PH <= 3)
+          const int pq0 = p0 / PH, r0 = p0 - pq0 * PH, s0 = j * Q + pq0;
+          const float x0 = Sdp[s0], x1 = Sdp[s0 + 1];
+          const unsigned m0 = Smk[s0], m1 = Smk[s0 + 1];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          x[q] = Sdp[sj + q];
-          mk[q] = p0 + q < P ? (unsigned)Smk[sj + q] : 0u;
+          for (int q = 0; q < 4; ++q) {
+            const bool sel = r0 + q >= PH;
+            rq[q] = (short)(r0 + q - (sel ? PH : 0));
+            x[q] = sel ? x1 : x0;
+            mk[q] = p0 + q < P ? (sel ? m1 : m0) : 0u;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            rq[q] = 0;
+            x[q] = Sdp[j * Q + p0 + q];
+            mk[q] = p0 + q < P ? (unsigned)Smk[j * Q + p0 + q] : 0u;
+          }
         }
         uint32_t h01, m01, l01, h23, m23, l23;
         split2(x[0], x[1], h01, m01, l01);
         split2(x[2], x[3], h23, m23, l23);
         const s16x2 w01 = __builtin_bit_cast(s16x2, mk[0] | (mk[1] << 16));
         const s16x2 w23 = __builtin_bit_cast(s16x2, mk[2] | (mk[3] << 16));
+        const s16x2 b01 = {(short)(15 - rq[0]), (short)(15 - rq[1])};
+        const s16x2 b23 = {(short)(15 - rq[2]), (short)(15 - rq[3])};
 #pragma unroll
         for (int c = 0; c < PCM; ++c) {
-          // bit c of each 16-bit half, sign-extended to 0 / 0xffff
-          const s16x2 sh = {(short)(15 - c), (short)(15 - c)}, k15 = {15, 15};
-          const uint32_t s01 = __builtin_bit_cast(uint32_t, (s16x2)((w01 << sh) >> k15));
-          const uint32_t s23 = __builtin_bit_cast(uint32_t, (s16x2)((w23 << sh) >> k15));
+          // bit c*PH + p % PH of each 16-bit half, sign-extended to 0 / 0xffff
+          const s16x2 cc = {(short)(c * PH), (short)(c * PH)}, k15 = {15, 15};
+          const s16x2 sh01 = b01 - cc, sh23 = b23 - cc;
+          const uint32_t s01 = __builtin_bit_cast(uint32_t, (s16x2)((w01 << sh01) >> k15));
+          const uint32_t s23 = __builtin_bit_cast(uint32_t, (s16x2)((w23 << sh23) >> k15));
           // yoff(j * PCM + c, p0) from the unit's precomputed parts
           const int o = ubase[i] + c * ROWB + ((ux[i][c >> 2] ^ ((c & 3) << 2)) << 4);
           *reinterpret_cast<uint2 *>(Yp + o) = make_uint2(h01 & s01, h23 & s23);
@@ -499,25 +526,28 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
   else frames(std::integral_constant<int, 2>{});
 }
 
-size_t x6_lds(const ConvGeom &g, bool dx, int pc) {
+size_t x6_lds(const ConvGeom &g, bool dx, int pc, int ph) {
   const int CHWp = g.C * (g.H + 2 * g.pad_h) * (g.W + 2 * g.pad_w);
   const int ZZ = g.Kdim | 1;
   return (size_t)3 * YPL + (dx ? 3 * WPL : 0) +
          (dx && pc > 0 ? (size_t)round4(g.P * ZZ) * 4 : 0) +
          (size_t)round4(CHWp + 1) * 4 + (size_t)PP * 4 +
-         (size_t)x6_stage_floats(g.P, pc) * 4 + (size_t)x6_stage_mask_bytes(g.P, pc);
+         (size_t)x6_stage_floats(g.P, pc, ph) * 4 + (size_t)x6_stage_mask_bytes(g.P, pc, ph);
 }
 
 }  // namespace
 
 // Eligible shapes: Kdim <= 31, 1 <= P <= 384, G a multiple of 32 up to 128,
-// C*H*W <= 2048, pc in {0, 4, 8}, and the LDS plan within 160 KB.
-bool kcnn_conv_bwd_x6_eligible(const ConvGeom &g, bool dx, int pc) {
+// C*H*W <= 2048, pc in {0, 4, 8}, a pool window ph x 1 x pc with ph in
+// {1, 2, 3} dividing oh and ph * pc <= 16, and the LDS plan within 160 KB.
+bool kcnn_conv_bwd_x6_eligible(const ConvGeom &g, bool dx, int pc, int ph) {
   if (g.Kdim > 31 || g.Kdim < 1 || g.P < 1 || g.P > PP) return false;
   if (g.G % 32 != 0 || g.G > 128 || g.G == 0) return false;
   if (g.C * g.HW > NT * MAXX) return false;
   if (!(pc == 0 || pc == 4 || pc == 8)) return false;
-  return x6_lds(g, dx, pc) <= (size_t)160 * 1024;
+  if (ph < 1 || ph > 3 || (ph > 1 && (pc == 0 || ph * pc > 16 || g.oh % ph != 0)))
+    return false;
+  return x6_lds(g, dx, pc, ph) <= (size_t)160 * 1024;
 }
 
 // One filter chunk (G <= 128): the workgroup partials ws_part[S][(Kdim+1) G]
@@ -526,10 +556,10 @@ bool kcnn_conv_bwd_x6_eligible(const ConvGeom &g, bool dx, int pc) {
 int kcnn_conv_bwd_x6(const ConvGeom &g, const float *X, int xs, const float *dY, int dys,
                      const float *K, int ks, float *dX, int dxs, float *ws_part, int S,
                      int dx_acc, hipStream_t st, const unsigned char *pmask, int pms,
-                     int pc) {
+                     int pc, int ph) {
   const bool dx = dX != nullptr, wg = ws_part != nullptr;
   if (!dx && !wg) return 0;
-  if (!kcnn_conv_bwd_x6_eligible(g, dx, pc)) return -1;
+  if (!kcnn_conv_bwd_x6_eligible(g, dx, pc, ph)) return -1;
   // LDS-DMA of dP (16 B per lane) and of the mask (4 B per lane)
   if ((uintptr_t)dY % 16 || dys % 4) return -1;
   if (pc > 0 && ((uintptr_t)pmask % 4 || pms % 4)) return -1;
@@ -543,23 +573,26 @@ int kcnn_conv_bwd_x6(const ConvGeom &g, const float *X, int xs, const float *dY,
     if (nstep > 4 * MAXS) return -1;
     for (int s = 0; s < nstep; ++s) tab.s[4 + s % 4][s / 4] = (uint8_t)s;
   }
-  const size_t lds = x6_lds(g, dx, pc);
+  const size_t lds = x6_lds(g, dx, pc, ph);
   const int ZZ = g.Kdim | 1;
-#define KCNN_X6P(NCH, DXB, WGB, PCM)                                                       \
+#define KCNN_X6P(NCH, DXB, WGB, PCM, PH)                                                   \
   do {                                                                                     \
     static bool attr = hipFuncSetAttribute(                                               \
-        reinterpret_cast<const void *>(&conv_bwd_x6_kernel<NCH, DXB, WGB, PCM>),            \
+        reinterpret_cast<const void *>(&conv_bwd_x6_kernel<NCH, DXB, WGB, PCM, PH>),        \
         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;             \
     (void)attr;                                                                            \
-    hipLaunchKernelGGL((conv_bwd_x6_kernel<NCH, DXB, WGB, PCM>), dim3(S), dim3(NT), lds, st, \
-                       g, X, xs, dY, dys, K, ks, dX, dxs, ws_part, ZZ, tab, dx_acc, pmask, \
-                       pms);                                                               \
+    hipLaunchKernelGGL((conv_bwd_x6_kernel<NCH, DXB, WGB, PCM, PH>), dim3(S), dim3(NT), lds, \
+                       st, g, X, xs, dY, dys, K, ks, dX, dxs, ws_part, ZZ, tab, dx_acc,     \
+                       pmask, pms);                                                        \
   } while (0)
-#define KCNN_X6M(NCH, DXB, WGB)                   \
-  do {                                            \
-    if (pc == 4) KCNN_X6P(NCH, DXB, WGB, 4);      \
-    else if (pc == 8) KCNN_X6P(NCH, DXB, WGB, 8); \
-    else KCNN_X6P(NCH, DXB, WGB, 0);              \
+#define KCNN_X6M(NCH, DXB, WGB)                                  \
+  do {                                                           \
+    if (pc == 4 && ph == 3) KCNN_X6P(NCH, DXB, WGB, 4, 3);       \
+    else if (pc == 4 && ph == 2) KCNN_X6P(NCH, DXB, WGB, 4, 2);  \
+    else if (pc == 4) KCNN_X6P(NCH, DXB, WGB, 4, 1);             \
+    else if (pc == 8 && ph == 2) KCNN_X6P(NCH, DXB, WGB, 8, 2);  \
+    else if (pc == 8) KCNN_X6P(NCH, DXB, WGB, 8, 1);             \
+    else KCNN_X6P(NCH, DXB, WGB, 0, 1);                          \
   } while (0)
 #define KCNN_X6N(NCH)                          \
   do {                                         \

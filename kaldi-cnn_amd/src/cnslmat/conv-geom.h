@@ -62,22 +62,23 @@ int kcnn_conv_dgrad_frame(const kcnn::ConvGeom &g, const float *dY, int dys,
 // Fused backward (one pass over dY): dX (nullable) and gW/gb.  ws must hold
 // kcnn_conv_bwd_frame_ws(g) bytes (0 = shape not eligible).
 size_t kcnn_conv_bwd_frame_ws(const kcnn::ConvGeom &g);
-// pc > 0: dY / dys are instead the derivative of a 1 x 1 x pc Maxpool over
-// Y and pmask / pms its routing mask (hipF_conv2d_maxpool); dY is built per
-// slab in LDS and never stored.
+// pc > 0: dY / dys are instead the derivative of a ph x 1 x pc Maxpool over
+// Y and pmask / pms its routing mask (hipF_conv2d_maxpool[3d]: 1 byte per
+// pooled value when ph == 1, else 2; pms in bytes); dY is built per slab in
+// LDS and never stored.  ph > 1 runs on the bf16x6 kernel only.
 int kcnn_conv_bwd_frame(const kcnn::ConvGeom &g, const float *X, int xs,
                         const float *dY, int dys, const float *K, int ks,
                         float *dX, int dxs, float *gW, int gws, float *gb,
                         void *ws, size_t ws_bytes, hipStream_t st,
                         const unsigned char *pmask = nullptr, int pms = 0,
-                        int pc = 0);
+                        int pc = 0, int ph = 1);
 // The same fused backward on the bf16 MFMAs with exact three-way operand
 // splits (cnsl-conv-x6.hip); ws_part == NULL runs the data gradient only.
-bool kcnn_conv_bwd_x6_eligible(const kcnn::ConvGeom &g, bool dx, int pc);
+bool kcnn_conv_bwd_x6_eligible(const kcnn::ConvGeom &g, bool dx, int pc, int ph = 1);
 int kcnn_conv_bwd_x6(const kcnn::ConvGeom &g, const float *X, int xs, const float *dY,
                      int dys, const float *K, int ks, float *dX, int dxs, float *ws_part,
                      int S, int dx_acc, hipStream_t st, const unsigned char *pmask,
-                     int pms, int pc);
+                     int pms, int pc, int ph);
 // Conv2D(concat) + bias (+ ReLU when relu) as an implicit GEMM on the bf16
 // MFMAs (cnsl-conv-igemm-x6.hip); -1 when the shape is outside its limits.
 int kcnn_conv_igemm_x6(const kcnn::ConvGeom &g, const float *X, int xs, const float *K,

@@ -669,8 +669,9 @@ bool ConvolutionComponent::BackpropPooled(const CuMatrixBase<BaseFloat> &in_valu
                                           BaseFloat *grad) const {
   ConvolutionComponent *to_update =
       grad ? NULL : dynamic_cast<ConvolutionComponent *>(to_update_in);
-  const int32 pc = pool.FusableChannelPool();
-  if (LiteralPath() || mask == NULL || !(pc == 4 || pc == 8)) return false;
+  if (LiteralPath() || mask == NULL || !pool.FoldsIntoConvBackprop()) return false;
+  int32 pc = pool.FusableChannelPool(), ph = 1, pw = 1;
+  if (pc == 0) KALDI_ASSERT(pool.FusableWindow3D(&ph, &pw, &pc));
   // Backprop without in_deriv: nothing to do, or (with an update) Update in
   // the unfused path, whose gradient kernel sums in another order: keep its bits
   if (grad == NULL && in_deriv == NULL) return false;
@@ -701,13 +702,22 @@ bool ConvolutionComponent::BackpropPooled(const CuMatrixBase<BaseFloat> &in_valu
   int rc;
   {
     CuProfileScope prof("ConvolutionComponent::BackpropPooled");
-    rc = hipF_conv2d_backward_pooled(
-        in_value.Data(), in_value.Dim(), in_height_, in_width_, in_channel_,
-        in_pad_height_, in_pad_width_, mask, mask_stride, pool_deriv.Data(),
-        pool_deriv.Dim(), pc, linear_params_.Data(), linear_params_.Dim(),
-        kernel_height_, kernel_width_, group_, in_deriv ? in_deriv->Data() : nullptr,
-        in_deriv ? in_deriv->Dim() : idd, g, Dense(KernelDim(), group_),
-        g ? g + (size_t)KernelDim() * group_ : nullptr, ws, ws_bytes, S());
+    rc = ph == 1
+        ? hipF_conv2d_backward_pooled(
+              in_value.Data(), in_value.Dim(), in_height_, in_width_, in_channel_,
+              in_pad_height_, in_pad_width_, mask, mask_stride, pool_deriv.Data(),
+              pool_deriv.Dim(), pc, linear_params_.Data(), linear_params_.Dim(),
+              kernel_height_, kernel_width_, group_, in_deriv ? in_deriv->Data() : nullptr,
+              in_deriv ? in_deriv->Dim() : idd, g, Dense(KernelDim(), group_),
+              g ? g + (size_t)KernelDim() * group_ : nullptr, ws, ws_bytes, S())
+        : hipF_conv2d_backward_pooled3d(
+              in_value.Data(), in_value.Dim(), in_height_, in_width_, in_channel_,
+              in_pad_height_, in_pad_width_, reinterpret_cast<const unsigned short *>(mask),
+              mask_stride, pool_deriv.Data(), pool_deriv.Dim(), ph, pw, pc,
+              linear_params_.Data(), linear_params_.Dim(), kernel_height_, kernel_width_,
+              group_, in_deriv ? in_deriv->Data() : nullptr,
+              in_deriv ? in_deriv->Dim() : idd, g, Dense(KernelDim(), group_),
+              g ? g + (size_t)KernelDim() * group_ : nullptr, ws, ws_bytes, S());
     if (rc < 0) prof.Cancel();  // declined: nothing launched
   }
   if (rc < 0) return false;
@@ -902,6 +912,16 @@ bool MaxpoolComponent::FusableWindow3D(int32 *ph, int32 *pw, int32 *pc) const {
   *pw = pool_width_dim_;
   *pc = c;
   return true;
+}
+
+bool MaxpoolComponent::FoldsIntoConvBackprop() const {
+  // KCNN_FOLD_3D=0: 3-D windows back to BackpropFromMask + the conv's Backprop
+  static const bool fold3d = getenv("KCNN_FOLD_3D") == nullptr || atoi(getenv("KCNN_FOLD_3D"));
+  const int32 c = FusableChannelPool();
+  if (c == 4 || c == 8) return true;
+  int32 ph, pw, pc;
+  return fold3d && c == 0 && FusableWindow3D(&ph, &pw, &pc) && pw == 1 && (ph == 2 || ph == 3) &&
+         (pc == 4 || pc == 8) && ph * pc <= 16;
 }
 
 int32 MaxpoolComponent::FusedMaskBytes() const {

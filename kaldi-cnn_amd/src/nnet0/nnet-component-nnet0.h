@@ -141,10 +141,10 @@ class ConvolutionComponent : public nnet2::UpdatableComponent {
   bool PropagateRelu(const CuMatrixBase<BaseFloat> &in,
                      CuMatrixBase<BaseFloat> *relu_out) const;
 
-  // The Backprop of `pool` (a channel-only MaxpoolComponent fed by this
-  // component, forward fused by PropagateMaxpool with routing mask `mask`)
-  // followed by this component's Backprop, in one pass
-  // (hipF_conv2d_backward_pooled): pool_deriv is the pool's out_deriv, and
+  // The Backprop of `pool` (a MaxpoolComponent fed by this component whose
+  // FoldsIntoConvBackprop() holds, forward fused by PropagateMaxpool with
+  // routing mask `mask`) followed by this component's Backprop, in one pass
+  // (hipF_conv2d_backward_pooled[3d]): pool_deriv is the pool's out_deriv, and
   // the pool's in_deriv (this component's out_deriv) is never stored.
   // grad != NULL: BackpropGradient (gradient out, no update); else Backprop
   // with the update going to to_update.  Returns false, having done nothing,
@@ -248,6 +248,11 @@ class MaxpoolComponent : public nnet2::Component {
   // Bytes per pooled value of the routing mask the fused forward writes for
   // this pool: 1 (channel-only), 2 (3-D window), 0 = not fusable.
   int32 FusedMaskBytes() const;
+  // The windows whose Backprop can run inside the backward of the
+  // convolution below (ConvolutionComponent::BackpropPooled): 1 x 1 x pc
+  // with pc in {4, 8}, and ph x 1 x pc 3-D windows with ph in {2, 3} and
+  // ph * pc <= 16 (c5's P1 3 x 1 x 4).
+  bool FoldsIntoConvBackprop() const;
   // Backprop (:882-892) from the routing mask written by
   // ConvolutionComponent::PropagateMaxpool for the same minibatch: identical
   // in_deriv to Backprop(in_value, out_value, out_deriv, ...), without

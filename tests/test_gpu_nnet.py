@@ -3,7 +3,8 @@ include/kcnn.h kcnn_nnet_*), in particular its Conv -> Maxpool fusion:
 ConvolutionComponent::PropagateMaxpool writes the pooled output and the pool's
 routing mask in one pass (Y too in fusion mode 2), and the pool's Backprop
 runs from the mask (MaxpoolComponent::BackpropFromMask), or for 1x1x4 / 1x1x8
-pools inside the conv's backward (ConvolutionComponent::BackpropPooled).
+pools and ph x 1 x pc windows (ph in {2, 3}, ph * pc <= 16) inside the conv's
+backward (ConvolutionComponent::BackpropPooled).
 
 The fusion is an exact transformation, so every output, input derivative and
 updated parameter must be bit-identical with fusion on and off; the pool
@@ -47,6 +48,7 @@ STACKS = {
     "c5_P1_3x1x4": (40, 11, 3, 8, 1, 256, 4, 16, 0, 0, 3, 1),
     "win_2x2x2": (9, 8, 2, 2, 1, 64, 2, 8, 0, 0, 2, 2),
     "win_2x1x8_pad": (6, 6, 1, 3, 3, 32, 8, 8, 1, 1, 2, 1),
+    "win_2x1x4_G96": (10, 6, 2, 3, 2, 96, 4, 8, 0, 0, 2, 1),
 }
 
 
@@ -140,7 +142,7 @@ def test_unstored_conv_output_after_backprop(kc):
             kc.set_fusion(1)
 
 
-@pytest.mark.parametrize("name", ["c2", "pc2_G96", "pc8_G64"])
+@pytest.mark.parametrize("name", ["c2", "pc2_G96", "pc8_G64", "c5_P1_3x1x4", "win_2x1x8_pad"])
 def test_fusion_exact_gradient_mode(kc, name):
     a = run(kc, STACKS[name], fused=True, mode=1)
     b = run(kc, STACKS[name], fused=False, mode=1)
@@ -160,9 +162,12 @@ def _calls(kc, key):
 
 
 @pytest.mark.parametrize("name,pooled", [("c2", True), ("pc8_G64", True), ("G256_pc4", True),
-                                         ("pc2_G96", False), ("G48_pad", False)])
+                                         ("c5_P1_3x1x4", True), ("win_2x1x8_pad", True),
+                                         ("win_2x1x4_G96", True), ("pc2_G96", False),
+                                         ("G48_pad", False), ("win_2x2x2", False)])
 def test_pooled_backward_path(kc, name, pooled):
-    """Fusion mode 1 runs a 1x1x4 / 1x1x8 pool's Backprop inside the conv's
+    """Fusion mode 1 runs a 1x1x4 / 1x1x8 pool's Backprop (and a 3x1x4, 2x1x4,
+    2x1x8 window's) inside the conv's
     (ConvolutionComponent::BackpropPooled); other shapes fall back to
     BackpropFromMask + the conv's own Backprop (the exactness tests above
     cover both routes)."""
@@ -177,7 +182,7 @@ def test_pooled_backward_path(kc, name, pooled):
     assert (after > before) == pooled
 
 
-@pytest.mark.parametrize("name", ["c2", "c5_P1_3x1x4", "win_2x1x8_pad"])
+@pytest.mark.parametrize("name", ["c2", "c5_P1_3x1x4", "win_2x1x8_pad", "win_2x1x4_G96"])
 @pytest.mark.parametrize("ties", [False, True])
 def test_fused_pool_matches_oracle(kc, name, ties):
     cfg = STACKS[name]

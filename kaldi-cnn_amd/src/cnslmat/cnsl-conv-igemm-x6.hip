@@ -50,10 +50,24 @@ __device__ __forceinline__ void put8(char *img, int pl_bytes, int off, const flo
   *reinterpret_cast<uint4 *>(img + 2 * pl_bytes + off) = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
-template <int BG, bool PADDED, bool STG, bool TAB>
+// The Maxpool that follows the convolution, pooled in the epilogue (POOL >
+// 0): a window of 2 consecutive map positions (ph x pw = 2 x 1 with oh even,
+// or 1 x 2 with oh = 1: positions p, p + 1 with p even, the columns m, m + 1
+// of lanes l, l ^ 1) by PC consecutive filters (rows 4k .. 4k + 3 of an
+// accumulator are 4 consecutive registers of one lane).  pool[n][j*P/2 +
+// p/2] and the 16-bit routing mask (bit c*2 + d for map PC*j + c at
+// position p + d) as hipF_conv2d_maxpool3d writes them; out (Y) nullable.
+struct PoolOut {
+  float *pool;
+  int ps;
+  unsigned short *mask;
+  int ms;
+};
+
+template <int BG, bool PADDED, bool STG, bool TAB, int POOL>
 __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
     ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ Kw, int ks,
-    const float *__restrict__ bias, float *__restrict__ out, int os, int relu) {
+    const float *__restrict__ bias, float *__restrict__ out, int os, int relu, PoolOut po) {
   constexpr int BN = 384 - BG;
   constexpr int APT = BG * BK / NT, BPT = BN * BK / NT;  // values per thread per step
   constexpr int PLA = BG * ROWB, PLB = BN * ROWB, BUF = 3 * (PLA + PLB);
@@ -246,6 +260,60 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
 
   // epilogue: accumulator r of lane (l, h) is row g0 + wm*64 + 32i +
   // mfma32_row(r), column m0 + wn*64 + 32j + l; concat layout + bias (+ReLU)
+  if constexpr (POOL > 0) {
+    constexpr int PC = POOL == 1 ? 4 : POOL == 2 ? 1 : 2;
+    const int Q = g.P >> 1;  // pooled positions per map
+    const int d = l & 1;     // this lane's position in its window
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const int64_t mm = m0 + wn * 64 + 32 * j + l;
+      const bool mv = mm < g.M;  // both lanes of a window alike (P even)
+      uint32_t on = 0, op = 0;
+      if (mv) g.div_P.divmod((uint32_t)mm, on, op);
+#pragma unroll
+      for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int r0 = 0; r0 < 16; r0 += PC) {
+          const int gg0 = g0 + wm * 64 + 32 * i + mfma32_row(r0, lane);
+          const bool gv = gg0 < g.G;  // G % PC == 0: a group is all in or all out
+          float v[PC], w[PC];
+#pragma unroll
+          for (int c = 0; c < PC; c++) {
+            float x = acc[i][j][r0 + c];
+            if (bias && gv) x = x + bias[gg0 + c];
+            v[c] = x;
+          }
+#pragma unroll
+          for (int c = 0; c < PC; c++) w[c] = __shfl_xor(v[c], 1);
+          if (out && mv && gv) {
+#pragma unroll
+            for (int c = 0; c < PC; c++) out[(int64_t)on * os + (int64_t)(gg0 + c) * g.P + op] = v[c];
+          }
+          // A.8's order and compare: maps c, then the window's two
+          // positions; the mask bit of each element equal to the max
+          float mx = -1e20f;
+#pragma unroll
+          for (int c = 0; c < PC; c++) {
+            const float e0 = d ? w[c] : v[c], e1 = d ? v[c] : w[c];
+            if (mx < e0) mx = e0;
+            if (mx < e1) mx = e1;
+          }
+          unsigned mk = 0;
+#pragma unroll
+          for (int c = 0; c < PC; c++) {
+            const float e0 = d ? w[c] : v[c], e1 = d ? v[c] : w[c];
+            mk |= (e0 == mx ? 1u : 0u) << (2 * c);
+            mk |= (e1 == mx ? 1u : 0u) << (2 * c + 1);
+          }
+          if (d == 0 && mv && gv) {
+            const int64_t q = (int64_t)(gg0 / PC) * Q + (op >> 1);
+            po.pool[(int64_t)on * po.ps + q] = mx;
+            po.mask[(int64_t)on * po.ms + q] = (unsigned short)mk;
+          }
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 2; j++) {
     const int64_t mm = m0 + wn * 64 + 32 * j + l;
@@ -661,16 +729,25 @@ int tab_bytes(const ConvGeom &g, bool padded) {
   return use && kImgBytes + b <= kLdsMax ? b : 0;
 }
 
-template <int BG, bool PADDED, bool STG, bool TAB>
+template <int BG, bool PADDED, bool STG, bool TAB, int POOL = 0>
 void launch_t(const ConvGeom &g, unsigned blocks, int lds, const float *X, int xs,
               const float *K, int ks, const float *bias, float *out, int os, int relu,
-              hipStream_t st) {
+              hipStream_t st, PoolOut po = PoolOut{}) {
   static bool attr = hipFuncSetAttribute(
-      reinterpret_cast<const void *>(&conv_igemm_x6_kernel<BG, PADDED, STG, TAB>),
+      reinterpret_cast<const void *>(&conv_igemm_x6_kernel<BG, PADDED, STG, TAB, POOL>),
       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax) == hipSuccess;
   (void)attr;
-  hipLaunchKernelGGL((conv_igemm_x6_kernel<BG, PADDED, STG, TAB>), dim3(blocks), dim3(NT),
-                     lds, st, g, X, xs, K, ks, bias, out, os, relu);
+  hipLaunchKernelGGL((conv_igemm_x6_kernel<BG, PADDED, STG, TAB, POOL>), dim3(blocks),
+                     dim3(NT), lds, st, g, X, xs, K, ks, bias, out, os, relu, po);
+}
+// pooled epilogue (POOL > 0): no stagger (the host declines it)
+template <int BG, bool PADDED, int POOL>
+void launch_pool(const ConvGeom &g, unsigned blocks, const float *X, int xs, const float *K,
+                 int ks, const float *bias, float *out, int os, PoolOut po, hipStream_t st) {
+  const int tb = tab_bytes(g, PADDED);
+  const int lds = kImgBytes + tb;
+  if (tb) launch_t<BG, PADDED, false, true, POOL>(g, blocks, lds, X, xs, K, ks, bias, out, os, 0, st, po);
+  else launch_t<BG, PADDED, false, false, POOL>(g, blocks, lds, X, xs, K, ks, bias, out, os, 0, st, po);
 }
 template <int BG, bool PADDED>
 void launch(const ConvGeom &g, unsigned blocks, const float *X, int xs, const float *K, int ks,
@@ -691,31 +768,71 @@ void launch(const ConvGeom &g, unsigned blocks, const float *X, int xs, const fl
 // Conv2D(concat) + bias (+ ReLU) on the bf16 MFMAs; -1 (nothing launched)
 // for shapes outside its addressing limits.  KCNN_IGEMM_X6=0 disables it
 // (the fp32-MFMA conv_igemm2_kernel then runs).
-int kcnn_conv_igemm_x6(const ConvGeom &g, const float *X, int xs, const float *K, int ks,
-                       const float *bias, float *out, int os, int relu, hipStream_t st) {
+// Blocks of kcnn_conv_igemm_x6 for g, 0 when the shape is outside its limits.
+static unsigned igemm_x6_blocks(const ConvGeom &g, int xs, int ks) {
   static const int use = [] {
     const char *e = getenv("KCNN_IGEMM_X6");
     return e && *e ? atoi(e) : 1;
   }();
-  if (!use || g.M <= 0 || g.G <= 0 || g.Kdim <= 0) return -1;
+  if (!use || g.M <= 0 || g.G <= 0 || g.Kdim <= 0) return 0;
   const bool padded = g.pad_h > 0 || g.pad_w > 0;
-  if (padded && g.kh * g.kw > 31) return -1;
+  if (padded && g.kh * g.kw > 31) return 0;
   if ((int64_t)g.R * xs * 4 >= (int64_t)kOob || (int64_t)g.C * g.HW * 4 >= (int64_t)kOob)
-    return -1;
+    return 0;
   if ((int64_t)(g.Kdim + BK) * ks * 4 >= (int64_t)kOob || g.M >= ((int64_t)1 << 31) ||
       (int64_t)g.G * g.P >= ((int64_t)1 << 31))
-    return -1;
+    return 0;
   const int BG = g.G <= 128 ? 128 : 256;
   const int64_t tiles = (int64_t)((g.G + BG - 1) / BG) * ((g.M + (384 - BG) - 1) / (384 - BG));
-  if (tiles >= ((int64_t)1 << 31)) return -1;
-  const unsigned nb = (unsigned)tiles;
-  if (BG == 128) {
+  if (tiles >= ((int64_t)1 << 31)) return 0;
+  return (unsigned)tiles;
+}
+
+int kcnn_conv_igemm_x6(const ConvGeom &g, const float *X, int xs, const float *K, int ks,
+                       const float *bias, float *out, int os, int relu, hipStream_t st) {
+  const unsigned nb = igemm_x6_blocks(g, xs, ks);
+  if (nb == 0) return -1;
+  const bool padded = g.pad_h > 0 || g.pad_w > 0;
+  if (g.G <= 128) {
     if (padded) launch<128, true>(g, nb, X, xs, K, ks, bias, out, os, relu, st);
     else launch<128, false>(g, nb, X, xs, K, ks, bias, out, os, relu, st);
   } else {
     if (padded) launch<256, true>(g, nb, X, xs, K, ks, bias, out, os, relu, st);
     else launch<256, false>(g, nb, X, xs, K, ks, bias, out, os, relu, st);
   }
+  return (int)hipGetLastError();
+}
+
+// The same convolution (bit for bit: the same kernel, tiles and K order) with
+// the following ph x pw x pc Maxpool in its epilogue, for windows of two
+// consecutive map positions: ph x pw = 2 x 1 (oh even) or 1 x 2 (oh = 1, ow
+// even), pc in {1, 2, 4} dividing G.  out (Y) nullable; mask 16-bit, ms in
+// elements.  -1 (nothing launched) otherwise.
+int kcnn_conv_igemm_x6_pool(const ConvGeom &g, const float *X, int xs, const float *K,
+                            int ks, const float *bias, float *out, int os, float *pool,
+                            int ps, unsigned short *mask, int ms, int ph, int pw, int pc,
+                            hipStream_t st) {
+  const bool win = (ph == 2 && pw == 1 && g.oh % 2 == 0) ||
+                   (ph == 1 && pw == 2 && g.oh == 1 && g.ow % 2 == 0);
+  if (!win || !(pc == 1 || pc == 2 || pc == 4) || g.G % pc != 0 || stagger()) return -1;
+  const unsigned nb = igemm_x6_blocks(g, xs, ks);
+  if (nb == 0) return -1;
+  const PoolOut po{pool, ps, mask, ms};
+  const bool padded = g.pad_h > 0 || g.pad_w > 0;
+#define KCNN_IGP(BG_, PAD_)                                                                 \
+  do {                                                                                      \
+    if (pc == 4) launch_pool<BG_, PAD_, 1>(g, nb, X, xs, K, ks, bias, out, os, po, st);     \
+    else if (pc == 1) launch_pool<BG_, PAD_, 2>(g, nb, X, xs, K, ks, bias, out, os, po, st); \
+    else launch_pool<BG_, PAD_, 3>(g, nb, X, xs, K, ks, bias, out, os, po, st);             \
+  } while (0)
+  if (g.G <= 128) {
+    if (padded) KCNN_IGP(128, true);
+    else KCNN_IGP(128, false);
+  } else {
+    if (padded) KCNN_IGP(256, true);
+    else KCNN_IGP(256, false);
+  }
+#undef KCNN_IGP
   return (int)hipGetLastError();
 }
 

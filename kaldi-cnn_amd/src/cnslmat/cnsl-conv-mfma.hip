@@ -1046,10 +1046,24 @@ int hipF_conv2d_maxpool3d(const float *in, MatrixDim in_dim, int in_height,
     return (int)hipErrorInvalidValue;
   if (g.R == 0) return 0;
   if (g.M >= ((int64_t)1 << 31)) return -1;
-  return kcnn_conv_fwd_frame_pool(g, in, in_dim.stride, kernel, kernel_dim.stride, bias,
-                                  out, out_dim.stride, pool, pool_dim.stride,
-                                  reinterpret_cast<unsigned char *>(mask), mask_stride, pc,
-                                  kcnn::as_stream(stream), ph, pw) == 0
+  hipStream_t st = kcnn::as_stream(stream);
+  if (kcnn_conv_fwd_frame_pool(g, in, in_dim.stride, kernel, kernel_dim.stride, bias, out,
+                               out_dim.stride, pool, pool_dim.stride,
+                               reinterpret_cast<unsigned char *>(mask), mask_stride, pc, st,
+                               ph, pw) == 0)
+    return 0;
+  // long kernels: the implicit GEMM with the pool in its epilogue, for the
+  // shapes whose unfused convolution is that same kernel (conv2d_impl: not
+  // in the frame kernels' range, not the small-filter direct kernel)
+  // (KCNN_IGEMM_POOL=0: unfused)
+  static const int igpool = [] {
+    const char *e = getenv("KCNN_IGEMM_POOL");
+    return e && *e ? atoi(e) : 1;
+  }();
+  if (!igpool || (g.Kdim <= 64 && g.P >= 16) || use_direct(g, 1)) return -1;
+  return kcnn_conv_igemm_x6_pool(g, in, in_dim.stride, kernel, kernel_dim.stride, bias, out,
+                                 out_dim.stride, pool, pool_dim.stride, mask, mask_stride, ph,
+                                 pw, pc, st) == 0
              ? 0
              : -1;
 }

@@ -84,6 +84,12 @@ int kcnn_conv_bwd_x6(const kcnn::ConvGeom &g, const float *X, int xs, const floa
 int kcnn_conv_igemm_x6(const kcnn::ConvGeom &g, const float *X, int xs, const float *K,
                        int ks, const float *bias, float *out, int os, int relu,
                        hipStream_t st);
+// kcnn_conv_igemm_x6 with a ph x pw x pc Maxpool of two-position windows in
+// its epilogue (pooled output and 16-bit routing mask); -1 when not covered.
+int kcnn_conv_igemm_x6_pool(const kcnn::ConvGeom &g, const float *X, int xs, const float *K,
+                            int ks, const float *bias, float *out, int os, float *pool,
+                            int ps, unsigned short *mask, int ms, int ph, int pw, int pc,
+                            hipStream_t st);
 // Weight gradient on the bf16 MFMAs (cnsl-conv-igemm-x6.hip): the split
 // plan (false = not eligible), then partials [S][G*Kdim + G] into ws for
 // kcnn_reduce_splits_wgrad.

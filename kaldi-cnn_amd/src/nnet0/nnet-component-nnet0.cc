@@ -251,7 +251,10 @@ bool ConvolutionComponent::PropagateMaxpool(const CuMatrixBase<BaseFloat> &in,
                  in_pad_width_, linear_params_.Data(), linear_params_.Dim(), kernel_height_,
                  kernel_width_, group_, bias_params_.Data(), store_out ? out->Data() : NULL,
                  out->Dim(), pool_out->Data(), pool_out->Dim(), mask, mask_stride, pc, S());
-  if (rc < 0) return false;
+  if (rc < 0) {
+    prof.Cancel();  // declined: nothing launched
+    return false;
+  }
   CNSL_SAFE_CALL(rc);
   return true;
 }

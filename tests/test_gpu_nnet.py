@@ -49,7 +49,13 @@ STACKS = {
     "win_2x2x2": (9, 8, 2, 2, 1, 64, 2, 8, 0, 0, 2, 2),
     "win_2x1x8_pad": (6, 6, 1, 3, 3, 32, 8, 8, 1, 1, 2, 1),
     "win_2x1x4_G96": (10, 6, 2, 3, 2, 96, 4, 8, 0, 0, 2, 1),
+    # long kernels (implicit GEMM, the pool in its epilogue): c5's C3 -> P2
+    # shape class, nnet.config's conv4 -> Maxpool(1x2x1), and pc = 2
+    "long_2x1x4_pad": (8, 9, 16, 3, 3, 256, 4, 8, 1, 1, 2, 1),
+    "long_1x2x1": (1, 14, 32, 1, 3, 64, 1, 8, 0, 0, 1, 2),
+    "long_2x1x2_G96": (6, 5, 8, 3, 3, 96, 2, 8, 0, 0, 2, 1),
 }
+LONG_POOLED = ["long_2x1x4_pad", "long_1x2x1", "long_2x1x2_G96"]
 
 
 def build(kc, cfg, seed, ties=False):
@@ -112,7 +118,7 @@ def test_fusion_is_exact(kc, name, ties):
         assert_same(u, v, f"{name} param {k}")
 
 
-@pytest.mark.parametrize("name", ["c2", "c5_P1_3x1x4"])
+@pytest.mark.parametrize("name", ["c2", "c5_P1_3x1x4", "long_2x1x4_pad", "long_1x2x1"])
 def test_fusion_storing_conv_output(kc, name):
     """Mode 2 stores Y in the fused pass; mode 1 recomputes it on request."""
     a = run(kc, STACKS[name], fused=2)
@@ -182,7 +188,8 @@ def test_pooled_backward_path(kc, name, pooled):
     assert (after > before) == pooled
 
 
-@pytest.mark.parametrize("name", ["c2", "c5_P1_3x1x4", "win_2x1x8_pad", "win_2x1x4_G96"])
+@pytest.mark.parametrize("name", ["c2", "c5_P1_3x1x4", "win_2x1x8_pad", "win_2x1x4_G96"] +
+                         LONG_POOLED)
 @pytest.mark.parametrize("ties", [False, True])
 def test_fused_pool_matches_oracle(kc, name, ties):
     cfg = STACKS[name]
@@ -197,6 +204,24 @@ def test_fused_pool_matches_oracle(kc, name, ties):
                 "mask-routed Maxpool_backprop")
     if ties and qh * qw == 1:  # every map of a group is a maximum: all get the derivative
         assert (derivs[1] != 0).mean() > 0.99 * (dp != 0).mean()
+
+
+@pytest.mark.parametrize("name,fused", [("c2", True), ("c5_P1_3x1x4", True),
+                                        ("long_2x1x4_pad", True), ("long_1x2x1", True),
+                                        ("long_2x1x2_G96", True), ("pc3_unfused", False)])
+def test_fused_forward_path(kc, name, fused):
+    """The conv + pool forward runs as one pass (PropagateMaxpool) for the
+    frame kernels' pools and for two-position windows after long kernels
+    (the implicit GEMM's pooled epilogue); other pools run unfused."""
+    key = "ConvolutionComponent::PropagateMaxpool"
+    kc.set_profiling(True)
+    try:
+        before = _calls(kc, key)
+        run(kc, STACKS[name], fused=1)
+        after = _calls(kc, key)
+    finally:
+        kc.set_profiling(False)
+    assert (after > before) == fused
 
 
 # Conv -> RectifiedLinearComponent: fusion mode 1 runs the ReLU in the conv's

@@ -224,7 +224,9 @@ __global__ __launch_bounds__(256) void conv_fwd_slab_kernel(
 // mask[n][j*P + q] bit c = (Y[PC*j + c][q] == pool value) that the pool's
 // Backprop (A.9) would recompute from Y.
 // PC == -1: a 3-D window (ph x pw x pc, runtime; pc divides 32) pooled from
-// the same slab, with a 16-bit mask (bit c*pw*ph + w*ph + h).
+// the same slab, with a 16-bit mask (bit c*pw*ph + w*ph + h); PC == -3 the
+// same for the 3 x 1 x 4 window (c5's P1) fixed at compile time, so the
+// window's 12 values are read once into registers.
 // X6: the products on the bf16 matrix cores (x6-util.h).  KS is then the
 // number of k16 steps; A = W^T split into its three bf16 planes once per
 // kernel (4 groups x KS x 3 fragments in VGPRs), with the bias as row k =
@@ -507,28 +509,46 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
         for (int e = tid_f; e < cnt; e += 256) dst[e] = T[e];
       }
       if constexpr (PC < 0) {  // 3-D window; rows % pc == 0 (host check)
-        const int cnt_p = rows / pw3.pc * pw3.OP;
-        const int64_t pb = (int64_t)(gb * 32 / pw3.pc) * pw3.OP;
+        constexpr int CPH = PC == -3 ? 3 : 0, CPW = PC == -3 ? 1 : 0, CPC = PC == -3 ? 4 : 0;
+        const int wph = CPH ? CPH : pw3.ph, wpw = CPW ? CPW : pw3.pw, wpc = CPC ? CPC : pw3.pc;
+        const int cnt_p = rows / wpc * pw3.OP;
+        const int64_t pb = (int64_t)(gb * 32 / wpc) * pw3.OP;
         float *pd = pool + (int64_t)n * ps + pb;
         unsigned short *md = reinterpret_cast<unsigned short *>(mask) + (int64_t)n * ms + pb;
         for (int e = tid_f; e < cnt_p; e += 256) {
           uint32_t j, q, wi, hi;
           pw3.div_OP.divmod((uint32_t)e, j, q);
           pw3.div_oh2.divmod(q, wi, hi);
-          const float *t = T + (int)j * pw3.pc * g.P + (int)wi * pw3.pw * g.oh + (int)hi * pw3.ph;
+          const float *t = T + (int)j * wpc * g.P + (int)wi * wpw * g.oh + (int)hi * wph;
           float val = -1e20f;  // A.8: c, then w, then h
-          for (int c = 0; c < pw3.pc; c++)
-            for (int w = 0; w < pw3.pw; w++)
-              for (int h = 0; h < pw3.ph; h++) {
-                const float v = t[c * g.P + w * g.oh + h];
-                if (val < v) val = v;
-              }
           unsigned m = 0;
-          int bit = 0;
-          for (int c = 0; c < pw3.pc; c++)
-            for (int w = 0; w < pw3.pw; w++)
-              for (int h = 0; h < pw3.ph; h++, bit++)
-                m |= (t[c * g.P + w * g.oh + h] == val ? 1u : 0u) << bit;
+          if constexpr (CPH > 0) {
+            float v[CPC * CPW * CPH];
+#pragma unroll
+            for (int c = 0; c < CPC; c++)
+#pragma unroll
+              for (int w = 0; w < CPW; w++)
+#pragma unroll
+                for (int h = 0; h < CPH; h++)
+                  v[(c * CPW + w) * CPH + h] = t[c * g.P + w * g.oh + h];
+#pragma unroll
+            for (int b = 0; b < CPC * CPW * CPH; b++)
+              if (val < v[b]) val = v[b];
+#pragma unroll
+            for (int b = 0; b < CPC * CPW * CPH; b++) m |= (v[b] == val ? 1u : 0u) << b;
+          } else {
+            for (int c = 0; c < wpc; c++)
+              for (int w = 0; w < wpw; w++)
+                for (int h = 0; h < wph; h++) {
+                  const float v = t[c * g.P + w * g.oh + h];
+                  if (val < v) val = v;
+                }
+            int bit = 0;
+            for (int c = 0; c < wpc; c++)
+              for (int w = 0; w < wpw; w++)
+                for (int h = 0; h < wph; h++, bit++)
+                  m |= (t[c * g.P + w * g.oh + h] == val ? 1u : 0u) << bit;
+          }
           pd[e] = val;
           md[e] = (unsigned short)m;
         }
@@ -1607,7 +1627,9 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
     else if (ksn <= 12) KCNN_FWD_POOL(12, PC_);   \
     else KCNN_FWD_POOL(16, PC_);                  \
   } while (0)
-  if (win3) KCNN_FWD_POOL_KS(-1);
+  static const int win_ct = env_int("KCNN_FWD_WIN_CT", 1);  // 0: the runtime window
+  if (win3 && win_ct && ph == 3 && pw == 1 && pc == 4) KCNN_FWD_POOL_KS(-3);
+  else if (win3) KCNN_FWD_POOL_KS(-1);
   else if (pc == 2) KCNN_FWD_POOL_KS(2);
   else if (pc == 4) KCNN_FWD_POOL_KS(4);
   else KCNN_FWD_POOL_KS(8);

@@ -284,6 +284,31 @@ def test_fc_component(kc, path, I, Od, N):
     assert_bound(host(comp.BiasParams()), of.b, np.abs(b0) + lr * gb_s, what="FC b'")
 
 
+@pytest.mark.parametrize("I,Od,N", [(512, 256, 2048), (300, 70, 33), (1000, 130, 4100)])
+def test_fc_update_equals_gradient_then_apply(kc, I, Od, N):
+    """The update inside Backprop (UpdateSimple, nnet-component-nnet0.cc:1133-1150)
+    must give the bits of ComputeGradient + ApplyGradient, the split the DP
+    step uses.  The first and last shapes split the gradient GEMM's K
+    (N >= 2048 frames), the second does not."""
+    line = (f"FullyConnectedComponent input-dim={I} output-dim={Od} learning-rate=0.02 "
+            f"param-stddev=0.01 bias-stddev=1 weight-decay=0.0002 momentum=0.9")
+    r = rng(9)
+    params = [randn(r, (Od, I), 0.05), randn(r, (Od,), 0.5), randn(r, (Od, I), 0.01)]
+    x, dy = dev(randn(r, (N, I))), dev(randn(r, (N, Od), 0.1))
+    out = []
+    for fused in (True, False):
+        comp = kc.Component.NewFromString(line)
+        for which, v in enumerate(params):
+            comp.SetParam(which, dev(v))
+        if fused:
+            comp.Backprop(x, None, dy, update=True)
+        else:
+            comp.ApplyGradient(comp.ComputeGradient(x, dy), N)
+        out.append([host(comp.GetParam(w)) for w in range(3)])
+    for k in range(3):
+        assert_same(out[0][k], out[1][k], f"FC param {k}")
+
+
 @pytest.mark.parametrize("binary", [True, False])
 def test_read_write_roundtrip(kc, tmp_path, binary):
     comps = [

@@ -500,6 +500,13 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
       // output and the routing mask, Y itself is never stored
       float *dst = out ? out + (int64_t)n * os + (int64_t)gb * 32 * g.P : nullptr;
       if (dst == nullptr) {
+      } else if (vec_ok & 2) {  // streaming stores: Y is not re-read here
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const f4 *src4 = reinterpret_cast<const f4 *>(T);
+        f4 *dst4 = reinterpret_cast<f4 *>(dst);
+        for (int e = tid_f; e < (cnt >> 2); e += 256)
+          __builtin_nontemporal_store(src4[e], dst4 + e);
+        for (int e = (cnt & ~3) + tid_f; e < cnt; e += 256) dst[e] = T[e];
       } else if (vec_ok) {
         const float4 *src4 = reinterpret_cast<const float4 *>(T);
         float4 *dst4 = reinterpret_cast<float4 *>(dst);
@@ -1484,6 +1491,15 @@ static int env_int(const char *name, int dflt) {
   return s && *s ? atoi(s) : dflt;
 }
 
+// The fused conv + pool forward's Y stores (fusion mode 2, Y kept for later)
+// as streaming stores (vec_ok bit 1): c2 213 -> 206 us.  Not for the unfused
+// conv, whose Y the pool reads right after (155 -> 181 us there).
+// KCNN_CONV_Y_NT=0 plain stores
+static int y_nt() {
+  static const int v = env_int("KCNN_CONV_Y_NT", 1) ? 2 : 0;
+  return v;
+}
+
 int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
                         const float *K, int ks, const float *bias, float *out,
                         int os, hipStream_t st) {
@@ -1606,7 +1622,7 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
   const size_t lds = (size_t)((32 * g.P + 3) & ~3) * 4 + 128 * 4 + 32 * 8 +
                      (size_t)g.C * g.HW * 4;
   if (lds > (size_t)kFrameLdsMax) return -1;
-  const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0);
+  const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0) ? 1 | y_nt() : 0;
   const int ksn = (g.Kdim + 1) / 2;
   static const int grid_env = env_int("KCNN_FWD_GRID", 0);  // timing experiments
   static const int use_x6 = env_int("KCNN_FWD_X6", 1);

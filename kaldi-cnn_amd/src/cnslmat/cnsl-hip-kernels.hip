@@ -385,7 +385,7 @@ __global__ __launch_bounds__(256) void maxpool_group_prop_kernel(
 // kPoolDirectOut * PC loads of a thread are issued before the first max.
 constexpr int kPoolDirectOut = 8;
 
-template <int PC>
+template <int PC, bool NT = false>
 __global__ __launch_bounds__(256) void maxpool_direct_prop_kernel(
     const float *__restrict__ src, int64_t ss, float *__restrict__ dst,
     int64_t ds, uint32_t total, FastDiv div_cols, FastDiv div_plane, int plane) {
@@ -401,7 +401,8 @@ __global__ __launch_bounds__(256) void maxpool_direct_prop_kernel(
     div_plane.divmod(j, k, q);
     const float *m = src + (int64_t)row * ss + (int64_t)k * PC * plane + q;
 #pragma unroll
-    for (int c = 0; c < PC; c++) v[t][c] = m[c * plane];
+    for (int c = 0; c < PC; c++)
+      v[t][c] = NT ? __builtin_nontemporal_load(m + c * plane) : m[c * plane];
     out[t] = e < total ? (int64_t)row * ds + j : -1;
   }
 #pragma unroll
@@ -410,13 +411,16 @@ __global__ __launch_bounds__(256) void maxpool_direct_prop_kernel(
 #pragma unroll
     for (int c = 0; c < PC; c++)
       if (val < v[t][c]) val = v[t][c];
-    if (out[t] >= 0) dst[out[t]] = val;
+    if (out[t] >= 0) {
+      if (NT) __builtin_nontemporal_store(val, dst + out[t]);
+      else dst[out[t]] = val;
+    }
   }
 }
 
 // Direct channel-group backprop (write_all semantics, like the group kernel
 // below): output e routes dP[e] to every input of its window equal to P[e].
-template <int PC>
+template <int PC, bool NT = false>
 __global__ __launch_bounds__(256) void maxpool_direct_backprop_kernel(
     const float *__restrict__ x, int64_t xs, const float *__restrict__ y,
     int64_t ys, const float *__restrict__ dy, int64_t dys,
@@ -437,17 +441,23 @@ __global__ __launch_bounds__(256) void maxpool_direct_backprop_kernel(
     const int64_t w = (int64_t)k * PC * plane + q;
     const float *m = x + (int64_t)row * xs + w;
 #pragma unroll
-    for (int c = 0; c < PC; c++) v[t][c] = m[c * plane];
-    pv[t] = y[(int64_t)row * ys + j];
-    dv[t] = dy[(int64_t)row * dys + j];  // own stride (B14)
+    for (int c = 0; c < PC; c++)
+      v[t][c] = NT ? __builtin_nontemporal_load(m + c * plane) : m[c * plane];
+    pv[t] = NT ? __builtin_nontemporal_load(y + (int64_t)row * ys + j)
+               : y[(int64_t)row * ys + j];
+    dv[t] = NT ? __builtin_nontemporal_load(dy + (int64_t)row * dys + j)
+               : dy[(int64_t)row * dys + j];  // own stride (B14)
     in_off[t] = (int64_t)row * dxs + w;
   }
 #pragma unroll
   for (int t = 0; t < kPoolDirectOut; t++) {
     if (!ok[t]) continue;
 #pragma unroll
-    for (int c = 0; c < PC; c++)
-      dx[in_off[t] + c * plane] = v[t][c] == pv[t] ? dv[t] : 0.0f;
+    for (int c = 0; c < PC; c++) {
+      const float r = v[t][c] == pv[t] ? dv[t] : 0.0f;
+      if (NT) __builtin_nontemporal_store(r, dx + in_off[t] + c * plane);
+      else dx[in_off[t] + c * plane] = r;
+    }
   }
 }
 
@@ -1189,6 +1199,18 @@ int hipF_copy_rows_at(const float *src, MatrixDim src_dim, float *dest,
   return launch_elem2d(src_dim.rows, src_dim.cols, f, kcnn::as_stream(stream));
 }
 
+// Streaming (nontemporal) loads and stores in the direct pool kernels.
+// KCNN_POOL_NT: bit 1 forward (default on: Y read once, P written once; c2
+// in the unfused step 225 -> 177-197 us, 52.8 % -> 60-67 % of HBM), bit 0
+// backprop (default off: 355 -> 461 us measured).
+static int pool_nt() {
+  static const int v = [] {
+    const char *e = getenv("KCNN_POOL_NT");
+    return e && *e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
 int hipF_maxpool_prop(const float *src, MatrixDim src_dim, float *pool,
                       MatrixDim pool_dim, int in_height, int in_width,
                       int pool_height_dim, int pool_width_dim,
@@ -1203,7 +1225,9 @@ int hipF_maxpool_prop(const float *src, MatrixDim src_dim, float *pool,
     if (nout == 0) return 0;
     const unsigned blocks =
         (unsigned)((nout + 256 * kPoolDirectOut - 1) / (256 * kPoolDirectOut));
-    auto kern = pool_channel_dim == 4   ? maxpool_direct_prop_kernel<4>
+    static const int nt = pool_nt();
+    auto kern = pool_channel_dim == 4   ? (nt >= 2 ? maxpool_direct_prop_kernel<4, true>
+                                              : maxpool_direct_prop_kernel<4>)
                 : pool_channel_dim == 3 ? maxpool_direct_prop_kernel<3>
                                         : maxpool_direct_prop_kernel<2>;
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, kcnn::as_stream(stream),
@@ -1293,7 +1317,9 @@ int hipF_maxpool_backprop(const float *in_val, MatrixDim in_val_dim,
     if (nout == 0) return 0;
     const unsigned blocks =
         (unsigned)((nout + 256 * kPoolDirectOut - 1) / (256 * kPoolDirectOut));
-    auto kern = pool_channel_dim == 4   ? maxpool_direct_backprop_kernel<4>
+    static const int nt = pool_nt();
+    auto kern = pool_channel_dim == 4   ? (nt == 1 || nt == 3 ? maxpool_direct_backprop_kernel<4, true>
+                                                              : maxpool_direct_backprop_kernel<4>)
                 : pool_channel_dim == 3 ? maxpool_direct_backprop_kernel<3>
                                         : maxpool_direct_backprop_kernel<2>;
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, st, in_val, (int64_t)in_val_dim.stride, out_val,

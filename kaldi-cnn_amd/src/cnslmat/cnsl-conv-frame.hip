@@ -1471,7 +1471,9 @@ int fwd_regs_blocks_per_cu(size_t lds) {
 // the fp32 kernel holds three, and the kernel is bound by its gather and
 // pool/store epilogue more than by its MFMAs: c2 fused forward + pool 137 ->
 // 132 us, but c5 C1 (G = 256 in two chunks, 3-D pool from LDS) 0.52 ->
-// 0.62 ms, so chunked layers keep the fp32 MFMA.  The rule depends on the
+// 0.62 ms with the runtime window, and the same speed (c5 447.0 k vs 446.5 k
+// frames/s) once the 3 x 1 x 4 window is compiled in, so chunked layers keep
+// the fp32 MFMA.  The rule depends on the
 // layer's shape only, so a fused and an unfused run of a layer use the same
 // arithmetic (bitwise-equal outputs).  KCNN_FWD_X6=0 keeps the fp32 MFMA.
 bool fwd_x6_ok(const ConvGeom &g, int use) {

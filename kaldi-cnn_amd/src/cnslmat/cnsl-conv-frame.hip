@@ -300,6 +300,24 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
   }
   const int CHW = g.C * g.HW;
   const int ntile = (g.P + 31) >> 5;
+  // X6: every aligned group of 8 taps one run of consecutive map offsets
+  // (c2's 8 x 1 kernel: taps c*8 + ky at c*HW + ky)?  Then a group's 8 values
+  // are read at one offset + e, without the per-tap table reads
+  bool run8 = false;
+  if constexpr (X6) {
+    run8 = !(dbg & 64);
+    for (int k = 0; k + 1 < g.Kdim && run8; k++) {
+      if ((k + 1) % 8 == 0) continue;
+      uint32_t c0, r0, x0, y0, c1, r1, x1, y1;
+      g.div_khkw.divmod((uint32_t)k, c0, r0);
+      g.div_kh.divmod(r0, x0, y0);
+      g.div_khkw.divmod((uint32_t)(k + 1), c1, r1);
+      g.div_kh.divmod(r1, x1, y1);
+      const int o0 = (int)c0 * g.HW + (int)x0 * g.H + (int)y0;
+      const int o1 = (int)c1 * g.HW + (int)x1 * g.H + (int)y1;
+      run8 = o1 == o0 + 1;
+    }
+  }
 #ifdef KCNN_PHASE_TIMING  // per-phase s_memtime totals of block 0 (dbg & 16)
   long long tm[6] = {0, 0, 0, 0, 0, 0};
   long long tprev = clock64();
@@ -351,11 +369,21 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
 #pragma unroll
         for (int s = 0; s < KS; s++) {
           float v[8];
+          const int k0 = 16 * s + 8 * h_f;
+          if (run8) {  // uniform
+            const float *xr = Xs + koff[k0].x + pb;
 #pragma unroll
-          for (int e = 0; e < 8; e++) {
-            const int k = 16 * s + 8 * h_f + e;
-            const float xval = Xs[koff[k].x + pb];
-            v[e] = k < g.Kdim ? xval : (k == g.Kdim ? 1.0f : 0.0f);
+            for (int e = 0; e < 8; e++) {
+              const float xval = xr[e];
+              v[e] = k0 + e < g.Kdim ? xval : (k0 + e == g.Kdim ? 1.0f : 0.0f);
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+              const int k = k0 + e;
+              const float xval = Xs[koff[k].x + pb];
+              v[e] = k < g.Kdim ? xval : (k == g.Kdim ? 1.0f : 0.0f);
+            }
           }
           x6::split8(v, bx6[t][s][0], bx6[t][s][1], bx6[t][s][2]);
         }

@@ -674,7 +674,10 @@ bool ConvolutionComponent::BackpropPooled(const CuMatrixBase<BaseFloat> &in_valu
       grad ? NULL : dynamic_cast<ConvolutionComponent *>(to_update_in);
   if (LiteralPath() || mask == NULL || !pool.FoldsIntoConvBackprop()) return false;
   int32 pc = pool.FusableChannelPool(), ph = 1, pw = 1;
-  if (pc == 0) KALDI_ASSERT(pool.FusableWindow3D(&ph, &pw, &pc));
+  if (pc == 0) {
+    const bool win3 = pool.FusableWindow3D(&ph, &pw, &pc);
+    KALDI_ASSERT(win3);
+  }
   // Backprop without in_deriv: nothing to do, or (with an update) Update in
   // the unfused path, whose gradient kernel sums in another order: keep its bits
   if (grad == NULL && in_deriv == NULL) return false;

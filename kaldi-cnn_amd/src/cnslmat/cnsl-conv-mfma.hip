@@ -759,7 +759,12 @@ __global__ __launch_bounds__(64) void conv_col2im_plane_kernel(
   for (int u = blockIdx.x; u < units; u += gridDim.x) {
     const int n = u / g.C, c = u - n * g.C;
     const float *src = Z + (int64_t)n * zs + (int64_t)c * U;
-    if (vec) {
+    if (vec & 2) {  // streaming loads: Z was just written and is read once
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      for (int i = lane; i < U / 4; i += 64)
+        reinterpret_cast<f4 *>(zp)[i] =
+            __builtin_nontemporal_load(reinterpret_cast<const f4 *>(src) + i);
+    } else if (vec) {
       for (int i = lane; i < U / 4; i += 64)
         reinterpret_cast<float4 *>(zp)[i] = reinterpret_cast<const float4 *>(src)[i];
     } else {
@@ -973,9 +978,13 @@ int dgrad_scatter(const ConvGeom &g, const float *dY, MatrixDim dyd,
   if (zlds >= 1024 && zlds <= 32768) {
     const int units = g.R * g.C;
     const bool vec = (g.kh * g.kw * g.P) % 4 == 0 && zd.stride % 4 == 0;
+    static const int nt = [] {
+      const char *e = getenv("KCNN_COL2IM_NT");
+      return e && *e ? atoi(e) : 1;
+    }();
     hipLaunchKernelGGL(conv_col2im_plane_kernel,
                        dim3((unsigned)(units < 256 * 24 ? units : 256 * 24)), dim3(64), zlds,
-                       st, g, z, zd.stride, dX, dxd.stride, vec ? 1 : 0);
+                       st, g, z, zd.stride, dX, dxd.stride, vec ? (nt ? 3 : 1) : 0);
     return kcnn::launch_status();
   }
   const int64_t ne = (int64_t)g.R * g.C * g.HW;

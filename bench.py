@@ -151,13 +151,17 @@ def parse_profile(text):
 
 
 def cpu_baseline(frames_hint, budget_s=12.0):
-    """The CPU oracle (restated reference CPU path) on a bounded sample."""
+    """The CPU oracle (restated reference CPU path): one full c2 step of
+    `frames_hint` frames (at most 4096) on this GPU job's CPU share, and a
+    bounded sample on one thread."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    # 16 threads: this GPU's share of the box's host CPUs (the box exposes
-    # every thread of a shared host, nproc = 256, but a one-GPU job is sized to
-    # 16); the label says so rather than calling it "all cores"
+    # 16 threads: this GPU's share of the box's host CPUs.  The box exposes
+    # every thread of a shared 8-GPU host (nproc = 256 on a 64-core EPYC), but
+    # a one-GPU job is allotted 16 (OMP_NUM_THREADS there); running the oracle
+    # on all 64 cores would take the other GPUs' jobs' CPUs, so the all-cores
+    # figure of SURVEY 8d(ii) is not measured and the label says so
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
@@ -193,7 +197,8 @@ def cpu_baseline(frames_hint, budget_s=12.0):
         n = max(8, (n // 8) * 8)
         return n, one_step(n)
 
-    n, t = sized(budget_s)
+    n = max(8, min(4096, frames_hint))
+    t = one_step(n)
     # also one thread (nnet-train-simple --use-gpu=no)
     O.set_threads(1)
     n1, t1 = sized(budget_s / 2)
@@ -223,7 +228,7 @@ def cpu_baseline(frames_hint, budget_s=12.0):
         pass
     return {"value": round(n / t, 2), "unit": "frames/sec", "cores": threads,
             "kind": "port",
-            "sample": f"{n} frames of the c2 stack, one fwd+bwd+update step, "
+            "sample": f"{n} frames of the c2 stack, one full fwd+bwd+update step, "
                       f"C oracle (oracle/kcnn_oracle.c) with {threads} OpenMP threads",
             "single_thread": {"value": round(n1 / t1, 2), "sample": f"{n1} frames, 1 thread"},
             "c1_forward": {"unit": "frames/sec", "threads_1": c1_1, f"threads_{threads}": c1_n,
@@ -231,7 +236,58 @@ def cpu_baseline(frames_hint, budget_s=12.0):
                                      "best of 3"},
             "host": {"cpu_model": model, "nproc": os.cpu_count(), "affinity": avail,
                      "threads_note": f"{threads} threads = one GPU's share of the box's "
-                                     "host CPUs, not all cores"}}
+                                     "host CPUs (the job's allotment), not all 64 cores"}}
+
+
+def baseline_config(frames_per_gpu, world):
+    """Which BASELINE.json config a c2-stack run is (configs[1..3])."""
+    if frames_per_gpu * world == 131072 and world > 1:
+        return "c4: 131072-frame minibatch sharded over %d GPUs" % world
+    if frames_per_gpu == 65536 and world == 1:
+        return "c3: 65536 frames, 1 GPU"
+    if frames_per_gpu == 16384 and world == 1:
+        return "one rank's shard of c4 (16384 frames), 1 GPU"
+    if frames_per_gpu == 4096:
+        return "c2: 4096-frame batch per GPU (BASELINE metric @%d GPU)" % world
+    return "c2 stack, %d frames per GPU" % frames_per_gpu
+
+
+def dp_report(dist, grads, marks, steps, reps=5):
+    """The data-parallel exchange of the timed (profiled) steps: the time the
+    compute stream waited for the all-reduces at the end of each step (what
+    the overlap did not hide), and the same collectives run alone."""
+    import torch
+    torch.cuda.synchronize()
+    exposed = [b.elapsed_time(e) for (nb, b), (ne, e) in zip(marks[0::2], marks[1::2])
+               if nb == "wait_begin" and ne == "wait_end"]
+    bufs = [grads[i] for i in grads.large] + \
+        ([grads.bucket] if grads.bucket is not None else [])
+    dist.barrier()
+    t0 = torch.cuda.Event(enable_timing=True)
+    t1 = torch.cuda.Event(enable_timing=True)
+    for b in bufs:                              # warm the communicator's paths
+        dist.all_reduce(b)
+    torch.cuda.synchronize()
+    t0.record()
+    for _ in range(reps):
+        for b in bufs:
+            dist.all_reduce(b)
+    t1.record()
+    torch.cuda.synchronize()
+    alone = t0.elapsed_time(t1) / reps
+    ranks = torch.ones(1, device="cuda")
+    dist.all_reduce(ranks)
+    exp_ms = sum(exposed) / max(1, len(exposed))
+    return {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+            "ranks_seen": int(ranks.item()),
+            "collectives_per_step": grads.num_collectives(),
+            "allreduce_bytes_per_step": grads.bytes_per_step(),
+            "allreduce_alone_ms_per_step": round(alone, 4),
+            "allreduce_exposed_ms_per_step": round(exp_ms, 4),
+            "overlap_frac": round(1 - exp_ms / alone, 4) if alone > 0 else None,
+            "note": "exposed = stream wait at the end of backprop for the step's "
+                    "all-reduces (rank 0, profiled pass); alone = the same collectives "
+                    "back to back with nothing else running"}
 
 
 def main():
@@ -264,10 +320,14 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     dist = None
     # one process per GPU; --dist-backend gloo rehearses the N > 1 path with
-    # several ranks sharing the GPUs there are (RCCL needs one GPU per rank)
+    # several ranks sharing the GPUs there are (RCCL needs one GPU per rank).
+    # Launched by torch.distributed.run (WORLD_SIZE set) the data-parallel
+    # step runs even at world size 1 (RCCL's own path, a no-op reduction);
+    # plain `python bench.py` is the single-GPU step
+    distributed = "WORLD_SIZE" in os.environ
     device = local_rank % max(1, torch.cuda.device_count()) \
         if args.dist_backend == "gloo" else local_rank
-    if world > 1:
+    if distributed:
         import torch.distributed as dist
         torch.cuda.set_device(device)
         if args.dist_backend == "nccl":
@@ -297,12 +357,22 @@ def main():
     grads = kcnn_dp.gradient_buffers(
         net, lambda n: torch.empty(n, device="cuda"))
 
+    marks = []
+
+    def mark(name):
+        if profiling_dp:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            marks.append((name, e))
+
+    profiling_dp = False
+
     def step():
-        if world == 1:
+        if not dist:
             net.Propagate(x)
             net.Backprop(dy)                     # reference semantics: update in Backprop
             return
-        kcnn_dp.dp_train_step(net, x, dy, grads, dist, B * world)
+        kcnn_dp.dp_train_step(net, x, dy, grads, dist, B * world, mark=mark)
 
     for _ in range(args.warmup):
         step()
@@ -335,7 +405,10 @@ def main():
     # again with hipEvents around every component scope, for the per-kernel
     # times of the roofline
     elapsed, _ = timed(False)
+    profiling_dp = True
     elapsed_prof, prof = timed(True)
+    profiling_dp = False
+    dp = dp_report(dist, grads, marks, args.steps) if dist else None
 
     frames = B * world * args.steps
     value = frames / elapsed
@@ -379,6 +452,8 @@ def main():
                                                     PEAK_BF16_MFMA_TFLOPS, 4) if conv_ms else None},
                 "scopes_ms_per_step": scopes,
             }
+            if dp:
+                result["dp"] = dp
             line = json.dumps(result)
             print(line, flush=True)
             if args.json_out:
@@ -495,6 +570,7 @@ def main():
             "profiled_ms_per_step": round(elapsed_prof / args.steps * 1e3, 4),
             "config": {"workload": "c2: Conv(40x11x3, 8x1, 128) -> Maxpool(1x1x4) -> "
                                    "FC(11616->1024), fwd+bwd+update",
+                       "baseline_config": baseline_config(B, world),
                        "frames_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"dp{world}",
                        "conv_maxpool_fusion": not args.no_fusion,
@@ -502,6 +578,8 @@ def main():
             "roofline": roofline,
             "kernels": kernels,
         }
+        if dp:
+            result["dp"] = dp
         if not args.no_cpu_baseline and world == 1:
             result["cpu_baseline"] = cpu_baseline(B)
         line = json.dumps(result)

@@ -70,6 +70,20 @@ int kcnn_set_fusion(int mode);
  *      kept (cu-gemm-x6.hip); same error bound as sgemm.
  * Env KCNN_GEMM (0/1) sets the initial mode. */
 int kcnn_set_gemm_mode(int mode);
+/* Kernel-family selectors (kaldi-lite/kcnn-knobs.h): each picks
+ * one of two implementations of the same fp32 math, the bf16x6 kernels on
+ * the bf16 matrix cores (default) or the fp32-input MFMA kernels.
+ *   "fwd_x6"   frame-resident conv forward      1 (default) / 0
+ *   "bwd_x6"   fused conv backward              1 (default) / 0
+ *   "igemm_x6" implicit-GEMM forward and dgrad  1 (default) / 0
+ *   "wgrad_x6" long-kernel weight gradient      2 (default, wide) / 1 / 0
+ *   "gemm"     AddMatMat (= kcnn_set_gemm_mode) 1 (default) / 0
+ * The environment variables KCNN_FWD_X6, KCNN_BWD_X6, KCNN_IGEMM_X6,
+ * KCNN_WGRAD_X6 and KCNN_GEMM set the initial values.  Returns nonzero for
+ * an unknown name or value. */
+int kcnn_set_kernel_family(const char *name, int value);
+/* The current value of a selector, or -1 for an unknown name. */
+int kcnn_get_kernel_family(const char *name);
 /* C[m x n] = alpha * op(A) op(B) + beta * C on row-major fp32 matrices,
  * exactly CuMatrixBase::AddMatMat(alpha, A, transA, B, transB, beta) with
  * op(X) = X^T when trans_x (cu-matrix.h, upstream Kaldi). */

@@ -150,11 +150,27 @@ def set_gemm_mode(mode: int):
     check(lib().kcnn_set_gemm_mode(int(mode)))
 
 
+def set_kernel_family(name: str, value: int):
+    """Kernel-family selector (kcnn.h): "fwd_x6", "bwd_x6", "igemm_x6",
+    "wgrad_x6" (2 wide / 1 / 0) or "gemm"; 0 = the fp32-MFMA kernels."""
+    check(lib().kcnn_set_kernel_family(name.encode(), int(value)))
+
+
+def get_kernel_family(name: str) -> int:
+    v = lib().kcnn_get_kernel_family(name.encode())
+    if v < 0:
+        raise KcnnError(f"unknown kernel family {name!r}")
+    return v
+
+
 def gemm(a, b, c, trans_a=False, trans_b=False, alpha=1.0, beta=0.0):
     """c = alpha * op(a) op(b) + beta * c (CuMatrixBase::AddMatMat) on torch
     fp32 device matrices with contiguous rows."""
     m, n = c.shape
-    k = a.shape[0] if trans_a else a.shape[1]
+    am, k = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    bk, bn = (b.shape[1], b.shape[0]) if trans_b else (b.shape[0], b.shape[1])
+    if am != m or bk != k or bn != n:
+        raise KcnnError(f"gemm: op(a) {am}x{k}, op(b) {bk}x{bn} do not make c {m}x{n}")
     for t in (a, b, c):
         dim(t)
     check(lib().kcnn_gemm(int(bool(trans_a)), int(bool(trans_b)), m, n, k,

@@ -205,6 +205,17 @@ int kcnn_set_gemm_mode(int mode) {
   CuDevice::Instantiate().SetGemmMode(mode);
   return 0;
 }
+int kcnn_set_kernel_family(const char *name, int value) {
+  const int f = kcnn::family_by_name(name);
+  if (f < 0) return fail("kcnn_set_kernel_family: unknown family");
+  if (kcnn::set_family(static_cast<kcnn::Family>(f), value) != 0)
+    return fail("kcnn_set_kernel_family: value out of range");
+  return 0;
+}
+int kcnn_get_kernel_family(const char *name) {
+  const int f = kcnn::family_by_name(name);
+  return f < 0 ? -1 : kcnn::family(static_cast<kcnn::Family>(f));
+}
 int kcnn_gemm(int trans_a, int trans_b, int m, int n, int k, float alpha,
               const float *a, int lda, const float *b, int ldb, float beta,
               float *c, int ldc) {

@@ -1101,8 +1101,7 @@ __global__ __launch_bounds__(BWD_THREADS, 1) void conv_bwd_dma_kernel(
       // explicit vmcnt(0): an LDS-DMA writes LDS, not VGPRs, so no wait of
       // the compiler's covers another wave's reads of it
       KCNN_TMARK(6)
-      x6::wait_dma();
-      __syncthreads();
+      x6::publish_dma();
       KCNN_TMARK(0)
       {
         const int nn = ch + 1 < NCH ? n : n + (int)gridDim.x;
@@ -1516,17 +1515,12 @@ unsigned frame_grid(const ConvGeom &g, int blocks_per_cu) {
 
 }  // namespace
 
-static int env_int(const char *name, int dflt) {
-  const char *s = getenv(name);
-  return s && *s ? atoi(s) : dflt;
-}
-
 // The fused conv + pool forward's Y stores (fusion mode 2, Y kept for later)
 // as streaming stores (vec_ok bit 1): c2 213 -> 206 us.  Not for the unfused
 // conv, whose Y the pool reads right after (155 -> 181 us there).
 // KCNN_CONV_Y_NT=0 plain stores
 static int y_nt() {
-  static const int v = env_int("KCNN_CONV_Y_NT", 1) ? 2 : 0;
+  static const int v = KCNN_KNOB("KCNN_CONV_Y_NT", 1) ? 2 : 0;
   return v;
 }
 
@@ -1546,7 +1540,7 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
     return 0;
   }
   const int Kpad = (g.Kdim + 1) & ~1;
-  static const int variant = env_int("KCNN_FWD_VARIANT", 2);
+  static const int variant = KCNN_KNOB("KCNN_FWD_VARIANT", 2);
   if (variant == 2 && g.Kdim <= 32 && g.G <= 128 && g.P <= 4 * 32 * 3 &&
       g.C * g.HW <= 256 * 8) {
     const size_t lds = (size_t)((32 * g.P + 3) & ~3) * 4 + 128 * 4 + 32 * 8 +
@@ -1554,9 +1548,8 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
     if (lds <= (size_t)kFrameLdsMax) {
       const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0);
       const int ksn = (g.Kdim + 1) / 2;
-      static const int bpc_env = env_int("KCNN_FWD_BPC", 0);  // timing experiments
-      static const int use_x6 = env_int("KCNN_FWD_X6", 1);
-      const bool x6 = fwd_x6_ok(g, use_x6);
+      static const int bpc_env = KCNN_KNOB("KCNN_FWD_BPC", 0);
+      const bool x6 = fwd_x6_ok(g, family(kFamFwdX6));
       const unsigned grid = frame_grid(
           g, bpc_env > 0 ? bpc_env : x6 ? 2 : fwd_regs_blocks_per_cu(lds));
 #define KCNN_FWD_REGS_T(KS_, X6_)                                                       \
@@ -1564,7 +1557,7 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
                      st, g, X, xs, K, ks, bias, out, os, vec_ok, dbg, nullptr, 0, nullptr, \
                      0, PoolWin{})
 #define KCNN_FWD_REGS(KS_) KCNN_FWD_REGS_T(KS_, false)
-      static const int dbg = env_int("KCNN_FWD_DEBUG", 0);
+      static const int dbg = KCNN_KNOB("KCNN_FWD_DEBUG", 0);
       if (x6 && g.Kdim < 16) KCNN_FWD_REGS_T(1, true);
       else if (x6) KCNN_FWD_REGS_T(2, true);
       else if (ksn <= 4) KCNN_FWD_REGS(4);
@@ -1654,12 +1647,11 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
   if (lds > (size_t)kFrameLdsMax) return -1;
   const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0) ? 1 | y_nt() : 0;
   const int ksn = (g.Kdim + 1) / 2;
-  static const int grid_env = env_int("KCNN_FWD_GRID", 0);  // timing experiments
-  static const int use_x6 = env_int("KCNN_FWD_X6", 1);
-  const bool x6 = fwd_x6_ok(g, use_x6);
+  static const int grid_env = KCNN_KNOB("KCNN_FWD_GRID", 0);
+  const bool x6 = fwd_x6_ok(g, family(kFamFwdX6));
   const unsigned grid = grid_env > 0 ? (unsigned)std::min<int64_t>(grid_env, g.R)
                                      : frame_grid(g, x6 ? 2 : fwd_regs_blocks_per_cu(lds));
-  static const int dbg = env_int("KCNN_FWD_DEBUG", 0);
+  static const int dbg = KCNN_KNOB("KCNN_FWD_DEBUG", 0);
 #define KCNN_FWD_POOL_T(KS_, PC_, X6_)                                                      \
   hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_, X6_>), dim3(grid), dim3(256), lds, \
                      st, g, X, xs, K, ks, bias, out, os, vec_ok, dbg, pool, ps, mask, ms, pw3)
@@ -1673,7 +1665,7 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
     else if (ksn <= 12) KCNN_FWD_POOL(12, PC_);   \
     else KCNN_FWD_POOL(16, PC_);                  \
   } while (0)
-  static const int win_ct = env_int("KCNN_FWD_WIN_CT", 1);  // 0: the runtime window
+  static const int win_ct = KCNN_KNOB("KCNN_FWD_WIN_CT", 1);  // 0: the runtime window
   if (win3 && win_ct && ph == 3 && pw == 1 && pc == 4) KCNN_FWD_POOL_KS(-3);
   else if (win3) KCNN_FWD_POOL_KS(-1);
   else if (pc == 2) KCNN_FWD_POOL_KS(2);
@@ -1776,15 +1768,14 @@ static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
                            void *ws, size_t ws_bytes, int dx_acc, hipStream_t st,
                            const unsigned char *pmask = nullptr, int pms = 0, int pc = 0,
                            int ph = 1) {
-  static const int enabled = env_int("KCNN_FUSED_BWD", 1);
-  static const int variant = env_int("KCNN_BWD_VARIANT", 3);  // 1: register-staged
-  static const int bdbg = env_int("KCNN_BWD_DEBUG", 0);
+  static const int enabled = KCNN_KNOB("KCNN_FUSED_BWD", 1);
+  static const int variant = KCNN_KNOB("KCNN_BWD_VARIANT", 3);  // 1: register-staged
+  static const int bdbg = KCNN_KNOB("KCNN_BWD_DEBUG", 0);
   if (!enabled || (dX == nullptr && gW == nullptr)) return -1;
   if (g.Kdim > 31 || g.G % 32 != 0 || g.G > 128 || g.G == 0) return -1;
   // the bf16x6 kernel (cnsl-conv-x6.hip) where the shape allows; KCNN_BWD_X6=0
   // keeps the fp32-MFMA kernels below
-  static const int use_x6 = env_int("KCNN_BWD_X6", 1);
-  if (use_x6 && variant == 3 && kcnn_conv_bwd_x6_eligible(g, dX != nullptr, pc, ph)) {
+  if (family(kFamBwdX6) && variant == 3 && kcnn_conv_bwd_x6_eligible(g, dX != nullptr, pc, ph)) {
     const int S = (int)frame_grid(g, 1);
     const int E = (g.Kdim + 1) * g.G;
     float *part = static_cast<float *>(ws);
@@ -1912,7 +1903,7 @@ int kcnn_conv_bwd_frame(const ConvGeom &g, const float *X, int xs,
     return bwd_frame_chunk(g, X, xs, dY, dys, K, ks, dX, dxs, gW, gws, gb, ws,
                            ws_bytes, 0, st, pmask, pms, pc, ph);
   if (g.G % 32 != 0 || (int64_t)g.G * g.P * 4 % 16 != 0) return -1;
-  static const int variant = env_int("KCNN_BWD_VARIANT", 3);
+  static const int variant = KCNN_KNOB("KCNN_BWD_VARIANT", 3);
   if (variant != 3 && dX != nullptr) return -1;  // chunking needs dX accumulation
   for (int g0 = 0; g0 < g.G; g0 += 128) {
     ConvGeom gc = g;

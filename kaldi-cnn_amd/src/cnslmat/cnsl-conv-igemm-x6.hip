@@ -708,10 +708,7 @@ __global__ __launch_bounds__(NT, 1) void conv_wgrad_x6w_kernel(
 // without SLP vectorization (Makefile) the kernels measure the same or
 // 0.6 % slower with it, so it is off by default.
 int stagger() {
-  static const int v = [] {
-    const char *e = getenv("KCNN_CONV_X6_STAGGER");
-    return e && *e ? atoi(e) : 0;
-  }();
+  static const int v = KCNN_KNOB("KCNN_CONV_X6_STAGGER", 0);
   return v;
 }
 
@@ -720,10 +717,7 @@ constexpr int kImgBytes = 2 * 3 * 384 * ROWB;  // the double-buffered plane imag
 
 // LDS of the tap table for Kdim (0: it does not fit beside the images)
 int tab_bytes(const ConvGeom &g, bool padded) {
-  static const int use = [] {
-    const char *e = getenv("KCNN_IGX6_TAB");
-    return e && *e ? atoi(e) : 1;
-  }();
+  static const int use = KCNN_KNOB("KCNN_IGX6_TAB", 1);
   const int KT = (g.Kdim + BK - 1) / BK * BK;
   const int b = KT * 4 + (padded ? KT : 0);
   return use && kImgBytes + b <= kLdsMax ? b : 0;
@@ -770,11 +764,7 @@ void launch(const ConvGeom &g, unsigned blocks, const float *X, int xs, const fl
 // (the fp32-MFMA conv_igemm2_kernel then runs).
 // Blocks of kcnn_conv_igemm_x6 for g, 0 when the shape is outside its limits.
 static unsigned igemm_x6_blocks(const ConvGeom &g, int xs, int ks) {
-  static const int use = [] {
-    const char *e = getenv("KCNN_IGEMM_X6");
-    return e && *e ? atoi(e) : 1;
-  }();
-  if (!use || g.M <= 0 || g.G <= 0 || g.Kdim <= 0) return 0;
+  if (!family(kFamIgemmX6) || g.M <= 0 || g.G <= 0 || g.Kdim <= 0) return 0;
   const bool padded = g.pad_h > 0 || g.pad_w > 0;
   if (padded && g.kh * g.kw > 31) return 0;
   if ((int64_t)g.R * xs * 4 >= (int64_t)kOob || (int64_t)g.C * g.HW * 4 >= (int64_t)kOob)
@@ -840,13 +830,7 @@ int kcnn_conv_igemm_x6_pool(const ConvGeom &g, const float *X, int xs, const flo
 // sized so the S x tiles blocks fill whole rounds of 256 (one per CU) and an
 // accumulation chain stays within ~16k terms.
 // KCNN_WGRAD_X6: 0 off, 1 the 128-wide k tiles, 2 the wide (256) k tiles
-static int wgrad_x6_mode() {
-  static const int v = [] {
-    const char *e = getenv("KCNN_WGRAD_X6");
-    return e && *e ? atoi(e) : 2;
-  }();
-  return v;
-}
+static int wgrad_x6_mode() { return family(kFamWgradX6); }
 static int wgrad_kwidth() { return wgrad_x6_mode() == 2 ? 256 : 128; }
 
 bool kcnn_conv_wgrad_x6_plan(const ConvGeom &g, int xs, int dys, int &S, int &fps,

@@ -855,10 +855,7 @@ struct Wgrad2Plan {
 // S keeps each accumulator chain <= ~8192 terms (fp32 chain error) and is
 // picked so that the blocks fill whole rounds of 512 (2 per CU).
 bool plan_wgrad2(const ConvGeom &g, int xs, int dys, Wgrad2Plan &pl) {
-  static const int enabled = [] {
-    const char *e = getenv("KCNN_WGRAD2");
-    return e && *e ? atoi(e) : 1;
-  }();
+  static const int enabled = KCNN_KNOB("KCNN_WGRAD2", 1);
   if (!enabled || g.R <= 0 || g.G < 32 || g.P > 96 || g.Kdim < 32)
     return false;
   pl.fpc = g.P <= 16 ? 32 / g.P : 1;
@@ -918,10 +915,7 @@ int launch_wgrad2(const ConvGeom &g, const Wgrad2Plan &pl, const float *X, int x
 // positions than the output (gather waste HW/P; nnet.config layer 1: 840 vs
 // 18, a 47x waste for the flipped-kernel gather).
 bool use_dgrad_scatter(const ConvGeom &g) {
-  static const int enabled = [] {
-    const char *e = getenv("KCNN_DGRAD_SCATTER");
-    return e && *e ? atoi(e) : 1;
-  }();
+  static const int enabled = KCNN_KNOB("KCNN_DGRAD_SCATTER", 1);
   return enabled && g.Kdim >= 32 && 4 * (int64_t)g.HW >= 5 * (int64_t)g.P && g.G >= 16;
 }
 
@@ -978,10 +972,7 @@ int dgrad_scatter(const ConvGeom &g, const float *dY, MatrixDim dyd,
   if (zlds >= 1024 && zlds <= 32768) {
     const int units = g.R * g.C;
     const bool vec = (g.kh * g.kw * g.P) % 4 == 0 && zd.stride % 4 == 0;
-    static const int nt = [] {
-      const char *e = getenv("KCNN_COL2IM_NT");
-      return e && *e ? atoi(e) : 1;
-    }();
+    static const int nt = KCNN_KNOB("KCNN_COL2IM_NT", 1);
     hipLaunchKernelGGL(conv_col2im_plane_kernel,
                        dim3((unsigned)(units < 256 * 24 ? units : 256 * 24)), dim3(64), zlds,
                        st, g, z, zd.stride, dX, dxd.stride, vec ? (nt ? 3 : 1) : 0);
@@ -1065,10 +1056,7 @@ int hipF_conv2d_maxpool3d(const float *in, MatrixDim in_dim, int in_height,
   // shapes whose unfused convolution is that same kernel (conv2d_impl: not
   // in the frame kernels' range, not the small-filter direct kernel)
   // (KCNN_IGEMM_POOL=0: unfused)
-  static const int igpool = [] {
-    const char *e = getenv("KCNN_IGEMM_POOL");
-    return e && *e ? atoi(e) : 1;
-  }();
+  static const int igpool = KCNN_KNOB("KCNN_IGEMM_POOL", 1);
   if (!igpool || (g.Kdim <= 64 && g.P >= 16) || use_direct(g, 1)) return -1;
   return kcnn_conv_igemm_x6_pool(g, in, in_dim.stride, kernel, kernel_dim.stride, bias, out,
                                  out_dim.stride, pool, pool_dim.stride, mask, mask_stride, ph,
@@ -1126,10 +1114,7 @@ static int conv2d_impl(const float *in, MatrixDim in_dim, int in_height, int in_
     return 0;
   // implicit GEMM v2 (fp32 MFMA): concat layout, X addressable with 32-bit
   // offsets, tap masks for padded maps need kh*kw <= 32
-  static const int ig2 = [] {
-    const char *e = getenv("KCNN_IGEMM2");
-    return e && *e ? atoi(e) : 1;
-  }();
+  static const int ig2 = KCNN_KNOB("KCNN_IGEMM2", 1);
   const bool padded = g.pad_h > 0 || g.pad_w > 0;
   const int wgg = g.G > 64 ? 2 : 1;
   if (ig2 && concat && (int64_t)g.R * in_dim.stride * 4 < ((int64_t)1 << 31) &&
@@ -1140,23 +1125,10 @@ static int conv2d_impl(const float *in, MatrixDim in_dim, int in_height, int in_
     dim3 grid2((unsigned)((g.M + bm - 1) / bm), (unsigned)((g.G + bg - 1) / bg));
     // timing experiments (operand loads / LDS stores / traffic switched off):
     // only in the phase-timing build (make timing), never in libkcnn.so
-    static const int ig2timing = [] {
-#ifdef KCNN_PHASE_TIMING
-      const char *e = getenv("KCNN_IGEMM2_DEBUG");
-      return e && *e ? atoi(e) : 0;
-#else
-      return 0;
-#endif
-    }();
+    static const int ig2timing = KCNN_KNOB("KCNN_IGEMM2_DEBUG", 0);
     const int ig2dbg = ig2timing | (relu ? kIg2Relu : 0);
-    static const int ig2bk = [] {
-      const char *e = getenv("KCNN_IGEMM2_BK");
-      return e && *e ? atoi(e) : 16;
-    }();
-    static const int ig2tab = [] {
-      const char *e = getenv("KCNN_IGEMM2_TAB");
-      return e && *e ? atoi(e) : 1;
-    }();
+    static const int ig2bk = KCNN_KNOB("KCNN_IGEMM2_BK", 16);
+    static const int ig2tab = KCNN_KNOB("KCNN_IGEMM2_TAB", 1);
     const bool tab = ig2tab && (g.Kdim + 15) / 16 * 16 <= IG2_KTAB &&
                      (int64_t)g.HW * g.C < (1 << 28) && (!padded || g.kh * g.kw <= 31);
 #define KCNN_IG2(W_, P_)                                                                  \

@@ -389,8 +389,9 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
       for (int t = 0; t < (RD ? MAXT : 1); ++t) zacc[t] = zero16();
 #pragma unroll
       for (int ch = 0; ch < NCH; ch++) {
-        x6::wait_dma();   // this wave's LDS-DMA of the slab (and map) has landed
-        __syncthreads();  // B1: the image's readers are done; last frame's Z is in LDS
+        // B1: the slab (and map) DMA has landed for every wave; the image's
+        // readers are done; last frame's Z is in LDS
+        x6::publish_dma();
         if (ch == 0) {
           if (WG) commit_x();
           if (DX && DEFER && nprev >= 0) col2im(nprev);

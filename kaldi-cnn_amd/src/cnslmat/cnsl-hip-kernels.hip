@@ -942,10 +942,7 @@ __global__ __launch_bounds__(256) void maxpool_group_backprop_kernel(
 
 // KCNN_POOL_DIRECT=0 selects the LDS-staged group forward (A/B measurements).
 bool env_pool_direct() {
-  static const int v = [] {
-    const char *e = getenv("KCNN_POOL_DIRECT");
-    return e ? atoi(e) : 1;
-  }();
+  static const int v = KCNN_KNOB("KCNN_POOL_DIRECT", 1);
   return v != 0;
 }
 
@@ -1112,10 +1109,7 @@ int hipF_maxpool_backprop_mask3d(const unsigned short *mask, int mask_stride,
     return (int)hipErrorInvalidValue;
   const int outh = in_height / ph;
   const int outplane = outh * (in_width / pw);
-  static const int scatter = [] {
-    const char *e = getenv("KCNN_MASK3D_SCATTER");
-    return e && *e ? atoi(e) : 1;
-  }();
+  static const int scatter = KCNN_KNOB("KCNN_MASK3D_SCATTER", 1);
   if (scatter) {
     const int64_t nout = (int64_t)out_deriv_dim.rows * out_deriv_dim.cols;
     if (nout == 0) return 0;
@@ -1204,10 +1198,7 @@ int hipF_copy_rows_at(const float *src, MatrixDim src_dim, float *dest,
 // in the unfused step 225 -> 177-197 us, 52.8 % -> 60-67 % of HBM), bit 0
 // backprop (default off: 355 -> 461 us measured).
 static int pool_nt() {
-  static const int v = [] {
-    const char *e = getenv("KCNN_POOL_NT");
-    return e && *e ? atoi(e) : 2;
-  }();
+  static const int v = KCNN_KNOB("KCNN_POOL_NT", 2);
   return v;
 }
 

@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "cnsl-hip-kernels.h"
+#include "kaldi-lite/kcnn-knobs.h"
 
 namespace kcnn {
 

@@ -85,7 +85,6 @@ CuDevice &CuDevice::Instantiate() {
 
 CuDevice::CuDevice() {
   if (getenv("KCNN_PROFILE")) profiling_ = atoi(getenv("KCNN_PROFILE")) != 0;
-  if (getenv("KCNN_GEMM")) gemm_mode_ = atoi(getenv("KCNN_GEMM")) != 0 ? 1 : 0;
 }
 CuDevice::~CuDevice() {}
 

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "kaldi-common.h"
+#include "kcnn-knobs.h"
 
 namespace kaldi {
 
@@ -77,8 +78,9 @@ class CuDevice {
   void ResetProfile() { profile_.clear(); }
 
   // AddMatMat's fp32 product: 0 = rocBLAS sgemm, 1 = bf16x6 split kernel
-  void SetGemmMode(int m) { gemm_mode_ = m; }
-  int GemmMode() const { return gemm_mode_; }
+  // (the "gemm" kernel family, kcnn-knobs.h)
+  void SetGemmMode(int m) { kcnn::set_family(kcnn::kFamGemm, m ? 1 : 0); }
+  int GemmMode() const { return kcnn::family(kcnn::kFamGemm); }
 
   void Synchronize();
 
@@ -91,7 +93,6 @@ class CuDevice {
   hipStream_t stream_ = nullptr;
   rocblas_handle blas_ = nullptr;
   bool profiling_ = false;
-  int gemm_mode_ = 1;
   std::map<std::string, std::pair<double, long>> profile_;
 
   std::mutex mu_;

@@ -307,11 +307,8 @@ void CuMatrixBase<Real>::AddMatMat(Real alpha, const CuMatrixBase<Real> &A,
       for (int s : {4, 2})
         if (k % s == 0 && k / s >= 1024 && tiles * s <= 512) { nsplit = s; break; }
     }
-    static const char *env = getenv("KCNN_GEMM_SPLITK");
-    if (env) {
-      const int e = atoi(env);
-      if (e >= 1 && k % e == 0) nsplit = e;
-    }
+    static const int e = KCNN_KNOB("KCNN_GEMM_SPLITK", 0);
+    if (e >= 1 && k % e == 0) nsplit = e;
   }
   if (nsplit > 1) {
     CuDevice &dev = CuDevice::Instantiate();

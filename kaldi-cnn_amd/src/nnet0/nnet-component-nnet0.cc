@@ -922,7 +922,7 @@ bool MaxpoolComponent::FusableWindow3D(int32 *ph, int32 *pw, int32 *pc) const {
 
 bool MaxpoolComponent::FoldsIntoConvBackprop() const {
   // KCNN_FOLD_3D=0: 3-D windows back to BackpropFromMask + the conv's Backprop
-  static const bool fold3d = getenv("KCNN_FOLD_3D") == nullptr || atoi(getenv("KCNN_FOLD_3D"));
+  static const bool fold3d = KCNN_KNOB("KCNN_FOLD_3D", 1) != 0;
   const int32 c = FusableChannelPool();
   if (c == 4 || c == 8) return true;
   int32 ph, pw, pc;

@@ -46,10 +46,10 @@ def triple(fn):
     return out
 
 
-def assert_bound(actual, truth, scale, rtol=1e-5, what=""):
+def assert_bound(actual, truth, scale, rtol=1e-5, what="", norm_rtol=None):
     """Parity criterion of SURVEY 8(d): |a - t| <= rtol * S elementwise (S =
     sum of |terms|, the dot-product error scale) and normwise
-    ||a - t|| / ||t|| <= rtol."""
+    ||a - t|| / ||t|| <= rtol (norm_rtol when given)."""
     a = np.asarray(actual, np.float64)
     t = np.asarray(truth, np.float64)
     s = np.asarray(scale, np.float64)
@@ -64,7 +64,8 @@ def assert_bound(actual, truth, scale, rtol=1e-5, what=""):
     nt = np.linalg.norm(t)
     if nt > 0:
         rel = np.linalg.norm(a - t) / nt
-        assert rel <= rtol, f"{what}: normwise rel err {rel:.3e} > {rtol}"
+        lim_n = rtol if norm_rtol is None else norm_rtol
+        assert rel <= lim_n, f"{what}: normwise rel err {rel:.3e} > {lim_n}"
 
 
 def assert_same(actual, expected, what=""):

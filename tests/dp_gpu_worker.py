@@ -59,9 +59,16 @@ def params(net):
 def main():
     out_dir, steps, n_global = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
     cfg, in_dim = CONFIGS[sys.argv[4] if len(sys.argv) > 4 else "c2"]
+    backend = sys.argv[5] if len(sys.argv) > 5 else "gloo"
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo")
-    kcnn.init(0)
+    if backend == "nccl":
+        # RCCL: one GPU per rank (the one-GPU test box runs world size 1)
+        torch.cuda.set_device(rank)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{rank}"))
+        kcnn.init(rank)
+    else:
+        dist.init_process_group("gloo")
+        kcnn.init(0)
     kcnn.set_randn_seed(7)
     net = kcnn.Nnet(cfg)
     r = np.random.default_rng(11)

@@ -77,3 +77,40 @@ def test_missing_library_raises(monkeypatch):
     monkeypatch.setattr(kcnn, "LIB_PATH", "/nonexistent/libkcnn.so")
     with pytest.raises(kcnn.KcnnError, match="not built"):
         kcnn.lib()
+
+
+# the documented run-time switches of the product library (kcnn-knobs.h):
+# kernel-family selectors plus fusion, literal replay, profiling and logging.
+# Experiment knobs are read only by the `make timing` build.
+DOCUMENTED_ENV = {"KCNN_FWD_X6", "KCNN_BWD_X6", "KCNN_IGEMM_X6", "KCNN_WGRAD_X6",
+                  "KCNN_GEMM", "KCNN_FUSE", "KCNN_LITERAL", "KCNN_PROFILE", "KCNN_QUIET"}
+
+
+def test_product_library_reads_only_documented_switches():
+    _lib()
+    out = subprocess.run(["strings", kcnn.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    env = {l for l in out.split() if l.startswith("KCNN_") and l.isupper()}
+    assert env <= DOCUMENTED_ENV, f"undocumented switches: {sorted(env - DOCUMENTED_ENV)}"
+
+
+def test_kernel_family_selectors():
+    _lib()
+    defaults = {"fwd_x6": 1, "bwd_x6": 1, "igemm_x6": 1, "wgrad_x6": 2, "gemm": 1}
+    for name, d in defaults.items():
+        if not os.environ.get("KCNN_" + name.upper()):
+            assert kcnn.get_kernel_family(name) == d, name
+    try:
+        kcnn.set_kernel_family("wgrad_x6", 1)
+        assert kcnn.get_kernel_family("wgrad_x6") == 1
+        kcnn.set_kernel_family("gemm", 0)
+        assert kcnn.get_kernel_family("gemm") == 0
+        with pytest.raises(kcnn.KcnnError, match="out of range"):
+            kcnn.set_kernel_family("bwd_x6", 2)
+        with pytest.raises(kcnn.KcnnError, match="unknown"):
+            kcnn.set_kernel_family("no_such_family", 0)
+        with pytest.raises(kcnn.KcnnError):
+            kcnn.get_kernel_family("no_such_family")
+    finally:
+        for name, d in defaults.items():
+            kcnn.set_kernel_family(name, d)

@@ -109,12 +109,16 @@ def _worker(rank, world, port, q, split):
 
 
 class _LocalDist:
-    """world_size 1: the all-reduce is the identity."""
+    """world_size 1: the all-reduce is the identity (counted)."""
     class _W:
         def wait(self):
             pass
 
+    def __init__(self):
+        self.sizes = []
+
     def all_reduce(self, t, async_op=False):
+        self.sizes.append(t.numel())
         return self._W()
 
 
@@ -124,11 +128,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("split", [1 << 20, 1])
-def test_dp_two_ranks_equal_one_process(split):
-    """split = 1: every gradient on its own (mode 3) with its all-reduce
-    started before the layer's data gradient (mode 2)."""
-    kcnn_dp.SPLIT_GRADIENT_PARAMS = split
+@pytest.mark.parametrize("split", [1 << 20, 1, 100])
+def test_dp_two_ranks_equal_one_process(split, monkeypatch):
+    """split = 1 << 20: both gradients in the flat bucket (one all-reduce);
+    split = 1: every gradient on its own (mode 3) with its all-reduce
+    started before the layer's data gradient (mode 2); split = 100: the FC
+    gradient (486 values) on its own, the conv's (52) in the bucket."""
+    monkeypatch.setattr(kcnn_dp, "SPLIT_GRADIENT_PARAMS", split)
     ref = OracleNet(seed=5)
     grads = kcnn_dp.gradient_buffers(ref, lambda n: torch.empty(n))
     for x, dy in zip(*_data()):
@@ -146,7 +152,6 @@ def test_dp_two_ranks_equal_one_process(split):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    kcnn_dp.SPLIT_GRADIENT_PARAMS = 1 << 20
     for r in range(2):
         for a, b in zip(got[r], want):
             # same math up to the fp32 rounding of a 2-way split of each sum
@@ -165,3 +170,25 @@ def test_dp_update_uses_global_count():
         kcnn_dp.dp_train_step(net, torch.from_numpy(x), torch.from_numpy(dy), g,
                               _LocalDist(), n)
     assert not np.allclose(_params(a)[0], _params(b)[0])
+
+
+@pytest.mark.parametrize("split,want", [(1 << 20, [52 + 486]), (1, [486, 52]), (100, [486, 52])])
+def test_dp_collectives_per_step(split, want, monkeypatch):
+    """The step issues one all-reduce per large gradient, in backprop order,
+    then one for the flat bucket of all the others (the conv's
+    filter and bias gradients in a single all-reduce)."""
+    monkeypatch.setattr(kcnn_dp, "SPLIT_GRADIENT_PARAMS", split)
+    net = OracleNet(seed=5)
+    grads = kcnn_dp.gradient_buffers(net, lambda n: torch.zeros(n))
+    assert grads.num_collectives() == len(want)
+    d = _LocalDist()
+    x, dy = (t[0] for t in _data())
+    marks = []
+    kcnn_dp.dp_train_step(net, torch.from_numpy(x), torch.from_numpy(dy), grads, d,
+                          N_GLOBAL, mark=marks.append)
+    assert d.sizes == want
+    assert marks == ["wait_begin", "wait_end"]
+    if grads.bucket is not None:
+        # the bucket's views alias one contiguous buffer
+        assert sum(grads[i].numel() for i in grads.small) == grads.bucket.numel()
+        assert grads[grads.small[0]].data_ptr() == grads.bucket.data_ptr()

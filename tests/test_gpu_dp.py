@@ -23,22 +23,27 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("stack,n_params,split", [("c2", 6, None), ("long", 9, None),
-                                                  ("c2", 6, "1")])
-def test_dp_two_ranks_match_single_process(tmp_path, stack, n_params, split):
+@pytest.mark.parametrize("stack,n_params,split,backend,nproc", [
+    ("c2", 6, None, "gloo", 2), ("long", 9, None, "gloo", 2), ("c2", 6, "1", "gloo", 2),
+    ("long", 9, None, "nccl", 1)])
+def test_dp_two_ranks_match_single_process(tmp_path, stack, n_params, split, backend, nproc):
     """split "1": every non-conv gradient computed on its own (mode 3) and
-    all-reduced while the layer's data gradient (mode 2) runs."""
+    all-reduced while the layer's data gradient (mode 2) runs.  backend
+    "nccl": the RCCL communicator and its async all-reduces (world size 1 on
+    the one-GPU test box; RCCL takes one GPU per rank)."""
     steps, n_global = 2, 48
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(HERE, "dp_gpu_worker.py"), str(tmp_path), str(steps), str(n_global),
-           stack]
+           stack, backend]
     env = dict(os.environ, OMP_NUM_THREADS="2")
     if split:
         env["KCNN_DP_SPLIT_PARAMS"] = split
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    a, b = np.load(tmp_path / "rank0.npz"), np.load(tmp_path / "rank1.npz")
+    a = np.load(tmp_path / "rank0.npz")
+    b = np.load(tmp_path / f"rank{nproc - 1}.npz")
     single = np.load(tmp_path / "single.npz")
     assert sorted(a.files) == sorted(single.files) and len(a.files) == n_params
     for k in a.files:

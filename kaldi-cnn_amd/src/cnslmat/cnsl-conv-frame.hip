@@ -1784,7 +1784,7 @@ static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
       if (need == 0 || ws == nullptr || ws_bytes < need) return -1;
     }
     int rc = kcnn_conv_bwd_x6(g, X, xs, dY, dys, K, ks, dX, dxs, gW ? part : nullptr, S,
-                              dx_acc, st, pmask, pms, pc, ph);
+                              dx_acc, st, pmask, pms, pc, ph, bdbg);
     if (rc || gW == nullptr) return rc;
     hipLaunchKernelGGL(reduce_splits_kernel, dim3((E + 63) / 64), dim3(256), 0, st, part, S,
                        E, g.Kdim * g.G, g.G, 0, gW, gws, gb);

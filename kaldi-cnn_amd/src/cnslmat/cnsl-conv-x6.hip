@@ -112,8 +112,21 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
     ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ dY, int dys,
     const float *__restrict__ K, int ks, float *__restrict__ dX, int dxs,
     float *__restrict__ ws_part, int ZZ, X6Steps steps, int dx_acc,
-    const unsigned char *__restrict__ pmask, int pms) {
+    const unsigned char *__restrict__ pmask, int pms, int dbg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+#ifdef KCNN_PHASE_TIMING  // per-phase clock totals of block 0's waves (dbg & 16)
+  long long tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long tprev = clock64();
+#define KCNN_TMARK(i)                                   \
+  if (dbg & 16) {                                       \
+    const long long tn = clock64();                     \
+    tm[i] += tn - tprev;                                \
+    tprev = tn;                                         \
+  }
+#else
+#define KCNN_TMARK(i)
+  (void)dbg;
+#endif
   const int P = g.P;
   const int Hp = g.H + 2 * g.pad_h, Wp = g.W + 2 * g.pad_w;
   const int CHWp = g.C * Hp * Wp;
@@ -391,13 +404,18 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
       for (int ch = 0; ch < NCH; ch++) {
         // B1: the slab (and map) DMA has landed for every wave; the image's
         // readers are done; last frame's Z is in LDS
+        KCNN_TMARK(7)
         x6::publish_dma();
+        KCNN_TMARK(0)
         if (ch == 0) {
           if (WG) commit_x();
           if (DX && DEFER && nprev >= 0) col2im(nprev);
         }
+        KCNN_TMARK(1)
         split_slab(ch);
+        KCNN_TMARK(2)
         __syncthreads();  // B2: the slab (and the frame's map) are in LDS
+        KCNN_TMARK(3)
         if (RW && ch == 0) {
           // the frame's im2col values of this wave's steps, split once
 #pragma unroll
@@ -413,6 +431,7 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
             split8(v, ain[s][0], ain[s][1], ain[s][2]);
           }
         }
+        KCNN_TMARK(4)
         // the next slab (or the next frame's first slab and map) into registers
         {
           const int nn = ch + 1 < NCH ? n : n + (int)gridDim.x;
@@ -422,6 +441,7 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
             if (WG && ch + 1 == NCH) load_x(nn);
           }
         }
+        KCNN_TMARK(5)
         if constexpr (RD) {
           // Z[p][k] += dY^T W on this wave's position tiles
           bf16x8 wf[2][3];
@@ -467,6 +487,7 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
             wacc[ch] = mfma6(ain[s], bf, wacc[ch]);
           }
         }
+        KCNN_TMARK(6)
       }
       if (DX && !DEFER) __syncthreads();  // the image is read no more: Z goes there
       if constexpr (RD) {
@@ -493,6 +514,11 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
       __syncthreads();
       col2im(nprev);
     }
+#ifdef KCNN_PHASE_TIMING
+    if ((dbg & 16) && blockIdx.x == 0 && lane == 0)
+      printf("bwdx6 wave %d: B1 %lld ch0 %lld split %lld B2 %lld im2col %lld dma %lld mfma %lld "
+             "tail %lld\n", wave, tm[0], tm[1], tm[2], tm[3], tm[4], tm[5], tm[6], tm[7]);
+#endif
     if (!WG) return;
     // the wgrad waves' partials (waves 4-7) summed in a fixed order
     const int E = (g.Kdim + 1) * g.G;
@@ -557,7 +583,7 @@ bool kcnn_conv_bwd_x6_eligible(const ConvGeom &g, bool dx, int pc, int ph) {
 int kcnn_conv_bwd_x6(const ConvGeom &g, const float *X, int xs, const float *dY, int dys,
                      const float *K, int ks, float *dX, int dxs, float *ws_part, int S,
                      int dx_acc, hipStream_t st, const unsigned char *pmask, int pms,
-                     int pc, int ph) {
+                     int pc, int ph, int dbg) {
   const bool dx = dX != nullptr, wg = ws_part != nullptr;
   if (!dx && !wg) return 0;
   if (!kcnn_conv_bwd_x6_eligible(g, dx, pc, ph)) return -1;
@@ -584,7 +610,7 @@ int kcnn_conv_bwd_x6(const ConvGeom &g, const float *X, int xs, const float *dY,
     (void)attr;                                                                            \
     hipLaunchKernelGGL((conv_bwd_x6_kernel<NCH, DXB, WGB, PCM, PH>), dim3(S), dim3(NT), lds, \
                        st, g, X, xs, dY, dys, K, ks, dX, dxs, ws_part, ZZ, tab, dx_acc,     \
-                       pmask, pms);                                                        \
+                       pmask, pms, dbg);                                                   \
   } while (0)
 #define KCNN_X6M(NCH, DXB, WGB)                                  \
   do {                                                           \

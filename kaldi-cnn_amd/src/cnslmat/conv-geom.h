@@ -78,7 +78,7 @@ bool kcnn_conv_bwd_x6_eligible(const kcnn::ConvGeom &g, bool dx, int pc, int ph 
 int kcnn_conv_bwd_x6(const kcnn::ConvGeom &g, const float *X, int xs, const float *dY,
                      int dys, const float *K, int ks, float *dX, int dxs, float *ws_part,
                      int S, int dx_acc, hipStream_t st, const unsigned char *pmask,
-                     int pms, int pc, int ph);
+                     int pms, int pc, int ph, int dbg = 0);
 // Conv2D(concat) + bias (+ ReLU when relu) as an implicit GEMM on the bf16
 // MFMAs (cnsl-conv-igemm-x6.hip); -1 when the shape is outside its limits.
 int kcnn_conv_igemm_x6(const kcnn::ConvGeom &g, const float *X, int xs, const float *K,

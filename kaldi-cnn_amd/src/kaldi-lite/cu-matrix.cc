@@ -287,10 +287,15 @@ void CuMatrixBase<Real>::AddMatMat(Real alpha, const CuMatrixBase<Real> &A,
                               Ap->Data(), Ap->Stride(), Bp->Data(), Bp->Stride(), beta,
                               data_, stride_, ws, wsb, S());
     if (ws) dev0.Free(ws);
-    if (rc != (int)hipErrorInvalidValue) {
-      CNSL_SAFE_CALL(rc);
-      return;
-    }
+    // The operands are aligned here, so the kernel declines (hipErrorInvalidValue)
+    // only past its grid limit (2^31 workgroups: M x N beyond 2^46 values).
+    // No silent switch of engine: that is the "gemm" family's to choose.
+    if (rc == (int)hipErrorInvalidValue)
+      KALDI_ERR << "AddMatMat: " << m << " x " << n << " x " << k
+                << " is outside the bf16x6 GEMM's limits; select rocBLAS sgemm with "
+                   "kcnn_set_kernel_family(\"gemm\", 0)";
+    CNSL_SAFE_CALL(rc);
+    return;
   }
   // Row-major C = op(A) op(B)  <=>  column-major C^T = op(B)^T op(A)^T.
   const rocblas_operation opB =

@@ -1,0 +1,125 @@
+"""Layer-by-layer parity of a whole kcnn_nnet training step against the oracle.
+
+One Propagate + Backprop (update in Backprop, the bench's step) of a
+Conv / Maxpool / FC stack runs on the GPU through libkcnn.so.  Every layer is
+then checked against the oracle applied to the GPU's own inputs of that
+layer -- the previous layer's GPU output going forward, the next layer's GPU
+input derivative going back -- so a check sees exactly one component's
+arithmetic (no rounding carried in from other layers, and max-pool routing
+decided by the same values on both sides):
+
+  Conv / FC Propagate        1e-5 * S bound       (nnet-component-nnet0.cc:423-446, 1133)
+  Maxpool Propagate/Backprop bit-exact            (A.8 / A.9)
+  Conv / FC Backprop (dX)    1e-5 * S bound       (:461-544)
+  Conv / FC update           bound on W', b', prev' (:738-777, :1133-1150)
+
+`rows` restricts the row-local checks (outputs and input derivatives) to a
+sample of rows; the parameter update, a sum over all rows, is then skipped.
+"""
+import numpy as np
+
+import oracle as O
+from _util import assert_bound, assert_same, host
+
+
+def truth(fn):
+    """fn in the oracle's fp64-accumulated mode (truth) and |.|-accumulated
+    mode (the error scale S)."""
+    out = []
+    for mode in (1, 2):
+        with O.accum(mode):
+            out.append(fn())
+    return out
+
+
+def oracle_layers(config, net, kc):
+    """Oracle objects for the stack's config lines, with the GPU stack's
+    current parameters."""
+    layers = []
+    for line, c in zip(config.strip().splitlines(), net.components):
+        t, *kvs = line.split()
+        info = dict(kv.split("=", 1) for kv in kvs)
+        g = lambda k, d=None: int(info.get(k, d))
+        assert t == c.Type(), (t, c.Type())
+        if t == "ConvolutionComponent":
+            # B4: weight-decay / momentum from the config line are ignored
+            oc = O.Conv(g("in-height"), g("in-width"), g("in-channel"), g("kernel-height"),
+                        g("kernel-width"), g("group"), in_pad_height=g("in-pad-height", 0),
+                        in_pad_width=g("in-pad-width", 0),
+                        learning_rate=float(info["learning-rate"]))
+        elif t == "MaxpoolComponent":
+            oc = O.Pool(g("in-height"), g("in-width"), g("in-channel"), g("pool-height-dim"),
+                        g("pool-width-dim"), g("pool-channel-dim"),
+                        info.get("overlap", "false") == "true",
+                        info.get("overlap2D", "false") == "true")
+        elif t == "FullyConnectedComponent":
+            oc = O.FC(c.InputDim(), c.OutputDim(),
+                      learning_rate=float(info["learning-rate"]),
+                      weight_decay=float(info.get("weight-decay", 0.0002)),
+                      momentum=float(info.get("momentum", 0.9)))
+        else:
+            raise ValueError(t)
+        if t != "MaxpoolComponent":
+            oc.W = host(c.GetParam(kc.PARAM_LINEAR))
+            oc.b = host(c.GetParam(kc.PARAM_BIAS)).ravel().copy()
+            oc.prev = host(c.GetParam(kc.PARAM_PREV_GRAD))
+        layers.append(oc)
+    return layers
+
+
+def _rows(t, rows):
+    if rows is None:
+        return host(t)
+    import torch
+    idx = torch.as_tensor(rows, device=t.device)
+    return host(t.index_select(0, idx))
+
+
+def run_step(kc, config, net, x, dy, rows=None):
+    """The training step on the GPU; returns the oracle layers (parameters
+    before the step), the layers' outputs and input derivatives (sampled
+    rows) and the parameters after."""
+    n = net.NumComponents()
+    before = oracle_layers(config, net, kc)
+    net.Propagate(x)
+    # outputs first: a fused conv's output is recomputed on request, which is
+    # possible until its backprop runs
+    outs = [_rows(net.Output(i), rows) for i in range(n)]
+    net.Backprop(dy)
+    derivs = [_rows(net.InputDeriv(i), rows) for i in range(n)]
+    after = [[host(c.GetParam(w)) for w in (kc.PARAM_LINEAR, kc.PARAM_BIAS, kc.PARAM_PREV_GRAD)]
+             if c.NumGradientParams() > 0 else None for c in net.components]
+    return before, outs, derivs, after
+
+
+def check_step(kc, config, net, x, dy, rows=None, what=""):
+    layers, outs, derivs, after = run_step(kc, config, net, x, dy, rows)
+    xin = _rows(x, rows)
+    dout = _rows(dy, rows)
+    ins = [xin] + outs[:-1]
+    d_next = derivs[1:] + [dout]
+    N = x.shape[0]
+    for i, oc in enumerate(layers):
+        tag = f"{what} layer {i} {type(oc).__name__}"
+        a, y = ins[i], outs[i]
+        if isinstance(oc, O.Pool):
+            assert_same(y, oc.propagate(a), f"{tag} Propagate")
+            assert_same(derivs[i], oc.backprop(a, y, d_next[i]), f"{tag} Backprop")
+            continue
+        y_t, y_s = truth(lambda: oc.propagate(a))
+        assert_bound(y, y_t, y_s, what=f"{tag} Propagate")
+        dx_t, dx_s = truth(lambda: oc.backprop(a, d_next[i], update=False))
+        assert_bound(derivs[i], dx_t, dx_s, what=f"{tag} dX")
+        if rows is not None:
+            continue
+        # the update: W' = W + m*prev - lr*wd*W + lr*gW (bias: b + lr*gb), lr
+        # divided by the rows of the step (B10)
+        (gW_t, gb_t), (gW_s, gb_s) = truth(lambda: oc.gradient(a, d_next[i]))
+        W0, b0, p0 = oc.W.copy(), oc.b.copy(), oc.prev.copy()
+        with O.accum(1):
+            oc.apply(gW_t, gb_t, N)
+        lr = oc.learning_rate / N
+        W1, b1, p1 = after[i]
+        assert_bound(W1, oc.W, np.abs(W0) + np.abs(p0) + lr * gW_s + 1e-30, what=f"{tag} W'")
+        assert_bound(b1.ravel(), oc.b, np.abs(b0) + lr * gb_s, what=f"{tag} b'")
+        assert_bound(p1, oc.prev, np.abs(p0) + lr * gW_s + 1e-6 * np.abs(W0), what=f"{tag} prev'")

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <fstream>
 #include <memory>
+#include <set>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -35,10 +36,14 @@ struct kcnn_nnet {
   std::vector<CuMatrix<BaseFloat>> fwd;    // fwd[0] borrowed input, fwd[i+1] = out_i
   std::vector<CuMatrix<BaseFloat>> deriv;  // deriv[i] = d input_i
   int num_chunks = 0;
-  // per component: first/last frame offset of its input and output chunk
-  // (upstream Nnet::ComputeChunkInfo for contiguous contexts: the last output
-  // is one frame per chunk; each component widens its input by Context())
-  std::vector<int> in_first, in_last, out_first, out_last;
+  // chunk offsets (upstream Nnet::ComputeChunkInfo): offs[i] are the frame
+  // offsets of component i's input chunk, offs[i + 1] of its output, in
+  // ascending order.  The last output is one frame per chunk; walking back,
+  // a component's input offsets are the set of output offset + Context();
+  // the network input is made contiguous; shifted so the first offset is 0.
+  // Gapped contexts (SpliceComponent context=-3:0:3) make a middle layer's
+  // offsets non-contiguous.
+  std::vector<std::vector<int32>> offs;
   // Conv -> channel-only Maxpool pairs run fused: routing mask of pool i
   // ([rows x OutputDim] bytes), valid for the minibatch of the last Propagate
   std::vector<unsigned char *> mask;
@@ -613,25 +618,24 @@ kcnn_nnet *kcnn_nnet_new(const char *config) {
                   << n->comps[i]->OutputDim() << ") and " << i + 1 << " ("
                   << n->comps[i + 1]->InputDim() << ")";
     const size_t nc = n->comps.size();
-    n->in_first.assign(nc, 0); n->in_last.assign(nc, 0);
-    n->out_first.assign(nc, 0); n->out_last.assign(nc, 0);
-    int f = 0, l = 0;
+    n->offs.assign(nc + 1, std::vector<int32>());
+    n->offs[nc].assign(1, 0);
     for (size_t k = nc; k-- > 0;) {
       const std::vector<int32> ctx = n->comps[k]->Context();
-      for (size_t j = 1; j < ctx.size(); j++)
-        if (ctx[j] != ctx[j - 1] + 1)
-          KALDI_ERR << "component " << k << " (" << n->comps[k]->Type()
-                    << "): only contiguous contexts are supported by the runtime";
-      n->out_first[k] = f; n->out_last[k] = l;
-      f += ctx.front(); l += ctx.back();
-      n->in_first[k] = f; n->in_last[k] = l;
+      std::set<int32> in;
+      for (int32 o : n->offs[k + 1])
+        for (int32 c : ctx) in.insert(o + c);
+      n->offs[k].assign(in.begin(), in.end());
+    }
+    {  // MakeOffsetsContiguous on the network input
+      const int32 lo = n->offs[0].front(), hi = n->offs[0].back();
+      n->offs[0].clear();
+      for (int32 o = lo; o <= hi; o++) n->offs[0].push_back(o);
     }
     // ChunkInfo offsets must be >= 0: shift everything by -first input offset
-    const int shift = -n->in_first[0];
-    for (size_t k = 0; k < nc; k++) {
-      n->in_first[k] += shift; n->in_last[k] += shift;
-      n->out_first[k] += shift; n->out_last[k] += shift;
-    }
+    const int32 shift = -n->offs[0].front();
+    for (auto &v : n->offs)
+      for (auto &o : v) o += shift;
     for (auto *c : n->comps) n->handles.push_back(kcnn_component{c});
     n->fwd.resize(n->comps.size() + 1);
     n->deriv.resize(n->comps.size());
@@ -651,11 +655,10 @@ kcnn_component *kcnn_nnet_component(kcnn_nnet *n, int i) {
 }
 
 static ChunkInfo nnet_in_info(const kcnn_nnet *n, size_t i) {
-  return ChunkInfo(n->comps[i]->InputDim(), n->num_chunks, n->in_first[i], n->in_last[i]);
+  return ChunkInfo(n->comps[i]->InputDim(), n->num_chunks, n->offs[i]);
 }
 static ChunkInfo nnet_out_info(const kcnn_nnet *n, size_t i) {
-  return ChunkInfo(n->comps[i]->OutputDim(), n->num_chunks, n->out_first[i],
-                   n->out_last[i]);
+  return ChunkInfo(n->comps[i]->OutputDim(), n->num_chunks, n->offs[i + 1]);
 }
 
 // The non-virtual Component::Propagate's sizing (nnet-component.h:203-215):
@@ -712,7 +715,7 @@ static bool propagate_relu_pair(kcnn_nnet *n, size_t i) {
 int kcnn_nnet_propagate(kcnn_nnet *n, const float *in, MatrixDim in_dim) {
   return guard([&] {
     KALDI_ASSERT(in_dim.cols == n->comps[0]->InputDim());
-    const int in_cs = n->in_last[0] - n->in_first[0] + 1;
+    const int in_cs = (int)n->offs[0].size();
     if (in_dim.rows % in_cs != 0)
       KALDI_ERR << "input rows " << in_dim.rows << " are not a multiple of the "
                 << in_cs << "-frame input chunk";

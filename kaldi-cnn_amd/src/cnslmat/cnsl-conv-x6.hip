@@ -70,6 +70,8 @@ constexpr int MAXS = 6;             // wgrad k16 steps per wave (24 over waves 4
 constexpr int MAXT = 3;             // dgrad position tiles per wave (12 over waves 0-3)
 constexpr int MAXU = 2;             // split units per thread (8 * 96 <= 2 * 512)
 constexpr int MAXX = 4;             // X values per thread (C*H*W <= 2048)
+constexpr int PZ = PP + 4;          // Z row (k-major) of conv_bwd_x6p_kernel: 16-B aligned,
+                                    // rows 4 banks apart
 
 struct X6Steps {
   uint8_t s[NW][MAXS];  // wgrad k16 steps of each wave, 0xff = none
@@ -551,6 +553,513 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
   }
   if (dgrad_wave) frames(std::integral_constant<int, 1>{});
   else frames(std::integral_constant<int, 2>{});
+#undef KCNN_TMARK
+}
+
+// ---------------------------------------------------------------------------
+// conv_bwd_x6p_kernel: conv_bwd_x6_kernel's math bit for bit -- the same
+// image contents, operand fragments, and order of the MFMAs into every
+// accumulator -- software-pipelined, for the pooled backward with both
+// outputs (DX and WG, a folded PH x 1 x PCM Maxpool, NCH >= 2 slabs per
+// frame: c2, c5 C1).
+//
+// conv_bwd_x6_kernel alternates an all-VALU phase (every wave splits the
+// next slab into the image) with an all-MFMA phase, two barriers apart, so
+// each SIMD's matrix pipe idles while its waves split (c2, block 0: split
+// 134 k, MFMA phase 167 k of 495 k cycles per wave, MFMA pipe 28 % busy).
+// Here the split of slab t+1 runs beside the MFMAs of slab t.  A thread
+// keeps its split units' gated bf16 planes in registers until the image is
+// free, and its raw dP / mask values come from HBM into registers one slab
+// ahead (no staging buffer, no LDS-DMA).  Per SIMD, the dgrad wave w and the
+// wgrad wave w + 4:
+//
+//   MFMA phase t   dgrad wave: split its 2 units of slab t+1, prefetch their
+//                  raw values of slab t+2, then its dgrad MFMAs of slab t
+//                  (position tiles w, w + 4, w + 8);  wgrad wave: its wgrad
+//                  MFMAs of slab t, then the frame work (col2im of the
+//                  previous frame on the first slab, the next frame's im2col
+//                  gather on the last), then its 1 unit of slab t+1 -- so
+//                  each wave's VALU runs beside its partner's MFMAs.  The
+//                  dgrad waves store the frame's Z on its last slab.
+//   barrier Ba     the image of slab t is read no more
+//   write phase    the held planes of slab t+1 -> the image; the map of the
+//                  frame after next -> LDS (last slab)
+//   barrier Bb     the image of slab t+1 is published
+//
+// Z is kept k-major here ([Kdim][PZ], a lane's accumulator rows are 16-B
+// runs); the col2im adds the same values in the same order.
+template <int NCH, int PCM, int PH>
+__global__ __launch_bounds__(NT, 1) void conv_bwd_x6p_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ dP, int dps,
+    const float *__restrict__ K, int ks, float *__restrict__ dX, int dxs,
+    float *__restrict__ ws_part, int ZZ, X6Steps steps, int dx_acc,
+    const unsigned char *__restrict__ pmask, int pms, int dbg) {
+  static_assert(NCH >= 2 && PCM > 0, "pooled backward with >= 2 slabs per frame");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+#ifdef KCNN_PHASE_TIMING  // per-phase clock totals of block 0's waves (dbg & 16)
+  long long tm[6] = {0, 0, 0, 0, 0, 0};
+  long long tprev = clock64();
+#define KCNN_TMARK(i)               \
+  if (dbg & 16) {                   \
+    const long long tn = clock64(); \
+    tm[i] += tn - tprev;            \
+    tprev = tn;                     \
+  }
+#else
+#define KCNN_TMARK(i)
+  (void)dbg;
+#endif
+  using MaskT = typename std::conditional<(PH > 1), unsigned short, unsigned char>::type;
+  constexpr int MB = (int)sizeof(MaskT);
+  constexpr int NJ = 32 / PCM;                         // pooled rows per slab
+  constexpr int SPL = NT;                                 // splitting threads
+  constexpr int MAXUP = (NJ * (PP / 4) + SPL - 1) / SPL;  // split units per thread
+  const int P = g.P;
+  const int Q = P / PH;  // pooled positions per dP row
+  const int Hp = g.H + 2 * g.pad_h, Wp = g.W + 2 * g.pad_w;
+  const int CHWp = g.C * Hp * Wp;
+  char *Yp = smem;                                            // [3][32][384] bf16
+  char *Wimg = Yp + 3 * YPL;                                  // [3][32][128] bf16
+  // Z k-major, [Kdim][PZ]: a lane's accumulator rows are runs of 4
+  // consecutive positions of one k, stored as 16-B writes
+  float *Zt = reinterpret_cast<float *>(Wimg + 3 * WPL);
+  float *Xs = Zt + g.Kdim * PZ;                               // padded map + {1}
+  int *qtab = reinterpret_cast<int *>(Xs + round4(CHWp + 1));  // [384]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l = lane & 31, hf = lane >> 5;
+  const int CHW = g.C * g.HW;
+  const bool unpadded = g.pad_h == 0 && g.pad_w == 0;
+  const int ntile = (P + 31) >> 5;
+  const int PW = (P + 15) & ~15;
+  const int NPQ = PW >> 2;
+  const int NU = NJ * NPQ;
+  const int G = (int)gridDim.x;
+  const int rowf = (g.G / PCM) * Q;  // pooled values per frame row
+
+  // W planes (dgrad B operand), as conv_bwd_x6_kernel
+  for (int e = tid; e < 32 * 64; e += NT) {
+    const int k = e >> 6, gg = (e & 63) * 2;
+    const float v0 = (k < g.Kdim && gg < g.G) ? K[(int64_t)k * ks + gg] : 0.0f;
+    const float v1 = (k < g.Kdim && gg + 1 < g.G) ? K[(int64_t)k * ks + gg + 1] : 0.0f;
+    uint32_t h, m, lo;
+    split2(v0, v1, h, m, lo);
+    const int o = woff(k, gg);
+    *reinterpret_cast<uint32_t *>(Wimg + o) = h;
+    *reinterpret_cast<uint32_t *>(Wimg + WPL + o) = m;
+    *reinterpret_cast<uint32_t *>(Wimg + 2 * WPL + o) = lo;
+  }
+  int abase = CHWp * 4, qmul = 0;
+  if (l < g.Kdim) {
+    uint32_t c, r, qx, qy;
+    g.div_khkw.divmod((uint32_t)l, c, r);
+    g.div_kh.divmod(r, qx, qy);
+    abase = ((int)c * Hp * Wp + (int)qx * Hp + (int)qy) * 4;
+    qmul = 1;
+  }
+  for (int e = tid; e < CHWp; e += NT) Xs[e] = 0.0f;
+  if (tid == 0) Xs[CHWp] = 1.0f;
+  for (int p = tid; p < PP; p += NT) {
+    uint32_t px, py;
+    g.div_oh.divmod((uint32_t)p, px, py);
+    qtab[p] = p < P ? ((int)px * Hp + (int)py) * 4 : 0x3fffffff;
+  }
+  const uint32_t amax = (uint32_t)CHWp * 4;
+  const char *Xb = reinterpret_cast<const char *>(Xs);
+
+  // ---- split units: (pooled row j, position quad p0), the same in every
+  // slab; the dgrad waves' threads own units tid + 256 i
+  int uj[MAXUP], up0[MAXUP], ubase[MAXUP], ux[MAXUP][2];
+#pragma unroll
+  for (int i = 0; i < MAXUP; ++i) {
+    const int u = min(tid + SPL * i, NU - 1);
+    uj[i] = u / NPQ;
+    up0[i] = (u - uj[i] * NPQ) * 4;
+    const int r0 = PCM * uj[i];
+    ubase[i] = r0 * ROWB + ((up0[i] >> 7) << 8) + ((up0[i] & 7) << 1);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) ux[i][hh] = ((up0[i] >> 3) & 15) ^ (((r0 >> 2) + hh) & 3);
+  }
+  // raw values of a unit: PH == 1 the quad's 4 dP values, PH > 1 the 2
+  // windows' values; the mask bytes of the same positions as two dwords
+  // (aligned down) and the byte shift.  U: units per thread of the role
+  // (MAXUP for the dgrad waves; the wgrad waves split nothing)
+  constexpr int NX = PH > 1 ? 2 : 4;
+  auto load_raw = [&](auto Uc, float (&rx)[decltype(Uc)::value][NX],
+                      uint32_t (&rm)[decltype(Uc)::value][2], int (&rsh)[decltype(Uc)::value],
+                      int nn, int cc) {
+    constexpr int U = decltype(Uc)::value;
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(dP + (int64_t)nn * dps), (short)0, rowf * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(pmask + (int64_t)nn * pms), (short)0, rowf * MB, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+      if (tid + SPL * i >= NU) break;
+      const int s = (cc * NJ + uj[i]) * Q + (PH > 1 ? up0[i] / PH : up0[i]);
+      if constexpr (NX == 4) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, (unsigned)s * 4u, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rx[i][q] = __uint_as_float(v[q]);
+      } else {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rd, (unsigned)s * 4u, 0, 0);
+        rx[i][0] = __uint_as_float(v[0]);
+        rx[i][1] = __uint_as_float(v[1]);
+      }
+      const unsigned mo = (unsigned)s * MB;
+      const auto w = __builtin_amdgcn_raw_buffer_load_b64(rk, mo & ~3u, 0, 0);
+      rm[i][0] = w[0];
+      rm[i][1] = w[1];
+      rsh[i] = (int)(mo & 3u);
+    }
+  };
+  // gated planes of a unit: [map c][plane][2 dwords]
+  auto split_raw = [&](auto Uc, const float (&rx)[decltype(Uc)::value][NX],
+                       const uint32_t (&rm)[decltype(Uc)::value][2],
+                       const int (&rsh)[decltype(Uc)::value],
+                       uint32_t (&sres)[decltype(Uc)::value][PCM][6]) {
+    constexpr int U = decltype(Uc)::value;
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+      if (tid + SPL * i >= NU) break;
+      const int p0 = up0[i];
+      const uint32_t mw = __builtin_amdgcn_alignbyte(rm[i][1], rm[i][0], (uint32_t)rsh[i]);
+      float x[4];
+      unsigned mk[4];
+      short rq[4];
+      if constexpr (PH > 1) {
+        const int pq0 = p0 / PH, r0 = p0 - pq0 * PH;
+        const unsigned m0 = mw & 0xffffu, m1 = mw >> 16;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool sel = r0 + q >= PH;
+          rq[q] = (short)(r0 + q - (sel ? PH : 0));
+          x[q] = sel ? rx[i][1] : rx[i][0];
+          mk[q] = p0 + q < P ? (sel ? m1 : m0) : 0u;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          rq[q] = 0;
+          x[q] = rx[i][q];
+          mk[q] = p0 + q < P ? (mw >> (8 * q)) & 0xffu : 0u;
+        }
+      }
+      uint32_t h01, m01, l01, h23, m23, l23;
+      split2(x[0], x[1], h01, m01, l01);
+      split2(x[2], x[3], h23, m23, l23);
+      const s16x2 w01 = __builtin_bit_cast(s16x2, mk[0] | (mk[1] << 16));
+      const s16x2 w23 = __builtin_bit_cast(s16x2, mk[2] | (mk[3] << 16));
+      const s16x2 b01 = {(short)(15 - rq[0]), (short)(15 - rq[1])};
+      const s16x2 b23 = {(short)(15 - rq[2]), (short)(15 - rq[3])};
+#pragma unroll
+      for (int c = 0; c < PCM; ++c) {
+        const s16x2 cc = {(short)(c * PH), (short)(c * PH)}, k15 = {15, 15};
+        const s16x2 sh01 = b01 - cc, sh23 = b23 - cc;
+        const uint32_t s01 = __builtin_bit_cast(uint32_t, (s16x2)((w01 << sh01) >> k15));
+        const uint32_t s23 = __builtin_bit_cast(uint32_t, (s16x2)((w23 << sh23) >> k15));
+        sres[i][c][0] = h01 & s01;
+        sres[i][c][1] = h23 & s23;
+        sres[i][c][2] = m01 & s01;
+        sres[i][c][3] = m23 & s23;
+        sres[i][c][4] = l01 & s01;
+        sres[i][c][5] = l23 & s23;
+      }
+    }
+  };
+  auto write_sres = [&](auto Uc, const uint32_t (&sres)[decltype(Uc)::value][PCM][6]) {
+    constexpr int U = decltype(Uc)::value;
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+      if (tid + SPL * i >= NU) break;
+#pragma unroll
+      for (int c = 0; c < PCM; ++c) {
+        const int o = ubase[i] + c * ROWB + ((ux[i][c >> 2] ^ ((c & 3) << 2)) << 4);
+        *reinterpret_cast<uint2 *>(Yp + o) = make_uint2(sres[i][c][0], sres[i][c][1]);
+        *reinterpret_cast<uint2 *>(Yp + YPL + o) = make_uint2(sres[i][c][2], sres[i][c][3]);
+        *reinterpret_cast<uint2 *>(Yp + 2 * YPL + o) = make_uint2(sres[i][c][4], sres[i][c][5]);
+      }
+    }
+  };
+
+  // ---- X map (wgrad A operand) ----
+  float xv[MAXX];
+  auto load_x = [&](int n) {
+#pragma unroll
+    for (int i = 0; i < MAXX; i++)
+      if (tid + NT * i < CHW) xv[i] = X[(int64_t)n * xs + tid + NT * i];
+  };
+  auto commit_x = [&]() {
+#pragma unroll
+    for (int i = 0; i < MAXX; i++) {
+      const int e = tid + NT * i;
+      if (e < CHW) {
+        int slot = e;
+        if (!unpadded) {
+          uint32_t c, q, wi, hi;
+          g.div_HW.divmod((uint32_t)e, c, q);
+          g.div_H.divmod(q, wi, hi);
+          slot = (int)c * Hp * Wp + ((int)wi + g.pad_w) * Hp + (int)hi + g.pad_h;
+        }
+        Xs[slot] = xv[i];
+      }
+    }
+  };
+  // ---- col2im (dX) from Zs: conv_bwd_x6_kernel's, the same sums in the same order
+  const int khkw = g.kh * g.kw;
+  // element (p, k) at k * PZ + p: tap (kx, ky) of output (c, tx, ty) at
+  // c khkw PZ + tx oh + ty + kx (kh PZ - oh) + ky (PZ - 1)
+  const int zax = g.kh * PZ - g.oh, zby = PZ - 1;
+  auto col2im = [&](int nn) {
+#pragma unroll 1
+    for (int i = 0; i < MAXX; i++) {
+      const int e = tid + NT * i;
+      if (e >= CHW) continue;
+      uint32_t c, q, wi, hi;
+      g.div_HW.divmod((uint32_t)e, c, q);
+      g.div_H.divmod(q, wi, hi);
+      const int ty = (int)hi + g.pad_h, tx = (int)wi + g.pad_w;
+      const int zb = (int)c * khkw * PZ + tx * g.oh + ty;
+      const int ylo = max(0, ty - g.oh + 1), ny = min(g.kh - 1, ty) - ylo;
+      const int xlo = max(0, tx - g.ow + 1), xhi = min(g.kw - 1, tx);
+      float sum = 0.0f;
+      for (int kx = xlo; kx <= xhi; kx++) {
+        const int zk = zb + kx * zax;
+        for (int k0 = 0; k0 < g.kh; k0 += 8) {
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) v[u] = Zt[zk + (k0 + u) * zby];
+#pragma unroll
+          for (int u = 0; u < 8; u++)
+            sum += (unsigned)(k0 + u - ylo) <= (unsigned)ny ? v[u] : 0.0f;
+        }
+      }
+      float *d = dX + (int64_t)nn * dxs + e;
+      *d = dx_acc ? *d + sum : sum;
+    }
+  };
+
+  const bool dgrad_wave = wave < 4;
+  int my_steps = 0;
+  int stp[MAXS];
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    stp[s] = steps.s[wave][s];
+    if (!dgrad_wave && stp[s] != 0xff) my_steps = s + 1;
+  }
+  // the frame's im2col values of this wave's steps, split once per frame
+  auto gather = [&](auto &a) {
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) {
+      if (s >= my_steps) break;
+      const int pbase = 16 * stp[s] + 8 * hf;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t off = min((uint32_t)(abase + qmul * qtab[pbase + e]), amax);
+        v[e] = *reinterpret_cast<const float *>(Xb + off);
+      }
+      split8(v, a[s][0], a[s][1], a[s][2]);
+      __builtin_amdgcn_sched_barrier(0);  // one step's temporaries at a time
+    }
+  };
+
+  const int n0 = blockIdx.x;
+  auto frames = [&](auto role) {
+    constexpr bool RD = decltype(role)::value == 1;  // dgrad waves
+    constexpr int U = RD ? MAXUP : 1;
+    using UC = std::integral_constant<int, U>;
+    float rx[U][NX];
+    uint32_t rm[U][2];
+    int rsh[U];
+    uint32_t sres[U][PCM][6];
+    // (defined on every path: steps past my_steps are never used, but an
+    // undefined register set costs the allocator spills)
+    bf16x8 ain[RD ? 1 : MAXS][3];
+#pragma unroll
+    for (int s = 0; s < (RD ? 1 : MAXS); ++s)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) ain[s][pl] = bf16x8{};
+    // ---- prologue: the maps of the first two frames, the first frame's
+    // im2col values, its first slab in the image, its second slab's raw values
+    load_x(n0);
+    load_raw(UC{}, rx, rm, rsh, n0, 0);
+    __syncthreads();  // Xs zeroed, qtab and the W image written
+    commit_x();
+    if (n0 + G < g.R) load_x(n0 + G);
+    __syncthreads();
+    if constexpr (!RD) gather(ain);
+    split_raw(UC{}, rx, rm, rsh, sres);
+    load_raw(UC{}, rx, rm, rsh, n0, 1);
+    __syncthreads();  // the gather's reads of Xs are done
+    if (n0 + G < g.R) commit_x();
+    write_sres(UC{}, sres);
+    __syncthreads();  // Bb: slab (n0, 0) in the image, frame n0 + G's map in Xs
+
+    floatx16 wacc[RD ? 1 : NCH];
+#pragma unroll
+    for (int c = 0; c < (RD ? 1 : NCH); c++) wacc[c] = zero16();
+    int nprev = -1;
+
+    for (int n = n0; n < g.R; n += G) {
+      // dgrad position tiles: the dgrad waves w, w + 4; the wgrad waves take
+      // one each (w + 4 = tiles 8-11), beside their weight-gradient steps
+      constexpr int TT = RD ? MAXT : 1;
+      floatx16 zacc[TT];
+#pragma unroll
+      for (int t = 0; t < TT; ++t) zacc[t] = zero16();
+      auto tile_of = [&](int t) { return wave + 4 * t; };
+      // Z[p][k] += dY^T W on this wave's position tiles: MFMA group gi =
+      // (tile t = gi / 2, k16 slice s = gi % 2), the next group's transposed
+      // reads issued before the current group's MFMAs (two fragment sets live,
+      // not every group's: the wgrad role's registers are tight)
+      auto dgrad = [&](int ch) {
+        bf16x8 wf[2][3];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            wf[s][pl] = *reinterpret_cast<const bf16x8 *>(
+                Wimg + pl * WPL + woff(l, ch * 32 + 16 * s + 8 * hf));
+        const int G4 = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+        auto load_af = [&](int gi, bf16x8 (&af)[3]) {
+          const int col = tile_of(gi >> 1) * 32 + 16 * (G4 & 1) + 4 * pp;
+          const int row = 16 * (gi & 1) + 8 * (G4 >> 1) + q;
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) {
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s16x4 *)(Yp + pl * YPL + yoff(row, col)));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s16x4 *)(Yp + pl * YPL + yoff(row + 4, col)));
+            af[pl] = __builtin_bit_cast(
+                bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          }
+        };
+        constexpr int NG = 2 * TT;
+        bf16x8 afb[2][3];
+        if (tile_of(0) < ntile) load_af(0, afb[0]);
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) {
+          if (tile_of(gi >> 1) >= ntile) break;  // uniform
+          if (gi + 1 < NG && tile_of((gi + 1) >> 1) < ntile) load_af(gi + 1, afb[(gi + 1) & 1]);
+          zacc[gi >> 1] = mfma6(afb[gi & 1], wf[gi & 1], zacc[gi >> 1]);
+        }
+      };
+      // Z of this frame -> LDS: its last reader, the col2im of the previous
+      // frame in this frame's first slab, is two barriers back
+      auto store_z = [&]() {
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+          const int pt = tile_of(t);
+          if (pt >= ntile) break;
+          // rows (r & 3) + 8 (r >> 2) + 4 hf: four runs of 4 positions
+          // (positions past P land in the row's tail, never read)
+          if (l < g.Kdim) {
+            float *zr = Zt + l * PZ + pt * 32 + 4 * hf;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+              *reinterpret_cast<float4 *>(zr + 8 * i) =
+                  make_float4(zacc[t][4 * i], zacc[t][4 * i + 1], zacc[t][4 * i + 2],
+                              zacc[t][4 * i + 3]);
+          }
+        }
+      };
+#pragma unroll
+      for (int ch = 0; ch < NCH; ch++) {
+        // slab t = (n, ch); t+1 and t+2 in frame order
+        const int n1 = ch + 1 < NCH ? n : n + G;
+        const int n2 = ch + 2 < NCH ? n : n + G, c2 = ch + 2 < NCH ? ch + 2 : ch + 2 - NCH;
+        const bool next = n1 < g.R;
+        KCNN_TMARK(5)
+        if (ch == 0 && n + 2 * G < g.R) load_x(n + 2 * G);
+        if constexpr (RD) {
+          // the split of slab t+1 beside the wgrad waves' MFMAs, then ours
+          if (next) {
+            split_raw(UC{}, rx, rm, rsh, sres);
+            if (n2 < g.R) load_raw(UC{}, rx, rm, rsh, n2, c2);
+          }
+          KCNN_TMARK(0)
+          dgrad(ch);
+          KCNN_TMARK(1)
+          if (ch == 0 && nprev >= 0) col2im(nprev);
+        } else {
+          // gW[k][g] += im2col(X) dY^T over this wave's k16 steps of p (the
+          // next step's row reads issued before the current step's MFMAs)
+          auto load_bf = [&](int s, bf16x8 (&bf)[3]) {
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+              bf[pl] = *reinterpret_cast<const bf16x8 *>(Yp + pl * YPL +
+                                                         yoff(l, 16 * stp[s] + 8 * hf));
+          };
+          bf16x8 bfb[2][3];
+          if (my_steps > 0) load_bf(0, bfb[0]);
+#pragma unroll
+          for (int s = 0; s < MAXS; ++s) {
+            if (s >= my_steps) break;
+            if (s + 1 < MAXS && s + 1 < my_steps) load_bf(s + 1, bfb[(s + 1) & 1]);
+            wacc[ch] = mfma6(ain[s], bfb[s & 1], wacc[ch]);
+          }
+          KCNN_TMARK(1)
+          if (ch == 0 && nprev >= 0) col2im(nprev);
+          // the next frame's im2col values (its map went to Xs two barriers
+          // ago; this slab's MFMAs were the last readers of ain)
+          if (ch == NCH - 1 && n + G < g.R) gather(ain);
+          if (next) {
+            split_raw(UC{}, rx, rm, rsh, sres);
+            if (n2 < g.R) load_raw(UC{}, rx, rm, rsh, n2, c2);
+          }
+        }
+        if (RD && ch == NCH - 1) store_z();
+        KCNN_TMARK(2)
+        __syncthreads();  // Ba: the image of slab t is read no more
+        KCNN_TMARK(3)
+        if (next) write_sres(UC{}, sres);
+        // the map of the frame after next (Xs was last read by this slab's gather)
+        if (ch == NCH - 1 && n + 2 * G < g.R) commit_x();
+        __syncthreads();  // Bb: slab t+1 published
+        KCNN_TMARK(4)
+      }
+      nprev = n;
+    }
+    __syncthreads();  // the last frame's Z
+    if (nprev >= 0) col2im(nprev);
+#ifdef KCNN_PHASE_TIMING
+    if ((dbg & 16) && blockIdx.x == 0 && lane == 0)
+      printf("bwdx6p wave %d: split %lld mfma %lld frame %lld Ba %lld write+Bb %lld top %lld\n",
+             wave, tm[0], tm[1], tm[2], tm[3], tm[4], tm[5]);
+#endif
+    // the wgrad waves' partials summed in a fixed order, as conv_bwd_x6_kernel
+    const int E = (g.Kdim + 1) * g.G;
+    float *dst = ws_part + (int64_t)blockIdx.x * E;
+    float *red = reinterpret_cast<float *>(Yp);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++) {
+      __syncthreads();
+      if constexpr (!RD) {
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+          red[(wave - 4) * 1024 + mfma32_row(r, lane) * 32 + l] = wacc[ch][r];
+      }
+      __syncthreads();
+      for (int e = tid; e < 1024; e += NT) {
+        const int i = e >> 5, j = e & 31;
+        if (i > g.Kdim) continue;
+        float sum = 0.0f;
+#pragma unroll
+        for (int w = 0; w < 4; w++) sum += red[w * 1024 + e];
+        dst[i * g.G + ch * 32 + j] = sum;
+      }
+    }
+  };
+  if (dgrad_wave) frames(std::integral_constant<int, 1>{});
+  else frames(std::integral_constant<int, 2>{});
+#undef KCNN_TMARK
+}
+
+size_t x6p_lds(const ConvGeom &g) {
+  const int CHWp = g.C * (g.H + 2 * g.pad_h) * (g.W + 2 * g.pad_w);
+  return (size_t)3 * YPL + 3 * WPL + (size_t)g.Kdim * PZ * 4 +
+         (size_t)round4(CHWp + 1) * 4 + (size_t)PP * 4;
 }
 
 size_t x6_lds(const ConvGeom &g, bool dx, int pc, int ph) {
@@ -600,8 +1109,41 @@ int kcnn_conv_bwd_x6(const ConvGeom &g, const float *X, int xs, const float *dY,
     if (nstep > 4 * MAXS) return -1;
     for (int s = 0; s < nstep; ++s) tab.s[4 + s % 4][s / 4] = (uint8_t)s;
   }
-  const size_t lds = x6_lds(g, dx, pc, ph);
   const int ZZ = g.Kdim | 1;
+  // the software-pipelined kernel for the pooled backward with both outputs
+  // (bitwise the same results); KCNN_BWD_X6P=0 (experiment build) keeps
+  // conv_bwd_x6_kernel for it too
+  static const int pipelined = KCNN_KNOB("KCNN_BWD_X6P", 1);
+  if (pipelined && dx && wg && pc > 0 && g.G >= 64 && x6p_lds(g) <= (size_t)160 * 1024) {
+    const size_t lds = x6p_lds(g);
+#define KCNN_X6PP(NCH, PCM, PH)                                                              \
+  do {                                                                                       \
+    static bool attr = hipFuncSetAttribute(                                                 \
+        reinterpret_cast<const void *>(&conv_bwd_x6p_kernel<NCH, PCM, PH>),                  \
+        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;               \
+    (void)attr;                                                                              \
+    hipLaunchKernelGGL((conv_bwd_x6p_kernel<NCH, PCM, PH>), dim3(S), dim3(NT), lds, st, g, X, \
+                       xs, dY, dys, K, ks, dX, dxs, ws_part, ZZ, tab, dx_acc, pmask, pms,    \
+                       dbg);                                                                 \
+  } while (0)
+#define KCNN_X6PM(NCH)                                      \
+  do {                                                      \
+    if (pc == 4 && ph == 3) KCNN_X6PP(NCH, 4, 3);           \
+    else if (pc == 4 && ph == 2) KCNN_X6PP(NCH, 4, 2);      \
+    else if (pc == 4) KCNN_X6PP(NCH, 4, 1);                 \
+    else if (pc == 8 && ph == 2) KCNN_X6PP(NCH, 8, 2);      \
+    else KCNN_X6PP(NCH, 8, 1);                              \
+  } while (0)
+    switch (g.G / 32) {
+      case 2: KCNN_X6PM(2); break;
+      case 3: KCNN_X6PM(3); break;
+      default: KCNN_X6PM(4); break;
+    }
+#undef KCNN_X6PM
+#undef KCNN_X6PP
+    return (int)hipGetLastError();
+  }
+  const size_t lds = x6_lds(g, dx, pc, ph);
 #define KCNN_X6P(NCH, DXB, WGB, PCM, PH)                                                   \
   do {                                                                                     \
     static bool attr = hipFuncSetAttribute(                                               \

@@ -651,8 +651,11 @@ int32 SpliceComponent::OutputDim() const {
 }
 
 namespace {
-// The splice geometry for contiguous chunk offsets (what the nnet runtime
-// builds for a contiguous context); other ChunkInfos are rejected.
+// The splice geometry of a pair of ChunkInfos.  Contiguous offsets (every
+// chunk info of a contiguous context) use the arithmetic form; otherwise
+// (a gapped context deeper in a stack) the row table of in-chunk indices,
+// ChunkInfo::GetIndex(out offset + context[c]) as in the reference's index
+// vectors (nnet-component.cc:2670-2681).
 kn_splice_geom SpliceGeom(const ChunkInfo &in_info, const ChunkInfo &out_info,
                           const std::vector<int32> &context, int32 input_dim,
                           int32 const_dim) {
@@ -663,9 +666,6 @@ kn_splice_geom SpliceGeom(const ChunkInfo &in_info, const ChunkInfo &out_info,
   if (out_cs <= 0)
     KALDI_ERR << "Splicing features: output will have zero dimension. "
               << "Probably a code error.";
-  if (in_info.GetOffset(in_cs - 1) - in_info.GetOffset(0) + 1 != in_cs ||
-      out_info.GetOffset(out_cs - 1) - out_info.GetOffset(0) + 1 != out_cs)
-    KALDI_ERR << "SpliceComponent: non-contiguous chunk offsets are not supported";
   kn_splice_geom g;
   g.num_chunks = in_info.NumChunks();
   g.in_cs = in_cs;
@@ -675,11 +675,25 @@ kn_splice_geom SpliceGeom(const ChunkInfo &in_info, const ChunkInfo &out_info,
   g.const_dim = const_dim;
   g.dim = input_dim - const_dim;
   g.num_splice = (int)context.size();
+  if (g.num_splice > KN_SPLICE_MAX_CONTEXT)
+    KALDI_ERR << "SpliceComponent: more than " << KN_SPLICE_MAX_CONTEXT << " spliced frames";
+  const bool contiguous = in_info.GetOffset(in_cs - 1) - g.in_first + 1 == in_cs &&
+                          out_info.GetOffset(out_cs - 1) - g.out_first + 1 == out_cs;
+  g.table = contiguous ? 0 : 1;
+  if (!contiguous && (int64_t)g.num_splice * out_cs > KN_SPLICE_MAX_TAB)
+    KALDI_ERR << "SpliceComponent: " << g.num_splice << " x " << out_cs
+              << " spliced rows per chunk exceed the row table (" << KN_SPLICE_MAX_TAB << ")";
   for (int c = 0; c < g.num_splice; c++) {
     g.context[c] = context[c];
-    // every spliced frame must exist in the input chunk (GetIndex asserts)
-    (void)in_info.GetIndex(g.out_first + context[c]);
-    (void)in_info.GetIndex(out_info.GetOffset(out_cs - 1) + context[c]);
+    if (contiguous) {
+      // every spliced frame must exist in the input chunk (GetIndex asserts)
+      (void)in_info.GetIndex(g.out_first + context[c]);
+      (void)in_info.GetIndex(out_info.GetOffset(out_cs - 1) + context[c]);
+    } else {
+      for (int32 oi = 0; oi < out_cs; oi++)
+        g.in_index[c * out_cs + oi] =
+            (short)in_info.GetIndex(out_info.GetOffset(oi) + context[c]);
+    }
   }
   return g;
 }

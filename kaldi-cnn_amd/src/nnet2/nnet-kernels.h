@@ -35,10 +35,18 @@ int kn_relu_backprop(const float *out_value, MatrixDim ov_dim, const float *out_
  * CopyRows/AddMat sequence: in_deriv row r sums, over c in order, the out_deriv
  * block of the output row that read it (0 if none). */
 #define KN_SPLICE_MAX_CONTEXT 64
+/* Non-contiguous chunk offsets (a gapped context deeper in a stack): table
+ * = 1 and in_index[c * out_cs + oi] is the in-chunk input row that splice
+ * block c of output row oi reads (ChunkInfo::GetIndex of out offset oi +
+ * context[c]); num_splice * out_cs <= KN_SPLICE_MAX_TAB.  table = 0: the
+ * contiguous form, in row = out_first + oi + context[c] - in_first. */
+#define KN_SPLICE_MAX_TAB 1024
 typedef struct {
   int num_chunks, in_cs, out_cs, in_first, out_first;
   int dim, const_dim, num_splice;
   int context[KN_SPLICE_MAX_CONTEXT];
+  int table;
+  short in_index[KN_SPLICE_MAX_TAB];
 } kn_splice_geom;
 int kn_splice_prop(const float *in, MatrixDim in_dim, float *out, MatrixDim out_dim,
                    kn_splice_geom geom, kcnn_stream_t st);

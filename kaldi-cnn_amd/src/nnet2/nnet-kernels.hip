@@ -85,7 +85,8 @@ __global__ __launch_bounds__(256) void splice_prop_kernel(const float *__restric
     if ((int)col < g.num_splice * g.dim) {
       uint32_t c, d;
       a.div_dim.divmod(col, c, d);
-      irow = (int)chunk * g.in_cs + (g.out_first + (int)oi + g.context[c] - g.in_first);
+      irow = (int)chunk * g.in_cs + (g.table ? (int)g.in_index[c * g.out_cs + oi]
+                                             : g.out_first + (int)oi + g.context[c] - g.in_first);
       icol = (int)d;
     } else {
       irow = (int)chunk * g.in_cs + (int)oi;
@@ -108,7 +109,13 @@ __global__ __launch_bounds__(256) void splice_backprop_kernel(
     float v = 0.0f;
     if (icol < g.dim) {
       for (int c = 0; c < g.num_splice; c++) {
-        const int oi = g.in_first + (int)ii - g.context[c] - g.out_first;
+        int oi = -1;
+        if (g.table) {  // the output row of block c that read row ii (at most one)
+          for (int o = 0; o < g.out_cs; o++)
+            if (g.in_index[c * g.out_cs + o] == (int)ii) { oi = o; break; }
+        } else {
+          oi = g.in_first + (int)ii - g.context[c] - g.out_first;
+        }
         if (oi >= 0 && oi < g.out_cs)
           v += od[((int64_t)chunk * g.out_cs + oi) * ods + c * g.dim + icol];
       }
@@ -193,9 +200,15 @@ int kn_splice_prop(const float *in, MatrixDim in_dim, float *out, MatrixDim out_
       in_dim.cols != g.dim + g.const_dim ||
       out_dim.cols != g.num_splice * g.dim + g.const_dim)
     return (int)hipErrorInvalidValue;
-  for (int c = 0; c < g.num_splice; c++) {
-    const int lo = g.out_first + g.context[c] - g.in_first;
-    if (lo < 0 || lo + g.out_cs > g.in_cs) return (int)hipErrorInvalidValue;
+  if (g.table) {
+    if ((int64_t)g.num_splice * g.out_cs > KN_SPLICE_MAX_TAB) return (int)hipErrorInvalidValue;
+    for (int e = 0; e < g.num_splice * g.out_cs; e++)
+      if (g.in_index[e] < 0 || g.in_index[e] >= g.in_cs) return (int)hipErrorInvalidValue;
+  } else {
+    for (int c = 0; c < g.num_splice; c++) {
+      const int lo = g.out_first + g.context[c] - g.in_first;
+      if (lo < 0 || lo + g.out_cs > g.in_cs) return (int)hipErrorInvalidValue;
+    }
   }
   const int64_t total = (int64_t)out_dim.rows * out_dim.cols;
   if (total == 0) return 0;

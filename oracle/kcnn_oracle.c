@@ -772,30 +772,34 @@ int orc_relu_backprop(const orc_mat *out_value, const orc_mat *out_deriv,
  * SpliceComponent (nnet2/nnet-component.cc:2638-2819), contiguous chunks:
  * GetOffset(i) = first + i, GetIndex(o) = o - first (asserted in range).
  * ======================================================================== */
-static int splice_check(int in_first, int in_cs, int out_first, int out_cs,
-                        const int *context, int num_splice) {
-  for (int c = 0; c < num_splice; c++)
-    for (int oi = 0; oi < out_cs; oi++) {
-      const int ii = out_first + oi + context[c] - in_first;   /* GetIndex */
-      if (ii < 0 || ii >= in_cs) return -1;
-    }
-  return 0;
+/* ChunkInfo::GetIndex over an explicit offset list (nnet-component.h
+ * ChunkInfo; upstream nnet2's offsets_ vector): -1 when absent */
+static int chunk_index(const int *offsets, int n, int offset) {
+  for (int i = 0; i < n; i++)
+    if (offsets[i] == offset) return i;
+  return -1;
 }
 
-int orc_splice_propagate(const orc_mat *in, orc_mat *out, int num_chunks, int in_first,
-                         int in_cs, int out_first, int out_cs, const int *context,
-                         int num_splice, int const_dim) {
+/* SpliceComponent::Propagate (nnet-component.cc:2638-2720) with the chunk
+ * offsets as lists (in_offsets[in_cs], out_offsets[out_cs], ascending; the
+ * rows of a chunk in that order): out row (chunk, oi), splice block c copies
+ * in row (chunk, GetIndex(out_offsets[oi] + context[c])) (:2674-2681); the
+ * const part copies in row (chunk, oi) (:2692-2698) */
+int orc_splice_propagate_offsets(const orc_mat *in, orc_mat *out, int num_chunks,
+                                 const int *in_offsets, int in_cs, const int *out_offsets,
+                                 int out_cs, const int *context, int num_splice,
+                                 int const_dim) {
   const int input_dim = in->cols, dim = input_dim - const_dim;
   CHECK(in->rows == num_chunks * in_cs && out->rows == num_chunks * out_cs);
   CHECK(out->cols == dim * num_splice + const_dim);
-  CHECK(splice_check(in_first, in_cs, out_first, out_cs, context, num_splice) == 0);
   for (int c = 0; c < num_splice; c++)                     /* :2697-2705 */
-    for (int chunk = 0; chunk < num_chunks; chunk++)
-      for (int oi = 0; oi < out_cs; oi++) {
-        const int src = chunk * in_cs + (out_first + oi + context[c] - in_first);
+    for (int oi = 0; oi < out_cs; oi++) {
+      const int ii = chunk_index(in_offsets, in_cs, out_offsets[oi] + context[c]);
+      CHECK(ii >= 0);                                      /* GetIndex: KALDI_ERR */
+      for (int chunk = 0; chunk < num_chunks; chunk++)
         for (int d = 0; d < dim; d++)
-          AT(out, chunk * out_cs + oi, c * dim + d) = AT(in, src, d);  /* CopyRows */
-      }
+          AT(out, chunk * out_cs + oi, c * dim + d) = AT(in, chunk * in_cs + ii, d);
+    }
   if (const_dim != 0)                                      /* :2706-2713 */
     for (int chunk = 0; chunk < num_chunks; chunk++)
       for (int oi = 0; oi < out_cs; oi++)
@@ -805,24 +809,28 @@ int orc_splice_propagate(const orc_mat *in, orc_mat *out, int num_chunks, int in
   return 0;
 }
 
-int orc_splice_backprop(const orc_mat *out_deriv, orc_mat *in_deriv, int num_chunks,
-                        int in_first, int in_cs, int out_first, int out_cs,
-                        const int *context, int num_splice, int const_dim) {
+/* SpliceComponent::Backprop (nnet-component.cc:2723-2819), offsets as lists:
+ * per splice block c the in_deriv rows are CopyRows of the out_deriv row
+ * that read them (-1: zero), c = 0 copied, later blocks added (AddMat) */
+int orc_splice_backprop_offsets(const orc_mat *out_deriv, orc_mat *in_deriv, int num_chunks,
+                                const int *in_offsets, int in_cs, const int *out_offsets,
+                                int out_cs, const int *context, int num_splice,
+                                int const_dim) {
   const int input_dim = in_deriv->cols, dim = input_dim - const_dim;
   CHECK(in_deriv->rows == num_chunks * in_cs && out_deriv->rows == num_chunks * out_cs);
   CHECK(out_deriv->cols == dim * num_splice + const_dim);
-  CHECK(splice_check(in_first, in_cs, out_first, out_cs, context, num_splice) == 0);
   const int R = in_deriv->rows;
   int *idx = (int *)malloc(sizeof(int) * (size_t)R);
   float *temp = (float *)malloc(sizeof(float) * (size_t)R * (dim > 0 ? dim : 1));
   if (!idx || !temp) { free(idx); free(temp); return -1; }
   for (int c = 0; c < num_splice; c++) {
-    for (int r = 0; r < R; r++) idx[r] = -1;               /* :2760-2762 */
-    for (int chunk = 0; chunk < num_chunks; chunk++)
-      for (int oi = 0; oi < out_cs; oi++) {
-        const int ii = out_first + oi + context[c] - in_first;
-        idx[chunk * in_cs + ii] = chunk * out_cs + oi;     /* :2768-2775 */
-      }
+    for (int r = 0; r < R; r++) idx[r] = -1;               /* :2757-2759 */
+    for (int oi = 0; oi < out_cs; oi++) {
+      const int ii = chunk_index(in_offsets, in_cs, out_offsets[oi] + context[c]);
+      if (ii < 0) { free(idx); free(temp); return -1; }
+      for (int chunk = 0; chunk < num_chunks; chunk++)
+        idx[chunk * in_cs + ii] = chunk * out_cs + oi;     /* :2766-2781 */
+    }
     for (int r = 0; r < R; r++)                            /* CopyRows :2804/2806 */
       for (int d = 0; d < dim; d++)
         temp[(size_t)r * dim + d] = idx[r] < 0 ? 0.0f : AT(out_deriv, idx[r], c * dim + d);
@@ -844,4 +852,37 @@ int orc_splice_backprop(const orc_mat *out_deriv, orc_mat *in_deriv, int num_chu
   free(idx);
   free(temp);
   return 0;
+}
+
+/* contiguous chunks: offsets in_first + [0, in_cs), out_first + [0, out_cs) */
+static int *range_offsets(int first, int n) {
+  int *o = (int *)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+  if (o)
+    for (int i = 0; i < n; i++) o[i] = first + i;
+  return o;
+}
+
+int orc_splice_propagate(const orc_mat *in, orc_mat *out, int num_chunks, int in_first,
+                         int in_cs, int out_first, int out_cs, const int *context,
+                         int num_splice, int const_dim) {
+  int *io = range_offsets(in_first, in_cs), *oo = range_offsets(out_first, out_cs);
+  const int rc = io && oo ? orc_splice_propagate_offsets(in, out, num_chunks, io, in_cs, oo,
+                                                         out_cs, context, num_splice, const_dim)
+                          : -1;
+  free(io);
+  free(oo);
+  return rc;
+}
+
+int orc_splice_backprop(const orc_mat *out_deriv, orc_mat *in_deriv, int num_chunks,
+                        int in_first, int in_cs, int out_first, int out_cs,
+                        const int *context, int num_splice, int const_dim) {
+  int *io = range_offsets(in_first, in_cs), *oo = range_offsets(out_first, out_cs);
+  const int rc = io && oo ? orc_splice_backprop_offsets(out_deriv, in_deriv, num_chunks, io,
+                                                        in_cs, oo, out_cs, context,
+                                                        num_splice, const_dim)
+                          : -1;
+  free(io);
+  free(oo);
+  return rc;
 }

@@ -169,6 +169,16 @@ int orc_relu_backprop(const orc_mat *out_value, const orc_mat *out_deriv,
 /* SpliceComponent::Propagate/Backprop (:2638-2819) for chunk offsets
  * [in_first, in_first + in_cs) -> [out_first, out_first + out_cs): the
  * reference's index vectors and CopyRows / AddMat sequence, literally. */
+/* SpliceComponent with the chunk offsets as explicit ascending lists (the
+ * upstream ChunkInfo offsets_ vector: gapped contexts) */
+int orc_splice_propagate_offsets(const orc_mat *in, orc_mat *out, int num_chunks,
+                                 const int *in_offsets, int in_cs, const int *out_offsets,
+                                 int out_cs, const int *context, int num_splice,
+                                 int const_dim);
+int orc_splice_backprop_offsets(const orc_mat *out_deriv, orc_mat *in_deriv, int num_chunks,
+                                const int *in_offsets, int in_cs, const int *out_offsets,
+                                int out_cs, const int *context, int num_splice,
+                                int const_dim);
 int orc_splice_propagate(const orc_mat *in, orc_mat *out, int num_chunks, int in_first,
                          int in_cs, int out_first, int out_cs, const int *context,
                          int num_splice, int const_dim);

@@ -410,6 +410,28 @@ class Splice:
                                         *self._geom(num_chunks, out_cs)))
         return out
 
+    def propagate_offsets(self, x, in_offsets, out_offsets, num_chunks):
+        """Propagate with explicit chunk offset lists (upstream ChunkInfo with
+        an offsets_ vector: gapped contexts deeper in a stack)."""
+        io = (ctypes.c_int * len(in_offsets))(*in_offsets)
+        oo = (ctypes.c_int * len(out_offsets))(*out_offsets)
+        ctx = (ctypes.c_int * len(self.context))(*self.context)
+        out = np.zeros((num_chunks * len(out_offsets), self.output_dim), np.float32)
+        _chk(lib().orc_splice_propagate_offsets(
+            ctypes.byref(mat(x)), ctypes.byref(mat(out)), num_chunks, io, len(in_offsets),
+            oo, len(out_offsets), ctx, len(self.context), self.const_dim))
+        return out
+
+    def backprop_offsets(self, dy, in_offsets, out_offsets, num_chunks):
+        io = (ctypes.c_int * len(in_offsets))(*in_offsets)
+        oo = (ctypes.c_int * len(out_offsets))(*out_offsets)
+        ctx = (ctypes.c_int * len(self.context))(*self.context)
+        dx = np.zeros((num_chunks * len(in_offsets), self.input_dim), np.float32)
+        _chk(lib().orc_splice_backprop_offsets(
+            ctypes.byref(mat(dy)), ctypes.byref(mat(dx)), num_chunks, io, len(in_offsets),
+            oo, len(out_offsets), ctx, len(self.context), self.const_dim))
+        return dx
+
     def backprop(self, dy, num_chunks=None, out_cs=1):
         ctx = list(self.context)
         in_cs = out_cs + ctx[-1] - ctx[0]
@@ -418,3 +440,19 @@ class Splice:
         _chk(lib().orc_splice_backprop(ctypes.byref(mat(dy)), ctypes.byref(mat(dx)),
                                        *self._geom(num_chunks, out_cs)))
         return dx
+
+
+def chunk_offsets(contexts, out_frames=1):
+    """Upstream nnet2 Nnet::ComputeChunkInfo for a stack whose components have
+    the given Context() lists: walking back from the last output (out_frames
+    consecutive offsets), each component's input offsets are the sorted set
+    of output offset + context; the network input is made contiguous
+    (MakeOffsetsContiguous); everything shifted so the first offset is 0.
+    Returns one ascending offset list per chunk info (len(contexts) + 1)."""
+    offs = [None] * (len(contexts) + 1)
+    offs[-1] = list(range(out_frames))
+    for k in range(len(contexts) - 1, -1, -1):
+        offs[k] = sorted({o + c for o in offs[k + 1] for c in contexts[k]})
+    offs[0] = list(range(offs[0][0], offs[0][-1] + 1))
+    shift = -offs[0][0]
+    return [[o + shift for o in lst] for lst in offs]

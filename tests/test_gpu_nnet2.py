@@ -157,3 +157,57 @@ def test_nnet_config_prefix(kc):
     vs, ds, cnt = r1.NonlinearStats()
     assert cnt == N
     np.testing.assert_array_equal(ds, orl1.deriv_sum)
+
+
+GAPPED_CFG = """SpliceComponent input-dim=8 context=-2:-1:0:1:2 const-component-dim=0
+RectifiedLinearComponent dim=40
+SpliceComponent input-dim=40 context=-3:0:3 const-component-dim=0
+FullyConnectedComponent input-dim=120 output-dim=16 learning-rate=0.02 param-stddev=0.05 bias-stddev=1 weight-decay=0.0002 momentum=0.9"""
+
+
+def test_gapped_splice_stack(kc):
+    """A gapped context deeper in the stack (upstream Nnet::ComputeChunkInfo:
+    the second Splice's context -3:0:3 leaves the first Splice's output and
+    the ReLU with chunk offsets {2, 5, 8}, not a contiguous range) against the
+    oracle's offset-list splices (oracle.chunk_offsets); the input chunk is
+    contiguous (11 frames per output frame)."""
+    kc.set_randn_seed(3)
+    net = kc.Nnet(GAPPED_CFG)
+    s1, rl, s2, fc = net.components
+    offs = O.chunk_offsets([s1.Context(), rl.Context(), s2.Context(), fc.Context()])
+    assert offs[1] == [2, 5, 8] and len(offs[0]) == 11
+    N = 13
+    r = rng(29)
+    x = randn(r, (N * len(offs[0]), 8))
+    dy = randn(r, (N, 16), 0.1)
+    net.Propagate(dev(x))
+    outs = [host(net.Output(i)) for i in range(4)]
+    o1, orl, o2 = O.Splice(8, tuple(s1.Context())), O.ReLU(40), O.Splice(40, tuple(s2.Context()))
+    of = O.FC(120, 16)
+    of.W = host(fc.LinearParams()); of.b = host(fc.BiasParams()); of.prev = host(fc.PrevGrad())
+    a0 = o1.propagate_offsets(x, offs[0], offs[1], N)
+    a1 = orl.propagate(a0)
+    a2 = o2.propagate_offsets(a1, offs[2], offs[3], N)
+    assert_same(outs[0], a0, "Splice 1 (gapped chunk offsets)")
+    assert_same(outs[1], a1, "ReLU")
+    assert_same(outs[2], a2, "Splice 2")
+    with O.accum(1):
+        y_t = of.propagate(a2)
+    np.testing.assert_allclose(outs[3], y_t, rtol=1e-5, atol=1e-6)
+    net.Backprop(dev(dy))
+    with O.accum(1):
+        d3 = of.backprop(a2, dy, update=True)
+    d2 = o2.backprop_offsets(d3, offs[2], offs[3], N)
+    d1 = orl.backprop(a1, d2)
+    d0 = o1.backprop_offsets(d1, offs[0], offs[1], N)
+    np.testing.assert_allclose(host(net.InputDeriv(3)), d3, rtol=1e-5, atol=1e-6)
+    # splice backprops and the ReLU backprop on the GPU's own derivatives
+    g3 = host(net.InputDeriv(3))
+    assert_same(host(net.InputDeriv(2)), o2.backprop_offsets(g3, offs[2], offs[3], N), "Splice 2 dX")
+    g2 = host(net.InputDeriv(2))
+    assert_same(host(net.InputDeriv(1)), orl.backprop(a1, g2, update=False), "ReLU dX")
+    g1 = host(net.InputDeriv(1))
+    assert_same(host(net.InputDeriv(0)), o1.backprop_offsets(g1, offs[0], offs[1], N), "Splice 1 dX")
+    np.testing.assert_allclose(host(net.InputDeriv(0)), d0, rtol=1e-5, atol=1e-6)
+    err = np.abs(host(fc.LinearParams()) - of.W).max() / np.abs(of.W).max()
+    assert err < 1e-5, err

@@ -89,3 +89,27 @@ def test_splice_matches_numpy_with_const_and_overlap():
                 exp[k * in_cs + t + c - ctx[0], :dim] += dy[k * out_cs + t, ci * dim:(ci + 1) * dim]
             exp[k * in_cs + t, dim:] = dy[k * out_cs + t, len(ctx) * dim:]
     np.testing.assert_allclose(dx, exp, rtol=1e-6, atol=1e-6)
+
+
+def test_chunk_offsets_and_gapped_splice():
+    """Upstream Nnet::ComputeChunkInfo restated (oracle.chunk_offsets) and the
+    offset-list splice against a direct numpy gather (SpliceComponent::
+    Propagate's index vectors, nnet-component.cc:2670-2681)."""
+    import numpy as np
+    offs = O.chunk_offsets([[-2, -1, 0, 1, 2], [0], [-3, 0, 3], [0]])
+    assert offs == [list(range(11)), [2, 5, 8], [2, 5, 8], [5], [5]]
+    assert O.chunk_offsets([list(range(-10, 11))]) == [list(range(21)), [10]]
+    r = np.random.default_rng(4)
+    N, D = 3, 5
+    sp = O.Splice(D, (-3, 0, 3))
+    x = r.standard_normal((N * 3, D)).astype(np.float32)          # offsets 2, 5, 8
+    y = sp.propagate_offsets(x, [2, 5, 8], [5], N)
+    want = np.concatenate([x.reshape(N, 3, D)[:, i] for i in range(3)], axis=1)
+    np.testing.assert_array_equal(y, want)
+    dx = sp.backprop_offsets(y, [2, 5, 8], [5], N)
+    np.testing.assert_array_equal(dx, x)                          # one reader per row
+    # contiguous offsets: the offset-list form equals the range form
+    sp2 = O.Splice(D, (-1, 0, 1))
+    x2 = r.standard_normal((N * 4, D)).astype(np.float32)
+    np.testing.assert_array_equal(sp2.propagate_offsets(x2, [0, 1, 2, 3], [1, 2], N),
+                                  sp2.propagate(x2, N, out_cs=2))

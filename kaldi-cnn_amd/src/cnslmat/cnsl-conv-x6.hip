@@ -985,11 +985,18 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6p_kernel(
         } else {
           // gW[k][g] += im2col(X) dY^T over this wave's k16 steps of p (the
           // next step's row reads issued before the current step's MFMAs)
+          // yoff(l, 16 stp + 8 hf) = l ROWB + (stp >> 3) 256 + (((stp & 7) << 5) ^
+          // ((hf ^ swz4(l)) << 4)): the lane part passes through an opaque
+          // move each slab, so the compiler does not hoist (and spill) six
+          // per-step addresses out of the frame loop
+          int lx, lrow;
+          asm volatile("v_mov_b32 %0, %1" : "=v"(lx) : "v"((hf ^ swz4(l)) << 4));
+          asm volatile("v_mov_b32 %0, %1" : "=v"(lrow) : "v"(l * ROWB));
           auto load_bf = [&](int s, bf16x8 (&bf)[3]) {
+            const int off = lrow + ((stp[s] >> 3) << 8) + (((stp[s] & 7) << 5) ^ lx);
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl)
-              bf[pl] = *reinterpret_cast<const bf16x8 *>(Yp + pl * YPL +
-                                                         yoff(l, 16 * stp[s] + 8 * hf));
+              bf[pl] = *reinterpret_cast<const bf16x8 *>(Yp + pl * YPL + off);
           };
           bf16x8 bfb[2][3];
           if (my_steps > 0) load_bf(0, bfb[0]);
@@ -1004,16 +1011,20 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6p_kernel(
           // the next frame's im2col values (its map went to Xs two barriers
           // ago; this slab's MFMAs were the last readers of ain)
           if (ch == NCH - 1 && n + G < g.R) gather(ain);
-          if (next) {
-            split_raw(UC{}, rx, rm, rsh, sres);
-            if (n2 < g.R) load_raw(UC{}, rx, rm, rsh, n2, c2);
-          }
         }
         if (RD && ch == NCH - 1) store_z();
         KCNN_TMARK(2)
         __syncthreads();  // Ba: the image of slab t is read no more
         KCNN_TMARK(3)
-        if (next) write_sres(UC{}, sres);
+        if (next) {
+          // the wgrad waves split their unit here, beside the dgrad waves'
+          // LDS writes (its planes are not held through the MFMA phase)
+          if constexpr (!RD) {
+            split_raw(UC{}, rx, rm, rsh, sres);
+            if (n2 < g.R) load_raw(UC{}, rx, rm, rsh, n2, c2);
+          }
+          write_sres(UC{}, sres);
+        }
         // the map of the frame after next (Xs was last read by this slab's gather)
         if (ch == NCH - 1 && n + 2 * G < g.R) commit_x();
         __syncthreads();  // Bb: slab t+1 published

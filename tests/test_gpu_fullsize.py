@@ -1,6 +1,7 @@
 """Parity at BASELINE.json's sizes (the configurations the bench lines are
 measured on), layer by layer against the oracle (tests/_stack.py):
 
+  * c1 (configs[0]): the Conv -> Maxpool forward at its 256 frames;
   * c2 (configs[1]): the exact bench.py step -- its stack, its parameters
     (kcnn_set_randn_seed 20261015), its inputs, 4096 frames, fusion mode 1,
     the default kernels -- with every output, input derivative and updated
@@ -20,7 +21,7 @@ import pytest
 
 import bench
 import oracle as O
-from _stack import check_step, truth
+from _stack import check_step, oracle_layers, truth
 from _util import assert_bound, assert_same, host, rng
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
@@ -33,6 +34,27 @@ def _inputs(B, in_cols, out_cols, seed=20261015):
     x = torch.randn((B, in_cols), generator=gen, device="cuda")
     dy = torch.randn((B, out_cols), generator=gen, device="cuda") * 1e-2
     return x, dy
+
+
+@pytest.mark.parametrize("fusion", [0, 1])
+def test_c1_forward(kc, fusion):
+    """BASELINE configs[0]: Conv(40x11x3, 8x1, 128) -> Maxpool(1x1x4), forward
+    only, 256 frames (the reference's --use-gpu=no case, here on the GPU)."""
+    kc.set_fusion(fusion)
+    try:
+        kc.set_randn_seed(20261015)
+        cfg = "\n".join(bench.stack_config().splitlines()[:2])
+        net = kc.Nnet(cfg)
+        x, _ = _inputs(256, bench.H * bench.W * bench.C, 1)
+        conv, pool = oracle_layers(cfg, net, kc)
+        net.Propagate(x)
+        y, p = host(net.Output(0)), host(net.Output(1))
+        xh = host(x)
+        y_t, y_s = truth(lambda: conv.propagate(xh))
+        assert_bound(y, y_t, y_s, what="c1 conv Propagate")
+        assert_same(p, pool.propagate(y), "c1 maxpool Propagate")
+    finally:
+        kc.set_fusion(1)
 
 
 def test_c2_bench_step(kc):

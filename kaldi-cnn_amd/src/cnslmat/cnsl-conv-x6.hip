@@ -1067,11 +1067,600 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6p_kernel(
 #undef KCNN_TMARK
 }
 
+// ---------------------------------------------------------------------------
+// conv_bwd_x6q_kernel: conv_bwd_x6p_kernel's math bit for bit (the same image
+// contents, fragments and MFMA order into every accumulator), with the slab
+// image consumed in two position halves so that its LDS writes run beside
+// the MFMAs instead of between them.
+//
+// Half A = positions 0-255 (dgrad tiles 0-7: tiles w and w + 4 of dgrad wave
+// w; wgrad steps 0-15: steps 0-3 of every wgrad wave), half B = 256-383
+// (tile w + 8; steps 4-5).  Every accumulator still sees its MFMAs in the
+// same order: a dgrad tile lives in one half, and a wgrad wave's A steps come
+// before its B steps.  Per slab t, two phases a barrier apart:
+//
+//   P_A(t)  MFMAs on half A of slab t; the B-half planes of slab t -> image
+//           (split during P_B(t-1)); the A units of slab t+1 split
+//   P_B(t)  MFMAs on half B of slab t; the A-half planes of slab t+1 -> image;
+//           the B units of slab t+1 split
+//
+// so one LDS image serves both halves and each phase pairs one half's MFMAs
+// with the other half's stores.  Split units: A unit u (quad u % 64 of
+// pooled row u / 64) belongs to thread u, B unit u (positions 256 + ...) to
+// dgrad-wave thread u.  Frame work sits where an accumulator's last reader
+// is behind a barrier: the wgrad waves gather the next frame's A-step
+// im2col values in P_B of the last slab and its B-step values in P_A of the
+// first; the next frame's map goes to Xs in P_B of the first slab; the
+// previous frame's col2im runs in the second slab (P_B, or P_A when NCH = 2,
+// ahead of the last slab's store of Z).
+template <int NCH, int PCM, int PH>
+__global__ __launch_bounds__(NT, 1) void conv_bwd_x6q_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ dP, int dps,
+    const float *__restrict__ K, int ks, float *__restrict__ dX, int dxs,
+    float *__restrict__ ws_part, int ZZ, X6Steps steps, int dx_acc,
+    const unsigned char *__restrict__ pmask, int pms, int dbg) {
+  static_assert(NCH >= 2 && PCM > 0, "pooled backward with >= 2 slabs per frame");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+#ifdef KCNN_PHASE_TIMING  // per-phase clock totals of block 0's waves (dbg & 16)
+  long long tm[5 * NCH] = {};
+  long long tprev = clock64();
+#define KCNN_TMARK(i)               \
+  if (dbg & 16) {                   \
+    const long long tn = clock64(); \
+    tm[i] += tn - tprev;            \
+    tprev = tn;                     \
+  }
+// timing experiments that skip work (wrong results): 32 no image stores, 64
+// no MFMAs, 128 no splits, 256 no frame work (gather, col2im, map, Z), 512
+// no gather, 1024 no col2im
+#define KCNN_SKIP(b) (dbg & (b))
+#else
+#define KCNN_TMARK(i)
+#define KCNN_SKIP(b) false
+  (void)dbg;
+#endif
+  (void)ZZ;
+  using MaskT = typename std::conditional<(PH > 1), unsigned short, unsigned char>::type;
+  constexpr int MB = (int)sizeof(MaskT);
+  constexpr int NJ = 32 / PCM;  // pooled rows per slab
+  constexpr int HALF = 256;     // positions of half A
+  constexpr int SA = HALF / 16 / 4;  // wgrad steps per wave in half A
+  constexpr int MAXC = 2 * MAXX;     // col2im elements per dgrad-wave thread
+  const int P = g.P;
+  const int Q = P / PH;
+  const int Hp = g.H + 2 * g.pad_h, Wp = g.W + 2 * g.pad_w;
+  const int CHWp = g.C * Hp * Wp;
+  char *Yp = smem;                                            // [3][32][384] bf16
+  char *Wimg = Yp + 3 * YPL;                                  // [3][32][128] bf16
+  float *Zt = reinterpret_cast<float *>(Wimg + 3 * WPL);      // [Kdim][PZ]
+  float *Xs = Zt + g.Kdim * PZ;                               // padded map + {1}
+  int *qtab = reinterpret_cast<int *>(Xs + round4(CHWp + 1));  // [384]
+  // col2im taps of each dX element (kw == 1, kh <= 8): Z offset | ylo << 16 |
+  // ny << 20, the same every frame
+  int *ctab = qtab + PP;  // [CHW]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l = lane & 31, hf = lane >> 5;
+  const int CHW = g.C * g.HW;
+  const bool unpadded = g.pad_h == 0 && g.pad_w == 0;
+  const int ntile = (P + 31) >> 5;
+  const int PW = (P + 15) & ~15;
+  const int NPQ = PW >> 2;
+  const int NPQA = min(NPQ, HALF / 4), NPQB = NPQ - NPQA;
+  const int G = (int)gridDim.x;
+  const int rowf = (g.G / PCM) * Q;
+
+  for (int e = tid; e < 32 * 64; e += NT) {
+    const int k = e >> 6, gg = (e & 63) * 2;
+    const float v0 = (k < g.Kdim && gg < g.G) ? K[(int64_t)k * ks + gg] : 0.0f;
+    const float v1 = (k < g.Kdim && gg + 1 < g.G) ? K[(int64_t)k * ks + gg + 1] : 0.0f;
+    uint32_t h, m, lo;
+    split2(v0, v1, h, m, lo);
+    const int o = woff(k, gg);
+    *reinterpret_cast<uint32_t *>(Wimg + o) = h;
+    *reinterpret_cast<uint32_t *>(Wimg + WPL + o) = m;
+    *reinterpret_cast<uint32_t *>(Wimg + 2 * WPL + o) = lo;
+  }
+  int abase = CHWp * 4, qmul = 0;
+  if (l < g.Kdim) {
+    uint32_t c, r, qx, qy;
+    g.div_khkw.divmod((uint32_t)l, c, r);
+    g.div_kh.divmod(r, qx, qy);
+    abase = ((int)c * Hp * Wp + (int)qx * Hp + (int)qy) * 4;
+    qmul = 1;
+  }
+  for (int e = tid; e < CHWp; e += NT) Xs[e] = 0.0f;
+  if (tid == 0) Xs[CHWp] = 1.0f;
+  for (int p = tid; p < PP; p += NT) {
+    uint32_t px, py;
+    g.div_oh.divmod((uint32_t)p, px, py);
+    qtab[p] = p < P ? ((int)px * Hp + (int)py) * 4 : 0x3fffffff;
+  }
+  const int khkw0 = g.kh * g.kw;
+  const bool c2fast = g.kw == 1 && g.kh <= 8;
+  if (c2fast) {
+    for (int e = tid; e < g.C * g.HW; e += NT) {
+      uint32_t c, q, wi, hi;
+      g.div_HW.divmod((uint32_t)e, c, q);
+      g.div_H.divmod(q, wi, hi);
+      const int ty = (int)hi + g.pad_h, tx = (int)wi + g.pad_w;
+      const int ylo = max(0, ty - g.oh + 1), ny = min(g.kh - 1, ty) - ylo;
+      ctab[e] = ((int)c * khkw0 * PZ + tx * g.oh + ty) | (ylo << 16) | (ny << 20);
+    }
+  }
+  const uint32_t amax = (uint32_t)CHWp * 4;
+  const char *Xb = reinterpret_cast<const char *>(Xs);
+
+  // ---- split units: (pooled row j, position quad p0), the same in every slab
+  struct Unit {
+    int j, p0, base, x0, x1;
+    bool on;
+  };
+  auto make_unit = [&](int u, int npq, int pfirst) {
+    Unit U;
+    U.on = u < NJ * npq;
+    const int uu = U.on ? u : 0;
+    U.j = npq > 0 ? uu / npq : 0;
+    U.p0 = pfirst + (uu - U.j * npq) * 4;
+    const int r0 = PCM * U.j;
+    U.base = r0 * ROWB + ((U.p0 >> 7) << 8) + ((U.p0 & 7) << 1);
+    U.x0 = ((U.p0 >> 3) & 15) ^ ((r0 >> 2) & 3);
+    U.x1 = ((U.p0 >> 3) & 15) ^ (((r0 >> 2) + 1) & 3);
+    return U;
+  };
+  constexpr int NX = PH > 1 ? 2 : 4;
+  auto load_raw = [&](const Unit &U, float (&rx)[NX], uint32_t (&rm)[2], int &rsh, int nn,
+                      int cc) {
+    // no branch: a unit that is off reads past the buffer (0s, unused), so
+    // every path issues the same loads and the compiler's vmcnt waits stay
+    // exact (a conditional load makes them vmcnt(0), which then also waits
+    // for the dX stores)
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(dP + (int64_t)nn * dps), (short)0, rowf * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(pmask + (int64_t)nn * pms), (short)0, rowf * MB, 0x00020000);
+    const int s = (cc * NJ + U.j) * Q + (PH > 1 ? U.p0 / PH : U.p0);
+    const unsigned oob = 0x40000000u;
+    if constexpr (NX == 4) {
+      const auto v =
+          __builtin_amdgcn_raw_buffer_load_b128(rd, U.on ? (unsigned)s * 4u : oob, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rx[q] = __uint_as_float(v[q]);
+    } else {
+      const auto v =
+          __builtin_amdgcn_raw_buffer_load_b64(rd, U.on ? (unsigned)s * 4u : oob, 0, 0);
+      rx[0] = __uint_as_float(v[0]);
+      rx[1] = __uint_as_float(v[1]);
+    }
+    const unsigned mo = (unsigned)s * MB;
+    const auto w = __builtin_amdgcn_raw_buffer_load_b64(rk, U.on ? mo & ~3u : oob, 0, 0);
+    rm[0] = w[0];
+    rm[1] = w[1];
+    rsh = (int)(mo & 3u);
+  };
+  auto split_raw = [&](const Unit &U, const float (&rx)[NX], const uint32_t (&rm)[2],
+                       int rsh, uint32_t (&sres)[PCM][6]) {
+    if (!U.on || KCNN_SKIP(128)) return;
+    const int p0 = U.p0;
+    const uint32_t mw = __builtin_amdgcn_alignbyte(rm[1], rm[0], (uint32_t)rsh);
+    float x[4];
+    unsigned mk[4];
+    short rq[4];
+    if constexpr (PH > 1) {
+      const int pq0 = p0 / PH, r0 = p0 - pq0 * PH;
+      const unsigned m0 = mw & 0xffffu, m1 = mw >> 16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool sel = r0 + q >= PH;
+        rq[q] = (short)(r0 + q - (sel ? PH : 0));
+        x[q] = sel ? rx[1] : rx[0];
+        mk[q] = p0 + q < P ? (sel ? m1 : m0) : 0u;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        rq[q] = 0;
+        x[q] = rx[q];
+        mk[q] = p0 + q < P ? (mw >> (8 * q)) & 0xffu : 0u;
+      }
+    }
+    uint32_t h01, m01, l01, h23, m23, l23;
+    split2(x[0], x[1], h01, m01, l01);
+    split2(x[2], x[3], h23, m23, l23);
+    const s16x2 w01 = __builtin_bit_cast(s16x2, mk[0] | (mk[1] << 16));
+    const s16x2 w23 = __builtin_bit_cast(s16x2, mk[2] | (mk[3] << 16));
+    const s16x2 b01 = {(short)(15 - rq[0]), (short)(15 - rq[1])};
+    const s16x2 b23 = {(short)(15 - rq[2]), (short)(15 - rq[3])};
+#pragma unroll
+    for (int c = 0; c < PCM; ++c) {
+      const s16x2 cc = {(short)(c * PH), (short)(c * PH)}, k15 = {15, 15};
+      const s16x2 sh01 = b01 - cc, sh23 = b23 - cc;
+      const uint32_t s01 = __builtin_bit_cast(uint32_t, (s16x2)((w01 << sh01) >> k15));
+      const uint32_t s23 = __builtin_bit_cast(uint32_t, (s16x2)((w23 << sh23) >> k15));
+      sres[c][0] = h01 & s01;
+      sres[c][1] = h23 & s23;
+      sres[c][2] = m01 & s01;
+      sres[c][3] = m23 & s23;
+      sres[c][4] = l01 & s01;
+      sres[c][5] = l23 & s23;
+    }
+  };
+  auto write_sres = [&](const Unit &U, const uint32_t (&sres)[PCM][6]) {
+    if (!U.on || KCNN_SKIP(32)) return;
+#pragma unroll
+    for (int c = 0; c < PCM; ++c) {
+      const int ux = (c >> 2) ? U.x1 : U.x0;
+      const int o = U.base + c * ROWB + ((ux ^ ((c & 3) << 2)) << 4);
+      *reinterpret_cast<uint2 *>(Yp + o) = make_uint2(sres[c][0], sres[c][1]);
+      *reinterpret_cast<uint2 *>(Yp + YPL + o) = make_uint2(sres[c][2], sres[c][3]);
+      *reinterpret_cast<uint2 *>(Yp + 2 * YPL + o) = make_uint2(sres[c][4], sres[c][5]);
+    }
+  };
+
+  float xv[MAXX];
+  auto load_x = [&](int n) {  // branch-free, as load_raw
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(X + (int64_t)n * xs), (short)0, CHW * 4, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < MAXX; i++)
+      xv[i] = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(rx, (unsigned)(tid + NT * i) * 4u, 0, 0));
+  };
+  auto commit_x = [&]() {
+#pragma unroll
+    for (int i = 0; i < MAXX; i++) {
+      const int e = tid + NT * i;
+      if (e < CHW) {
+        int slot = e;
+        if (!unpadded) {
+          uint32_t c, q, wi, hi;
+          g.div_HW.divmod((uint32_t)e, c, q);
+          g.div_H.divmod(q, wi, hi);
+          slot = (int)c * Hp * Wp + ((int)wi + g.pad_w) * Hp + (int)hi + g.pad_h;
+        }
+        Xs[slot] = xv[i];
+      }
+    }
+  };
+  const int khkw = g.kh * g.kw;
+  const int zax = g.kh * PZ - g.oh, zby = PZ - 1;
+  const int ZMAX = g.Kdim * PZ - 1;  // (a tap past kh reads in-bounds Z, masked off)
+  // elements tid + 256 i, i in [I0, I1), of the dgrad waves' share; a fixed
+  // trip count and buffer stores (an element past the map is stored past
+  // the row and dropped) keep the compiler's vmcnt counts exact
+  auto col2im_v = [&](int nn, int I0, int I1, auto ACCc) {
+    constexpr bool ACC = decltype(ACCc)::value;
+    const __amdgpu_buffer_rsrc_t rdx = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(dX + (int64_t)nn * dxs), (short)0, CHW * 4, 0x00020000);
+    if (c2fast) {  // two elements at a time from the tap table (same sums, same order)
+#pragma unroll 1
+      for (int i = I0; i < I1; i += 2) {
+        int e[2], t[2];
+        float v[2][8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          e[h] = tid + (NT / 2) * (i + h);
+          t[h] = ctab[min(e[h], CHW - 1)];
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int u = 0; u < 8; u++) v[h][u] = Zt[min((t[h] & 0xffff) + u * zby, ZMAX)];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ylo = (t[h] >> 16) & 15, ny = t[h] >> 20;
+          float sum = 0.0f;
+#pragma unroll
+          for (int u = 0; u < 8; u++) sum += (unsigned)(u - ylo) <= (unsigned)ny ? v[h][u] : 0.0f;
+          const unsigned off = e[h] < CHW && i + h < I1 ? (unsigned)e[h] * 4u : 0x40000000u;
+          if constexpr (ACC)
+            sum += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rdx, off, 0, 0));
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sum), rdx, off, 0, 0);
+        }
+      }
+      return;
+    }
+#pragma unroll 1
+    for (int i = I0; i < I1; i++) {
+      const int e = tid + (NT / 2) * i;
+      const int ec = min(e, CHW - 1);
+      uint32_t c, q, wi, hi;
+      g.div_HW.divmod((uint32_t)ec, c, q);
+      g.div_H.divmod(q, wi, hi);
+      const int ty = (int)hi + g.pad_h, tx = (int)wi + g.pad_w;
+      const int zb = (int)c * khkw * PZ + tx * g.oh + ty;
+      const int ylo = max(0, ty - g.oh + 1), ny = min(g.kh - 1, ty) - ylo;
+      const int xlo = max(0, tx - g.ow + 1), xhi = min(g.kw - 1, tx);
+      float sum = 0.0f;
+      for (int kx = xlo; kx <= xhi; kx++) {
+        const int zk = zb + kx * zax;
+        for (int k0 = 0; k0 < g.kh; k0 += 8) {
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) v[u] = Zt[zk + (k0 + u) * zby];
+#pragma unroll
+          for (int u = 0; u < 8; u++)
+            sum += (unsigned)(k0 + u - ylo) <= (unsigned)ny ? v[u] : 0.0f;
+        }
+      }
+      const unsigned off = e < CHW ? (unsigned)e * 4u : 0x40000000u;
+      if constexpr (ACC)  // (a runtime test here became an unconditional load + wait)
+        sum += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rdx, off, 0, 0));
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sum), rdx, off, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // one element's temporaries at a time
+    }
+  };
+  auto col2im = [&](int nn, int I0, int I1) {
+    if (dx_acc) col2im_v(nn, I0, I1, std::true_type{});
+    else col2im_v(nn, I0, I1, std::false_type{});
+  };
+
+  const bool dgrad_wave = wave < 4;
+  int my_steps = 0;
+  int stp[MAXS];
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    stp[s] = steps.s[wave][s];
+    if (!dgrad_wave && stp[s] != 0xff) my_steps = s + 1;
+  }
+  // the frame's im2col values of this wave's steps [S0, S1), split once per
+  // frame: every step's offsets (two 16-B qtab reads), then every value, then
+  // the splits, so the LDS round trips overlap (a step past my_steps reads
+  // clamped, in-bounds addresses; its planes are never used)
+  auto gather = [&](auto &a, auto S0c, auto S1c) {
+    constexpr int S0 = decltype(S0c)::value, S1 = decltype(S1c)::value;
+    constexpr int NS = S1 - S0;
+    int4 qv[NS][2];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int pbase = min(16 * stp[S0 + s] + 8 * hf, PP - 8);
+      qv[s][0] = *reinterpret_cast<const int4 *>(qtab + pbase);
+      qv[s][1] = *reinterpret_cast<const int4 *>(qtab + pbase + 4);
+    }
+    float v[NS][8];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int q[8] = {qv[s][0].x, qv[s][0].y, qv[s][0].z, qv[s][0].w,
+                        qv[s][1].x, qv[s][1].y, qv[s][1].z, qv[s][1].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t off = min((uint32_t)(abase + qmul * q[e]), amax);
+        v[s][e] = *reinterpret_cast<const float *>(Xb + off);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) split8(v[s], a[S0 + s][0], a[S0 + s][1], a[S0 + s][2]);
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using CA = std::integral_constant<int, SA>;
+  using CS = std::integral_constant<int, MAXS>;
+
+  const int n0 = blockIdx.x;
+  auto frames = [&](auto role) {
+    constexpr bool RD = decltype(role)::value == 1;  // dgrad waves
+    const Unit ua = make_unit(tid, NPQA, 0);
+    const Unit ub = make_unit(RD ? tid : NT, NPQB, HALF);
+    float rxA[NX], rxB[NX];
+    uint32_t rmA[2], rmB[2];
+    int rshA = 0, rshB = 0;
+    uint32_t sresA[PCM][6], sresB[PCM][6];
+    bf16x8 ain[RD ? 1 : MAXS][3];
+#pragma unroll
+    for (int s = 0; s < (RD ? 1 : MAXS); ++s)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) ain[s][pl] = bf16x8{};
+    // ---- prologue: frame n0's map and A-step im2col values, the A half of
+    // its first slab in the image, the B half split, slab 1's raw values
+    load_x(n0);
+    load_raw(ua, rxA, rmA, rshA, n0, 0);
+    if constexpr (RD) load_raw(ub, rxB, rmB, rshB, n0, 0);
+    __syncthreads();  // Xs zeroed, qtab and the W image written
+    commit_x();
+    if (n0 + G < g.R) load_x(n0 + G);
+    split_raw(ua, rxA, rmA, rshA, sresA);
+    if constexpr (RD) split_raw(ub, rxB, rmB, rshB, sresB);
+    load_raw(ua, rxA, rmA, rshA, n0, 1);
+    if constexpr (RD) load_raw(ub, rxB, rmB, rshB, n0, 1);
+    write_sres(ua, sresA);
+    __syncthreads();  // A(n0, 0) in the image, frame n0's map in Xs
+    if constexpr (!RD) gather(ain, C0{}, CA{});
+
+    floatx16 wacc[RD ? 1 : NCH];
+#pragma unroll
+    for (int c = 0; c < (RD ? 1 : NCH); c++) wacc[c] = zero16();
+    int nprev = -1;
+
+    for (int n = n0; n < g.R; n += G) {
+      constexpr int TT = RD ? MAXT : 1;
+      floatx16 zacc[TT];
+#pragma unroll
+      for (int t = 0; t < TT; ++t) zacc[t] = zero16();
+      auto tile_of = [&](int t) { return wave + 4 * t; };
+      // Z[p][k] += dY^T W on this wave's tiles [T0, T1): MFMA group gi = (tile
+      // gi / 2, k16 slice gi % 2), the next group's transposed reads issued
+      // before the current group's MFMAs
+      auto dgrad = [&](int ch, auto T0c, auto T1c) {
+        constexpr int T0 = decltype(T0c)::value, T1 = decltype(T1c)::value;
+        if (tile_of(T0) >= ntile) return;
+        bf16x8 wf[2][3];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            wf[s][pl] = *reinterpret_cast<const bf16x8 *>(
+                Wimg + pl * WPL + woff(l, ch * 32 + 16 * s + 8 * hf));
+        const int G4 = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+        auto load_af = [&](int gi, bf16x8 (&af)[3]) {
+          const int col = tile_of(gi >> 1) * 32 + 16 * (G4 & 1) + 4 * pp;
+          const int row = 16 * (gi & 1) + 8 * (G4 >> 1) + q;
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) {
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s16x4 *)(Yp + pl * YPL + yoff(row, col)));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s16x4 *)(Yp + pl * YPL + yoff(row + 4, col)));
+            af[pl] = __builtin_bit_cast(
+                bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          }
+        };
+        bf16x8 afb[2][3];
+        load_af(2 * T0, afb[0]);
+#pragma unroll
+        for (int gi = 2 * T0; gi < 2 * T1; ++gi) {
+          if (tile_of(gi >> 1) >= ntile) break;  // uniform
+          if (gi + 1 < 2 * T1) load_af(gi + 1, afb[(gi + 1 - 2 * T0) & 1]);  // unconditional
+          __builtin_amdgcn_sched_barrier(0);
+          if (!KCNN_SKIP(64))
+            zacc[gi >> 1] = mfma6(afb[(gi - 2 * T0) & 1], wf[gi & 1], zacc[gi >> 1]);
+        }
+      };
+      // gW[k][g] += im2col(X) dY^T over this wave's k16 steps [S0, S1) (the
+      // next step's row reads issued before the current step's MFMAs; the
+      // lane part of the address passes through an opaque move, so the
+      // compiler does not hoist per-step addresses out of the frame loop)
+      auto wgrad = [&](int ch, auto S0c, auto S1c) {
+        constexpr int S0 = decltype(S0c)::value, S1 = decltype(S1c)::value;
+        if (S0 >= my_steps) return;
+        int lx, lrow;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(lx) : "v"((hf ^ swz4(l)) << 4));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(lrow) : "v"(l * ROWB));
+        auto load_bf = [&](int s, bf16x8 (&bf)[3]) {
+          const int off = lrow + ((stp[s] >> 3) << 8) + (((stp[s] & 7) << 5) ^ lx);
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            bf[pl] = *reinterpret_cast<const bf16x8 *>(Yp + pl * YPL + off);
+        };
+        bf16x8 bfb[2][3];
+        load_bf(S0, bfb[0]);
+#pragma unroll
+        for (int s = S0; s < S1; ++s) {
+          if (s >= my_steps) break;
+          // the prefetch is unconditional (a step past my_steps reads unused
+          // in-bounds LDS): a branch here would make the compiler's LDS wait
+          // counts at the MFMAs conservative and serialise the reads
+          if (s + 1 < S1) load_bf(s + 1, bfb[(s + 1 - S0) & 1]);
+          __builtin_amdgcn_sched_barrier(0);  // the next step's reads stay ahead of these MFMAs
+          if (!KCNN_SKIP(64)) wacc[ch] = mfma6(ain[s], bfb[(s - S0) & 1], wacc[ch]);
+        }
+      };
+      auto store_z = [&]() {
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+          const int pt = tile_of(t);
+          if (pt >= ntile) break;
+          if (l < g.Kdim) {
+            float *zr = Zt + l * PZ + pt * 32 + 4 * hf;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+              *reinterpret_cast<float4 *>(zr + 8 * i) =
+                  make_float4(zacc[t][4 * i], zacc[t][4 * i + 1], zacc[t][4 * i + 2],
+                              zacc[t][4 * i + 3]);
+          }
+        }
+      };
+#pragma unroll
+      for (int ch = 0; ch < NCH; ch++) {
+        const int n1 = ch + 1 < NCH ? n : n + G;
+        const int n2 = ch + 2 < NCH ? n : n + G, c2 = ch + 2 < NCH ? ch + 2 : ch + 2 - NCH;
+        const bool next = n1 < g.R;
+        KCNN_TMARK(5 * ch + 4)
+        // ---- P_A(t): half A's MFMAs; slab t's B planes -> image; A(t+1) split
+        if constexpr (RD) {
+          write_sres(ub, sresB);
+          // the previous frame's dX (its Z went to LDS before the last Bb;
+          // this frame's store of Z is in P_B of its last slab), here where
+          // the fewest registers are live, beside the wgrad waves' MFMAs
+          if (nprev >= 0 && !KCNN_SKIP(256 | 1024)) {  // spread over the frame's P_A phases
+            constexpr int PER = (MAXC + NCH - 1) / NCH;
+            col2im(nprev, ch * PER, min((ch + 1) * PER, MAXC));
+          }
+          if (next) {
+            split_raw(ua, rxA, rmA, rshA, sresA);
+            load_raw(ua, rxA, rmA, rshA, min(n2, g.R - 1), c2);
+          }
+          dgrad(ch, std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{});
+        } else {
+          wgrad(ch, C0{}, CA{});
+          if (next) {
+            split_raw(ua, rxA, rmA, rshA, sresA);
+            load_raw(ua, rxA, rmA, rshA, min(n2, g.R - 1), c2);
+          }
+          // frame n's B-step values (their last reader: P_B of frame n - G's
+          // last slab; Xs holds frame n's map until P_B of this slab)
+          if (ch == 0 && !KCNN_SKIP(256 | 512)) gather(ain, CA{}, CS{});
+        }
+        KCNN_TMARK(5 * ch + 0)
+        __syncthreads();  // Ba: half A of slab t read, its B half published
+        KCNN_TMARK(5 * ch + 1)
+        // ---- P_B(t): half B's MFMAs; A(t+1) -> image; B(t+1) split
+        if (next) write_sres(ua, sresA);
+        if constexpr (RD) {
+          if (next) {
+            split_raw(ub, rxB, rmB, rshB, sresB);
+            load_raw(ub, rxB, rmB, rshB, min(n2, g.R - 1), c2);
+          }
+          dgrad(ch, std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{});
+          if (ch == NCH - 1 && !KCNN_SKIP(256)) store_z();
+        } else {
+          wgrad(ch, CA{}, CS{});
+          // the next frame's A-step values (their last reader was P_A of this
+          // slab; its map went to Xs in P_B of the first slab)
+          if (ch == NCH - 1 && n + G < g.R && !KCNN_SKIP(256 | 512)) gather(ain, C0{}, CA{});
+        }
+        if (ch == 0) {
+          if (n + G < g.R) commit_x();
+          load_x(min(n + 2 * G, g.R - 1));  // unconditional (a clamped frame: unused)
+        }
+        KCNN_TMARK(5 * ch + 2)
+        __syncthreads();  // Bb: slab t read, A(t+1) published
+        KCNN_TMARK(5 * ch + 3)
+      }
+      nprev = n;
+    }
+    if (RD && nprev >= 0) col2im(nprev, 0, MAXC);  // the last frame's Z (stored before the last Bb)
+#ifdef KCNN_PHASE_TIMING
+    if ((dbg & 16) && blockIdx.x == 0 && lane == 0)
+      for (int c = 0; c < NCH; ++c)
+        printf("bwdx6q wave %d ch %d: PA %lld Ba %lld PB %lld Bb %lld top %lld\n", wave, c,
+               tm[5 * c], tm[5 * c + 1], tm[5 * c + 2], tm[5 * c + 3], tm[5 * c + 4]);
+#endif
+    const int E = (g.Kdim + 1) * g.G;
+    float *dst = ws_part + (int64_t)blockIdx.x * E;
+    float *red = reinterpret_cast<float *>(Yp);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++) {
+      __syncthreads();
+      if constexpr (!RD) {
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+          red[(wave - 4) * 1024 + mfma32_row(r, lane) * 32 + l] = wacc[ch][r];
+      }
+      __syncthreads();
+      for (int e = tid; e < 1024; e += NT) {
+        const int i = e >> 5, j = e & 31;
+        if (i > g.Kdim) continue;
+        float sum = 0.0f;
+#pragma unroll
+        for (int w = 0; w < 4; w++) sum += red[w * 1024 + e];
+        dst[i * g.G + ch * 32 + j] = sum;
+      }
+    }
+  };
+  if (dgrad_wave) frames(std::integral_constant<int, 1>{});
+  else frames(std::integral_constant<int, 2>{});
+#undef KCNN_TMARK
+#undef KCNN_SKIP
+}
+
+size_t x6q_lds(const ConvGeom &g);
 size_t x6p_lds(const ConvGeom &g) {
   const int CHWp = g.C * (g.H + 2 * g.pad_h) * (g.W + 2 * g.pad_w);
   return (size_t)3 * YPL + 3 * WPL + (size_t)g.Kdim * PZ * 4 +
          (size_t)round4(CHWp + 1) * 4 + (size_t)PP * 4;
 }
+
+// conv_bwd_x6q_kernel: x6p's plan and the col2im tap table
+size_t x6q_lds(const ConvGeom &g) { return x6p_lds(g) + (size_t)round4(g.C * g.HW) * 4; }
 
 size_t x6_lds(const ConvGeom &g, bool dx, int pc, int ph) {
   const int CHWp = g.C * (g.H + 2 * g.pad_h) * (g.W + 2 * g.pad_w);
@@ -1124,18 +1713,23 @@ int kcnn_conv_bwd_x6(const ConvGeom &g, const float *X, int xs, const float *dY,
   // the software-pipelined kernel for the pooled backward with both outputs
   // (bitwise the same results); KCNN_BWD_X6P=0 (experiment build) keeps
   // conv_bwd_x6_kernel for it too
-  static const int pipelined = KCNN_KNOB("KCNN_BWD_X6P", 1);
-  if (pipelined && dx && wg && pc > 0 && g.G >= 64 && x6p_lds(g) <= (size_t)160 * 1024) {
-    const size_t lds = x6p_lds(g);
-#define KCNN_X6PP(NCH, PCM, PH)                                                              \
-  do {                                                                                       \
-    static bool attr = hipFuncSetAttribute(                                                 \
-        reinterpret_cast<const void *>(&conv_bwd_x6p_kernel<NCH, PCM, PH>),                  \
-        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;               \
-    (void)attr;                                                                              \
-    hipLaunchKernelGGL((conv_bwd_x6p_kernel<NCH, PCM, PH>), dim3(S), dim3(NT), lds, st, g, X, \
-                       xs, dY, dys, K, ks, dX, dxs, ws_part, ZZ, tab, dx_acc, pmask, pms,    \
-                       dbg);                                                                 \
+  static const int pipelined = KCNN_KNOB("KCNN_BWD_X6P", 2);
+  const size_t plds = pipelined == 1 ? x6p_lds(g) : x6q_lds(g);
+  if (pipelined && dx && wg && pc > 0 && g.G >= 64 && plds <= (size_t)160 * 1024) {
+    const size_t lds = plds;
+#define KCNN_X6PK(KER, NCH, PCM, PH)                                                       \
+  do {                                                                                     \
+    static bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&KER<NCH, PCM, PH>), \
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,      \
+                                           160 * 1024) == hipSuccess;                       \
+    (void)attr;                                                                            \
+    hipLaunchKernelGGL((KER<NCH, PCM, PH>), dim3(S), dim3(NT), lds, st, g, X, xs, dY, dys, K, \
+                       ks, dX, dxs, ws_part, ZZ, tab, dx_acc, pmask, pms, dbg);            \
+  } while (0)
+#define KCNN_X6PP(NCH, PCM, PH)                                \
+  do {                                                         \
+    if (pipelined == 1) KCNN_X6PK(conv_bwd_x6p_kernel, NCH, PCM, PH); \
+    else KCNN_X6PK(conv_bwd_x6q_kernel, NCH, PCM, PH);         \
   } while (0)
 #define KCNN_X6PM(NCH)                                      \
   do {                                                      \
@@ -1152,6 +1746,7 @@ int kcnn_conv_bwd_x6(const ConvGeom &g, const float *X, int xs, const float *dY,
     }
 #undef KCNN_X6PM
 #undef KCNN_X6PP
+#undef KCNN_X6PK
     return (int)hipGetLastError();
   }
   const size_t lds = x6_lds(g, dx, pc, ph);

@@ -1091,8 +1091,17 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6p_kernel(
 // is behind a barrier: the wgrad waves gather the next frame's A-step
 // im2col values in P_B of the last slab and its B-step values in P_A of the
 // first; the next frame's map goes to Xs in P_B of the first slab; the
-// previous frame's col2im runs in the second slab (P_B, or P_A when NCH = 2,
-// ahead of the last slab's store of Z).
+// dgrad waves col2im the previous frame over P_A of every slab (from a
+// per-element tap table, ahead of the last slab's store of Z; on the wgrad
+// waves instead it measured 205 against 174 us).
+//
+// The steady-state loop issues its global loads and stores on every path
+// (buffer loads and stores past the buffer's range stand in for the lanes
+// and frames that have none): a load or store under a branch, or in a loop
+// of unknown trip count, leaves the compiler unsure how many vector-memory
+// operations are younger than the one a split waits for, and it then waits
+// for all of them (vmcnt(0)), the prefetch just issued included.  For the
+// same reason a phase issues its dX stores before its raw-value loads.
 template <int NCH, int PCM, int PH>
 __global__ __launch_bounds__(NT, 1) void conv_bwd_x6q_kernel(
     ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ dP, int dps,

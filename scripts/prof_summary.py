@@ -22,6 +22,7 @@ import shutil
 # hot-path kernel (regex on the demangled name) -> bench.py kernel-table key;
 # first match wins
 HOT = [
+    (r"conv_bwd_x6[pq]_kernel", "conv_bwd_pooled"),
     (r"conv_bwd_x6_kernel<\d+, \w+, \w+, [48](, \d)?>", "conv_bwd_pooled"),
     (r"conv_bwd_x6_kernel", "conv_bwd_fused"),
     (r"conv_bwd_dma_kernel<\d+, \w+, \w+, [48]>", "conv_bwd_pooled"),

@@ -281,6 +281,215 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6_kernel(GemmX6Args p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// gemm_x6d_kernel: gemm_x6_kernel (same tiles, images, MFMA order: bitwise the
+// same C) with its operand prefetch two K steps deep instead of one.  In
+// gemm_x6_kernel the loads of tile t+2 go out at the end of step t and are
+// split during step t+1, about 1.3 us later: an HBM miss under full load can
+// take longer (rocprofv3: 40-54 % MFMA busy at 2.0-2.2 GHz on the c2 FC
+// shapes).  Here tile t+3 is loaded at the end of step t into the register
+// set that the split of step t just freed, so each load has two steps.  The
+// loads are buffer loads with no branch (a row past the matrix, or a step
+// past the split, reads past the buffer or re-reads the last tile), so every
+// path issues the same loads and the compiler's vmcnt wait before a split
+// counts exactly the later tile's loads instead of waiting for all of them.
+// Needs whole BK steps (K % BK == 0) and the workgroup's offsets below 2^31
+// (the host checks, as for the fast kernel).
+template <int R, bool KC>
+struct TileLoaderD {
+  static constexpr int KPT = KC ? 8 : R * BK / NT;
+  static constexpr int UNITS = KC ? R * 4 : R * BK / KPT;
+  static constexpr int UPT = (UNITS + NT - 1) / NT;
+  static_assert(UNITS % NT == 0 && KPT % 8 == 0, "tile shape");
+  float v[UPT][KPT];
+
+  // base: KC, the tile's first row (src + row0 * ld); !KC, the split's first
+  // k and the tile's first column (src + kbeg * ld + row0)
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, int ld, int vrows, int kk,
+                                       int tid) {
+    constexpr unsigned OOB = 0x80000000u;
+#pragma unroll
+    for (int u = 0; u < UPT; ++u) {
+      const int unit = tid + u * NT;
+      if constexpr (KC) {
+        const int r = unit >> 2, k = kk + (unit & 3) * 8;
+        const unsigned off = r < vrows ? (unsigned)(r * ld + k) * 4u : OOB;
+        const auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+        const auto b = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16u, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[u][j] = __uint_as_float(a[j]);
+          v[u][4 + j] = __uint_as_float(b[j]);
+        }
+      } else {
+        const int r = unit % R, k = kk + (unit / R) * KPT;
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+          const unsigned off = r < vrows ? (unsigned)((k + j) * ld + r) * 4u : OOB;
+          v[u][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+        }
+      }
+    }
+  }
+
+  template <int PL>
+  __device__ __forceinline__ void store(char *lds, int tid) const {
+#pragma unroll
+    for (int u = 0; u < UPT; ++u) {
+      const int unit = tid + u * NT;
+      int r, c0;
+      if constexpr (KC) {
+        r = unit >> 2;
+        c0 = unit & 3;
+      } else {
+        r = unit % R;
+        c0 = (unit / R) * (KPT / 8);
+      }
+#pragma unroll
+      for (int cc = 0; cc < KPT / 8; ++cc) {
+        uint4 h, m, l;
+        split8(&v[u][cc * 8], h, m, l);
+        const int off = swz(r, c0 + cc);
+        *reinterpret_cast<uint4 *>(lds + off) = h;
+        *reinterpret_cast<uint4 *>(lds + PL + off) = m;
+        *reinterpret_cast<uint4 *>(lds + 2 * PL + off) = l;
+      }
+    }
+  }
+};
+
+template <bool A_KC, bool B_KC>
+__global__ __launch_bounds__(NT, 1) void gemm_x6d_kernel(GemmX6Args p) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, q = nb >> 3, rr = nb & 7;
+  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
+  const int split = lid % p.ksplit;
+  const int rest = lid / p.ksplit;
+  const int tn = rest % p.tiles_n, tm = rest / p.tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const int kbeg = split * p.kps;
+  const int kend = min(p.K, kbeg + p.kps);
+  const int T = kend > kbeg ? (kend - kbeg) / BK : 0;
+
+  const float *baseA = A_KC ? p.A + (int64_t)row0 * p.lda : p.A + (int64_t)kbeg * p.lda + row0;
+  const float *baseB = B_KC ? p.B + (int64_t)col0 * p.ldb : p.B + (int64_t)kbeg * p.ldb + col0;
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc((void *)baseA, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc((void *)baseB, (short)0, 0x7fffffff, 0x00020000);
+  const int vra = p.M - row0, vrb = p.N - col0;
+  // k of tile t relative to the base (clamped to the last tile: a re-read)
+  auto kk = [&](int t, bool kc) { return (kc ? kbeg : 0) + min(t, T - 1) * BK; };
+
+  TileLoaderD<BM, A_KC> la[2];
+  TileLoaderD<BN, B_KC> lb[2];
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) acc[i][j][g] = 0.0f;
+  if (T == 0) goto epilogue;
+
+  la[0].load(rsA, p.lda, vra, kk(0, A_KC), tid);
+  lb[0].load(rsB, p.ldb, vrb, kk(0, B_KC), tid);
+  la[0].template store<A_PLANE>(lds, tid);
+  lb[0].template store<B_PLANE>(lds + 3 * A_PLANE, tid);
+  la[1].load(rsA, p.lda, vra, kk(1, A_KC), tid);
+  lb[1].load(rsB, p.ldb, vrb, kk(1, B_KC), tid);
+  // tile 1's loads before tile 2's, as at every later loop entry (the vmcnt
+  // wait before tile 1's split then leaves tile 2's loads in flight)
+  __builtin_amdgcn_sched_barrier(0);
+  la[0].load(rsA, p.lda, vra, kk(2, A_KC), tid);
+  lb[0].load(rsB, p.ldb, vrb, kk(2, B_KC), tid);
+  __syncthreads();
+  {
+    const int ar = wm * 64 + (lane & 31), br = wn * 64 + (lane & 31);
+    const int half = lane >> 5;
+    auto half_step = [&](const char *bufA, int s) {
+      const char *bufB = bufA + 3 * A_PLANE;
+      bf16x8 a[2][3], bb[2][3];
+      const int c = 2 * s + half;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          a[i][pl] = *reinterpret_cast<const bf16x8 *>(bufA + pl * A_PLANE + swz(ar + 32 * i, c));
+          bb[i][pl] = *reinterpret_cast<const bf16x8 *>(bufB + pl * B_PLANE + swz(br + 32 * i, c));
+        }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x16 x = acc[i][j];
+          x = mfma(a[i][2], bb[j][0], x);  // lh
+          x = mfma(a[i][0], bb[j][2], x);  // hl
+          x = mfma(a[i][1], bb[j][1], x);  // mm
+          x = mfma(a[i][1], bb[j][0], x);  // mh
+          x = mfma(a[i][0], bb[j][1], x);  // hm
+          x = mfma(a[i][0], bb[j][0], x);  // hh
+          acc[i][j] = x;
+        }
+    };
+    // waves 4-7 split the next tile between their two MFMA halves, waves
+    // 0-3 after both (gemm_x6_kernel's stagger)
+    const bool late = wave < 4;
+    // step t: tile t+1 is in set (t+1) & 1, which then takes tile t+3
+    // (a step past T, the second of the last pair when T is odd, does no
+    // MFMAs but still issues its (clamped) loads: every path then issues the
+    // same loads, so the loop header's vmcnt state is known and each split
+    // waits only for its own tile)
+    auto step = [&](int t, auto &lan, auto &lbn) {
+      if (t < T) {
+        const char *buf = lds + (t & 1) * BUF;
+        char *nA = lds + ((t + 1) & 1) * BUF;
+        half_step(buf, 0);
+        if (!late && t + 1 < T) {
+          lan.template store<A_PLANE>(nA, tid);
+          lbn.template store<B_PLANE>(nA + 3 * A_PLANE, tid);
+        }
+        half_step(buf, 1);
+        if (late && t + 1 < T) {
+          lan.template store<A_PLANE>(nA, tid);
+          lbn.template store<B_PLANE>(nA + 3 * A_PLANE, tid);
+        }
+      }
+      lan.load(rsA, p.lda, vra, kk(t + 3, A_KC), tid);
+      lbn.load(rsB, p.ldb, vrb, kk(t + 3, B_KC), tid);
+      __syncthreads();
+    };
+    for (int t = 0; t < T; t += 2) {
+      step(t, la[1], lb[1]);
+      step(t + 1, la[0], lb[0]);
+    }
+  }
+epilogue:
+  float *out = p.partial ? p.C + (int64_t)split * p.M * p.N : p.C;
+  const int ldo = p.partial ? p.N : p.ldc;
+  const int half2 = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = col0 + wn * 64 + j * 32 + (lane & 31);
+      if (col >= p.N) continue;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int row = row0 + wm * 64 + i * 32 + (g & 3) + 8 * (g >> 2) + 4 * half2;
+        if (row >= p.M) continue;
+        float *o = out + (int64_t)row * ldo + col;
+        if (p.partial) *o = acc[i][j][g];
+        else *o = p.beta == 0.0f ? p.alpha * acc[i][j][g]
+                                 : p.alpha * acc[i][j][g] + p.beta * *o;
+      }
+    }
+}
+
 // C = alpha * sum_s part[s] + beta * C, the splits added in increasing s
 __global__ void gemm_x6_reduce_kernel(const float *__restrict__ part, int S, int M,
                                       int N, float alpha, float beta, float *C,
@@ -695,6 +904,11 @@ bool fast_enabled() {
   static const bool on = KCNN_KNOB("KCNN_X6_FAST", 0) != 0;
   return on;
 }
+// KCNN_X6_DEEP=0 (experiment build): gemm_x6_kernel's one-step prefetch
+bool deep_enabled() {
+  static const bool on = KCNN_KNOB("KCNN_X6_DEEP", 1) != 0;
+  return on;
+}
 
 // ---------------------------------------------------------------------------
 // Plane GEMM: both operands already split into their three bf16 planes in
@@ -944,6 +1158,17 @@ void launch_x6(const GemmX6Args &a, unsigned blocks, hipStream_t st) {
   else launch_x6_t<A_KC, B_KC, false>(a, blocks, st);
 }
 
+template <bool A_KC, bool B_KC>
+void launch_x6d(const GemmX6Args &a, unsigned blocks, hipStream_t st) {
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_x6d_kernel<A_KC, B_KC>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               LDS_BYTES) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((gemm_x6d_kernel<A_KC, B_KC>), dim3(blocks), dim3(NT), LDS_BYTES, st, a);
+}
+
 // K splits for a tile count: the fraction of the last wave of workgroups
 // that is busy, less a small charge per extra split (partials + reduction)
 int choose_ksplit(int64_t tiles, int K) {
@@ -1004,6 +1229,11 @@ extern "C" int kl_gemm_x6(int transA, int transB, int M, int N, int K, float alp
     if (kc) return (int64_t)R * ld * 4 + (int64_t)K * 4 < ((int64_t)1 << 31);
     return rows % 4 == 0 && (int64_t)(a.kps + 1) * ld * 4 < ((int64_t)1 << 31);
   };
+  // two-deep prefetch kernel: whole BK steps, the workgroup's offsets below 2^31
+  auto deep_fits = [&](bool kc, int ld, int R) {
+    if (kc) return (int64_t)R * ld * 4 + (int64_t)K * 4 < ((int64_t)1 << 31);
+    return (int64_t)(a.kps + 1) * ld * 4 + (int64_t)R * 4 < ((int64_t)1 << 31);
+  };
   if (fast_enabled() && K % BK == 0 && fits(a_kc, A, lda, M, BM) &&
       fits(b_kc, B, ldb, N, BN)) {
     GemmFastArgs f;
@@ -1015,6 +1245,12 @@ extern "C" int kl_gemm_x6(int transA, int transB, int M, int N, int K, float alp
     else if (a_kc) launch_fast<true, false>(f, (unsigned)nb, st);
     else if (b_kc) launch_fast<false, true>(f, (unsigned)nb, st);
     else launch_fast<false, false>(f, (unsigned)nb, st);
+  } else if (deep_enabled() && K % BK == 0 && deep_fits(a_kc, lda, BM) &&
+             deep_fits(b_kc, ldb, BN)) {
+    if (a_kc && b_kc) launch_x6d<true, true>(a, (unsigned)nb, st);
+    else if (a_kc) launch_x6d<true, false>(a, (unsigned)nb, st);
+    else if (b_kc) launch_x6d<false, true>(a, (unsigned)nb, st);
+    else launch_x6d<false, false>(a, (unsigned)nb, st);
   } else if (a_kc && b_kc) launch_x6<true, true>(a, (unsigned)nb, st);
   else if (a_kc) launch_x6<true, false>(a, (unsigned)nb, st);
   else if (b_kc) launch_x6<false, true>(a, (unsigned)nb, st);

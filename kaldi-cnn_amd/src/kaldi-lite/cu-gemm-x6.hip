@@ -358,7 +358,7 @@ struct TileLoaderD {
   }
 };
 
-template <bool A_KC, bool B_KC>
+template <bool A_KC, bool B_KC, int DEPTH>
 __global__ __launch_bounds__(NT, 1) void gemm_x6d_kernel(GemmX6Args p) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x;
@@ -385,8 +385,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6d_kernel(GemmX6Args p) {
   // k of tile t relative to the base (clamped to the last tile: a re-read)
   auto kk = [&](int t, bool kc) { return (kc ? kbeg : 0) + min(t, T - 1) * BK; };
 
-  TileLoaderD<BM, A_KC> la[2];
-  TileLoaderD<BN, B_KC> lb[2];
+  TileLoaderD<BM, A_KC> la[DEPTH];
+  TileLoaderD<BN, B_KC> lb[DEPTH];
   f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -400,13 +400,15 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6d_kernel(GemmX6Args p) {
   lb[0].load(rsB, p.ldb, vrb, kk(0, B_KC), tid);
   la[0].template store<A_PLANE>(lds, tid);
   lb[0].template store<B_PLANE>(lds + 3 * A_PLANE, tid);
-  la[1].load(rsA, p.lda, vra, kk(1, A_KC), tid);
-  lb[1].load(rsB, p.ldb, vrb, kk(1, B_KC), tid);
-  // tile 1's loads before tile 2's, as at every later loop entry (the vmcnt
-  // wait before tile 1's split then leaves tile 2's loads in flight)
-  __builtin_amdgcn_sched_barrier(0);
-  la[0].load(rsA, p.lda, vra, kk(2, A_KC), tid);
-  lb[0].load(rsB, p.ldb, vrb, kk(2, B_KC), tid);
+  // tiles 1..DEPTH into sets 1, .., 0 in order, as at every later loop entry
+  // (the vmcnt wait before tile 1's split then leaves the later tiles' loads
+  // in flight)
+#pragma unroll
+  for (int j = 1; j <= DEPTH; ++j) {
+    __builtin_amdgcn_sched_barrier(0);
+    la[j % DEPTH].load(rsA, p.lda, vra, kk(j, A_KC), tid);
+    lb[j % DEPTH].load(rsB, p.ldb, vrb, kk(j, B_KC), tid);
+  }
   __syncthreads();
   {
     const int ar = wm * 64 + (lane & 31), br = wn * 64 + (lane & 31);
@@ -439,8 +441,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6d_kernel(GemmX6Args p) {
     // waves 4-7 split the next tile between their two MFMA halves, waves
     // 0-3 after both (gemm_x6_kernel's stagger)
     const bool late = wave < 4;
-    // step t: tile t+1 is in set (t+1) & 1, which then takes tile t+3
-    // (a step past T, the second of the last pair when T is odd, does no
+    // step t: tile t+1 is in set (t+1) % DEPTH, which then takes tile
+    // t+1+DEPTH (a step past T, in the last group of DEPTH steps, does no
     // MFMAs but still issues its (clamped) loads: every path then issues the
     // same loads, so the loop header's vmcnt state is known and each split
     // waits only for its own tile)
@@ -459,13 +461,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_x6d_kernel(GemmX6Args p) {
           lbn.template store<B_PLANE>(nA + 3 * A_PLANE, tid);
         }
       }
-      lan.load(rsA, p.lda, vra, kk(t + 3, A_KC), tid);
-      lbn.load(rsB, p.ldb, vrb, kk(t + 3, B_KC), tid);
+      lan.load(rsA, p.lda, vra, kk(t + 1 + DEPTH, A_KC), tid);
+      lbn.load(rsB, p.ldb, vrb, kk(t + 1 + DEPTH, B_KC), tid);
       __syncthreads();
     };
-    for (int t = 0; t < T; t += 2) {
-      step(t, la[1], lb[1]);
-      step(t + 1, la[0], lb[0]);
+    for (int t = 0; t < T; t += DEPTH) {
+#pragma unroll
+      for (int i = 0; i < DEPTH; ++i) step(t + i, la[(i + 1) % DEPTH], lb[(i + 1) % DEPTH]);
     }
   }
 epilogue:
@@ -1158,15 +1160,23 @@ void launch_x6(const GemmX6Args &a, unsigned blocks, hipStream_t st) {
   else launch_x6_t<A_KC, B_KC, false>(a, blocks, st);
 }
 
-template <bool A_KC, bool B_KC>
-void launch_x6d(const GemmX6Args &a, unsigned blocks, hipStream_t st) {
+template <bool A_KC, bool B_KC, int DEPTH>
+void launch_x6d_t(const GemmX6Args &a, unsigned blocks, hipStream_t st) {
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_x6d_kernel<A_KC, B_KC>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                               LDS_BYTES) == hipSuccess;
+    return hipFuncSetAttribute(
+               reinterpret_cast<const void *>(&gemm_x6d_kernel<A_KC, B_KC, DEPTH>),
+               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_x6d_kernel<A_KC, B_KC>), dim3(blocks), dim3(NT), LDS_BYTES, st, a);
+  hipLaunchKernelGGL((gemm_x6d_kernel<A_KC, B_KC, DEPTH>), dim3(blocks), dim3(NT), LDS_BYTES,
+                     st, a);
+}
+// prefetch depth 2; KCNN_X6_DEEP=2 (experiment build) selects depth 3
+template <bool A_KC, bool B_KC>
+void launch_x6d(const GemmX6Args &a, unsigned blocks, hipStream_t st) {
+  static const int depth = KCNN_KNOB("KCNN_X6_DEEP", 1);
+  if (depth == 2) launch_x6d_t<A_KC, B_KC, 3>(a, blocks, st);
+  else launch_x6d_t<A_KC, B_KC, 2>(a, blocks, st);
 }
 
 // K splits for a tile count: the fraction of the last wave of workgroups

@@ -49,6 +49,10 @@ STACKS = {
     "win_2x2x2": (9, 8, 2, 2, 1, 64, 2, 8, 0, 0, 2, 2),
     "win_2x1x8_pad": (6, 6, 1, 3, 3, 32, 8, 8, 1, 1, 2, 1),
     "win_2x1x4_G96": (10, 6, 2, 3, 2, 96, 4, 8, 0, 0, 2, 1),
+    # the position-half pooled backward (conv_bwd_x6q_kernel) with a B half
+    # (P > 256) at 2 and 3 slabs per frame, PCM = 8 and a 2 x 1 x 4 window
+    "halfB_G64_pc8": (40, 9, 1, 8, 1, 64, 8, 8, 0, 0),
+    "halfB_G96_2x1x4": (34, 10, 2, 3, 2, 96, 4, 8, 0, 0, 2, 1),
     # long kernels (implicit GEMM, the pool in its epilogue): c5's C3 -> P2
     # shape class, nnet.config's conv4 -> Maxpool(1x2x1), and pc = 2
     "long_2x1x4_pad": (8, 9, 16, 3, 3, 256, 4, 8, 1, 1, 2, 1),
@@ -148,7 +152,8 @@ def test_unstored_conv_output_after_backprop(kc):
             kc.set_fusion(1)
 
 
-@pytest.mark.parametrize("name", ["c2", "pc2_G96", "pc8_G64", "c5_P1_3x1x4", "win_2x1x8_pad"])
+@pytest.mark.parametrize("name", ["c2", "pc2_G96", "pc8_G64", "c5_P1_3x1x4", "win_2x1x8_pad",
+                                  "halfB_G64_pc8", "halfB_G96_2x1x4"])
 def test_fusion_exact_gradient_mode(kc, name):
     a = run(kc, STACKS[name], fused=True, mode=1)
     b = run(kc, STACKS[name], fused=False, mode=1)
@@ -188,8 +193,8 @@ def test_pooled_backward_path(kc, name, pooled):
     assert (after > before) == pooled
 
 
-@pytest.mark.parametrize("name", ["c2", "c5_P1_3x1x4", "win_2x1x8_pad", "win_2x1x4_G96"] +
-                         LONG_POOLED)
+@pytest.mark.parametrize("name", ["c2", "c5_P1_3x1x4", "win_2x1x8_pad", "win_2x1x4_G96",
+                                  "halfB_G64_pc8", "halfB_G96_2x1x4"] + LONG_POOLED)
 @pytest.mark.parametrize("ties", [False, True])
 def test_fused_pool_matches_oracle(kc, name, ties):
     cfg = STACKS[name]

@@ -1089,8 +1089,9 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6p_kernel(
 // pooled row u / 64) belongs to thread u, B unit u (positions 256 + ...) to
 // dgrad-wave thread u.  Frame work sits where an accumulator's last reader
 // is behind a barrier: the wgrad waves gather the next frame's A-step
-// im2col values in P_B of the last slab and its B-step values in P_A of the
-// first; the next frame's map goes to Xs in P_B of the first slab; the
+// im2col values in P_A of the last slab, behind that phase's MFMAs on them
+// (KCNN_X6Q_GA of them; the rest in its P_B), and its B-step values in P_A
+// of the first; the next frame's map goes to Xs in P_B of the first slab; the
 // dgrad waves col2im the previous frame over P_A of every slab (from a
 // per-element tap table, ahead of the last slab's store of Z; on the wgrad
 // waves instead it measured 205 against 174 us).
@@ -1443,6 +1444,15 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6q_kernel(
   using C0 = std::integral_constant<int, 0>;
   using CA = std::integral_constant<int, SA>;
   using CS = std::integral_constant<int, MAXS>;
+  // A steps of the next frame gathered in P_A of the last slab, the rest in
+  // its P_B (c2 pooled backward, 3 runs each: 0 178.5 us, 1 179.1, 2 176.7,
+  // 4 174.6; moving the dgrad waves' col2im shares to P_B measured 184.5)
+#ifndef KCNN_X6Q_GA
+#define KCNN_X6Q_GA 4
+#endif
+  constexpr int GA = KCNN_X6Q_GA;
+  static_assert(GA >= 0 && GA <= SA, "A-step gather split");
+  using CGA = std::integral_constant<int, GA>;
 
   const int n0 = blockIdx.x;
   auto frames = [&](auto role) {
@@ -1597,6 +1607,11 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6q_kernel(
           // frame n's B-step values (their last reader: P_B of frame n - G's
           // last slab; Xs holds frame n's map until P_B of this slab)
           if (ch == 0 && !KCNN_SKIP(256 | 512)) gather(ain, CA{}, CS{});
+          // the next frame's first GA A-step values, behind this phase's MFMAs
+          // on them (Xs has held the next frame's map since P_B of the first
+          // slab): the wgrad waves' P_A is the shorter of the two roles'
+          if constexpr (GA > 0)
+            if (ch == NCH - 1 && n + G < g.R && !KCNN_SKIP(256 | 512)) gather(ain, C0{}, CGA{});
         }
         KCNN_TMARK(5 * ch + 0)
         __syncthreads();  // Ba: half A of slab t read, its B half published
@@ -1612,9 +1627,10 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6q_kernel(
           if (ch == NCH - 1 && !KCNN_SKIP(256)) store_z();
         } else {
           wgrad(ch, CA{}, CS{});
-          // the next frame's A-step values (their last reader was P_A of this
-          // slab; its map went to Xs in P_B of the first slab)
-          if (ch == NCH - 1 && n + G < g.R && !KCNN_SKIP(256 | 512)) gather(ain, C0{}, CA{});
+          // the next frame's other A-step values (their last reader was P_A
+          // of this slab; its map went to Xs in P_B of the first slab)
+          if constexpr (GA < SA)
+            if (ch == NCH - 1 && n + G < g.R && !KCNN_SKIP(256 | 512)) gather(ain, CGA{}, CA{});
         }
         if (ch == 0) {
           if (n + G < g.R) commit_x();

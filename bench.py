@@ -151,24 +151,29 @@ def parse_profile(text):
 
 
 def cpu_baseline(frames_hint, budget_s=12.0):
-    """The CPU oracle (restated reference CPU path): one full c2 step of
-    `frames_hint` frames (at most 4096) on this GPU job's CPU share, and a
-    bounded sample on one thread."""
+    """The reference's CPU path, restated by the C oracle: one full c2 step of
+    `frames_hint` frames (at most 4096) on this GPU job's CPU share, and
+    bounded samples on one thread and on every CPU of the process's affinity.
+    The AddMatMat legs (Conv2D's im2col GEMM, conv2D.cc:138-139; the FC GEMMs,
+    nnet-component.cc:1227, :1247, nnet-component-nnet0.cc:1141) run on
+    OpenBLAS sgemm, as upstream Kaldi's CPU AddMatMat runs on CBLAS; im2col,
+    col2im, the reshapes and the maxpool loops are the reference's own CPU
+    branches."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     # 16 threads: this GPU's share of the box's host CPUs.  The box exposes
-    # every thread of a shared 8-GPU host (nproc = 256 on a 64-core EPYC), but
-    # a one-GPU job is allotted 16 (OMP_NUM_THREADS there); running the oracle
-    # on all 64 cores would take the other GPUs' jobs' CPUs, so the all-cores
-    # figure of SURVEY 8d(ii) is not measured and the label says so
+    # every thread of a shared 8-GPU host (nproc = 256 on a 64-core EPYC); a
+    # one-GPU job is allotted 16 (OMP_NUM_THREADS there)
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
     threads = max(1, min(16, avail))
+    blas = O.use_blas(True)
     O.set_threads(threads)
     r = np.random.default_rng(1)
+    legs = ("conv_fwd", "pool_fwd", "fc_fwd", "fc_bwd_update", "pool_bwd", "conv_bwd_update")
 
     def one_step(n):
         oc = O.Conv(H, W, C, KH, KW, G)
@@ -180,28 +185,39 @@ def cpu_baseline(frames_hint, budget_s=12.0):
         of.b = np.ones(FC_OUT, np.float32)
         x = r.standard_normal((n, H * W * C)).astype(np.float32)
         dy = (r.standard_normal((n, FC_OUT)) * 1e-2).astype(np.float32)
+        ts = []
         t0 = time.perf_counter()
-        y1 = oc.propagate(x)
-        y2 = op.propagate(y1)
-        of.propagate(y2)
-        d2 = of.backprop(y2, dy, update=True)
-        d1 = op.backprop(y1, y2, d2)
-        oc.backprop(x, d1, update=True)
-        return time.perf_counter() - t0
+        y1 = oc.propagate(x); ts.append(time.perf_counter())
+        y2 = op.propagate(y1); ts.append(time.perf_counter())
+        of.propagate(y2); ts.append(time.perf_counter())
+        d2 = of.backprop(y2, dy, update=True); ts.append(time.perf_counter())
+        d1 = op.backprop(y1, y2, d2); ts.append(time.perf_counter())
+        oc.backprop(x, d1, update=True); ts.append(time.perf_counter())
+        split = {k: round(b - a, 4) for k, a, b in zip(legs, [t0] + ts[:-1], ts)}
+        return ts[-1] - t0, split
 
-    one_step(8)  # first call: library load, OpenMP pool, page faults
+    one_step(8)  # first call: library load, thread pools, page faults
 
     def sized(budget):
-        t_small = one_step(8)
-        n = int(max(8, min(frames_hint, 8 * budget / max(t_small, 1e-3))))
-        n = max(8, (n // 8) * 8)
-        return n, one_step(n)
+        t_small = one_step(16)[0]
+        n = int(max(16, min(frames_hint, 16 * budget / max(t_small, 1e-3))))
+        n = max(16, (n // 16) * 16)
+        t, _ = one_step(n)
+        return n, t
 
     n = max(8, min(4096, frames_hint))
-    t = one_step(n)
-    # also one thread (nnet-train-simple --use-gpu=no)
+    t, split = one_step(n)
+    # one thread (nnet-train-simple --use-gpu=no) ...
     O.set_threads(1)
     n1, t1 = sized(budget_s / 2)
+    # ... and every CPU of the affinity mask (nnet-train-parallel
+    # --num-threads, train_conv_dropout.sh:205-208), a short sample: on the
+    # GPU box those CPUs belong to the other GPUs' jobs too
+    all_cores = None
+    if avail > threads:
+        O.set_threads(avail)
+        na, ta = sized(budget_s / 4)
+        all_cores = {"value": round(na / ta, 2), "threads": avail, "sample": f"{na} frames"}
 
     def c1_forward(reps=3):
         """BASELINE configs[0]: Conv + Maxpool forward, 256 frames."""
@@ -217,9 +233,11 @@ def cpu_baseline(frames_hint, budget_s=12.0):
             best = min(best, time.perf_counter() - t0)
         return round(256 / best, 1)
 
+    O.set_threads(1)
     c1_1 = c1_forward()
     O.set_threads(threads)
     c1_n = c1_forward()
+    O.use_blas(False)
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -229,14 +247,19 @@ def cpu_baseline(frames_hint, budget_s=12.0):
     return {"value": round(n / t, 2), "unit": "frames/sec", "cores": threads,
             "kind": "port",
             "sample": f"{n} frames of the c2 stack, one full fwd+bwd+update step, "
-                      f"C oracle (oracle/kcnn_oracle.c) with {threads} OpenMP threads",
+                      f"C oracle (oracle/kcnn_oracle.c) with {threads} threads",
+            "blas": f"OpenBLAS 0.3.29 sgemm ({os.path.basename(blas)}, numpy's) for the "
+                    "AddMatMat legs; im2col / col2im / reshapes / maxpool as the "
+                    "reference's CPU loops (OpenMP)",
+            "seconds_per_leg": split,
             "single_thread": {"value": round(n1 / t1, 2), "sample": f"{n1} frames, 1 thread"},
+            "all_affinity": all_cores,
             "c1_forward": {"unit": "frames/sec", "threads_1": c1_1, f"threads_{threads}": c1_n,
                            "sample": "BASELINE configs[0]: Conv+Maxpool forward, 256 frames, "
                                      "best of 3"},
             "host": {"cpu_model": model, "nproc": os.cpu_count(), "affinity": avail,
                      "threads_note": f"{threads} threads = one GPU's share of the box's "
-                                     "host CPUs (the job's allotment), not all 64 cores"}}
+                                     "host CPUs (the job's allotment)"}}
 
 
 def baseline_config(frames_per_gpu, world):

@@ -65,10 +65,15 @@ int kcnn_set_fusion(int mode);
 /* How CuMatrixBase::AddMatMat (every FullyConnectedComponent GEMM) computes
  * its fp32 product (upstream: cuBLAS sgemm, cu-matrix.cc AddMatMat):
  *   0: rocBLAS sgemm on the fp32-input MFMA;
- *   1 (default): the in-house kernel on the bf16 MFMA with each fp32 operand
- *      split exactly into three bf16 parts and the six leading cross products
- *      kept (cu-gemm-x6.hip); same error bound as sgemm.
- * Env KCNN_GEMM (0/1) sets the initial mode. */
+ *   1: the in-house kernel on the bf16 MFMA with each fp32 operand split
+ *      exactly into three bf16 parts and the six leading cross products kept
+ *      (cu-gemm-x6.hip); same error bound as sgemm;
+ *   2 (default): the in-house kernel on the f16 MFMA with each operand scaled
+ *      by a power of two per row of op(A) / column of op(B) and split into
+ *      two f16 parts, three cross products kept (cu-gemm-f16x3.hip); same
+ *      error bound, IEEE Inf / NaN rows and columns; shapes past its 32-bit
+ *      addressing run mode 1.
+ * Env KCNN_GEMM (0/1/2) sets the initial mode. */
 int kcnn_set_gemm_mode(int mode);
 /* Kernel-family selectors (kaldi-lite/kcnn-knobs.h): each picks
  * one of two implementations of the same fp32 math, the bf16x6 kernels on
@@ -77,7 +82,7 @@ int kcnn_set_gemm_mode(int mode);
  *   "bwd_x6"   fused conv backward              1 (default) / 0
  *   "igemm_x6" implicit-GEMM forward and dgrad  1 (default) / 0
  *   "wgrad_x6" long-kernel weight gradient      2 (default, wide) / 1 / 0
- *   "gemm"     AddMatMat (= kcnn_set_gemm_mode) 1 (default) / 0
+ *   "gemm"     AddMatMat (= kcnn_set_gemm_mode) 2 (default, f16x3) / 1 / 0
  * The environment variables KCNN_FWD_X6, KCNN_BWD_X6, KCNN_IGEMM_X6,
  * KCNN_WGRAD_X6 and KCNN_GEMM set the initial values.  Returns nonzero for
  * an unknown name or value. */

@@ -146,7 +146,8 @@ def profile_string() -> str:
 
 
 def set_gemm_mode(mode: int):
-    """AddMatMat's fp32 product: 0 = rocBLAS sgemm, 1 = bf16x6 split kernel."""
+    """AddMatMat's fp32 product: 0 = rocBLAS sgemm, 1 = bf16x6 split kernel,
+    2 = f16x3 split kernel (default)."""
     check(lib().kcnn_set_gemm_mode(int(mode)))
 
 

@@ -206,7 +206,7 @@ int kcnn_set_fusion(int on) {
   return 0;
 }
 int kcnn_set_gemm_mode(int mode) {
-  if (mode < 0 || mode > 1) return fail("kcnn_set_gemm_mode: mode is 0 or 1");
+  if (mode < 0 || mode > 2) return fail("kcnn_set_gemm_mode: mode is 0, 1 or 2");
   CuDevice::Instantiate().SetGemmMode(mode);
   return 0;
 }
@@ -250,7 +250,8 @@ int kcnn_gemm_planes(int trans_a, int trans_b, int m, int n, int k, float alpha,
   return guard([&] {
     CuDevice &d = CuDevice::Instantiate();
     const size_t wsb = kl_gemm_planes_workspace_bytes(m, n, k);
-    void *ws = wsb ? d.Workspace(wsb) : nullptr;
+    CuScratch ws_s(wsb);
+    void *ws = ws_s.p;
     const int rc = kl_gemm_planes(trans_a, trans_b, m, n, k, alpha, a, lda, aps, b, ldb, bps,
                                   beta, c, ldc, ws, wsb,
                                   reinterpret_cast<kcnn_stream_t>(d.Stream()));

@@ -557,6 +557,8 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
 }
 
 // ---------------------------------------------------------------------------
+#ifdef KCNN_EXPERIMENTS  // the round-2/3 pipelined kernel, x6q's predecessor:
+                         // only the experiment build (KCNN_BWD_X6P=1) has it
 // conv_bwd_x6p_kernel: conv_bwd_x6_kernel's math bit for bit -- the same
 // image contents, operand fragments, and order of the MFMAs into every
 // accumulator -- software-pipelined, for the pooled backward with both
@@ -1066,6 +1068,7 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6p_kernel(
   else frames(std::integral_constant<int, 2>{});
 #undef KCNN_TMARK
 }
+#endif  // KCNN_EXPERIMENTS
 
 // ---------------------------------------------------------------------------
 // conv_bwd_x6q_kernel: conv_bwd_x6p_kernel's math bit for bit (the same image
@@ -1751,11 +1754,15 @@ int kcnn_conv_bwd_x6(const ConvGeom &g, const float *X, int xs, const float *dY,
     hipLaunchKernelGGL((KER<NCH, PCM, PH>), dim3(S), dim3(NT), lds, st, g, X, xs, dY, dys, K, \
                        ks, dX, dxs, ws_part, ZZ, tab, dx_acc, pmask, pms, dbg);            \
   } while (0)
+#ifdef KCNN_EXPERIMENTS
 #define KCNN_X6PP(NCH, PCM, PH)                                \
   do {                                                         \
     if (pipelined == 1) KCNN_X6PK(conv_bwd_x6p_kernel, NCH, PCM, PH); \
     else KCNN_X6PK(conv_bwd_x6q_kernel, NCH, PCM, PH);         \
   } while (0)
+#else
+#define KCNN_X6PP(NCH, PCM, PH) KCNN_X6PK(conv_bwd_x6q_kernel, NCH, PCM, PH)
+#endif
 #define KCNN_X6PM(NCH)                                      \
   do {                                                      \
     if (pc == 4 && ph == 3) KCNN_X6PP(NCH, 4, 3);           \

@@ -41,11 +41,11 @@ void CuMatrixBase<Real>::Conv2D(const CuMatrixBase<Real> &kernel,
     KALDI_ASSERT(out->NumRows() == out_height * out_width * NumRows() &&
                  out->NumCols() == group);
   CuProfileScope prof("Conv2D");
-  CuDevice &dev = CuDevice::Instantiate();
   const size_t ws_bytes = hipF_conv2d_workspace_bytes(
       Dim(), in_height, in_width, in_channel, 0, 0, kernel_height,
       kernel_width, group);
-  void *ws = ws_bytes ? dev.Workspace(ws_bytes) : nullptr;
+  CuScratch ws_s(ws_bytes);
+  void *ws = ws_s.p;
   CNSL_SAFE_CALL(hipF_conv2d(data_, Dim(), in_height, in_width, in_channel, 0,
                              0, kernel.Data(), kernel.Dim(), kernel_height,
                              kernel_width, group, nullptr, out->Data(),

@@ -52,6 +52,12 @@ std::vector<PendingEvent> &pending() {
   static std::vector<PendingEvent> p;
   return p;
 }
+// guards pending(), event_pool() and the profile map: profiled scopes may
+// close on several host threads at once
+std::mutex &prof_mu() {
+  static std::mutex m;
+  return m;
+}
 // Events of resolved scopes are kept for reuse: a profiled step creates no
 // new events once the pool holds one pair per scope.
 std::vector<hipEvent_t> &event_pool() {
@@ -59,6 +65,7 @@ std::vector<hipEvent_t> &event_pool() {
   return p;
 }
 hipEvent_t take_event() {
+  std::lock_guard<std::mutex> lk(prof_mu());
   auto &p = event_pool();
   if (!p.empty()) {
     hipEvent_t e = p.back();
@@ -68,8 +75,12 @@ hipEvent_t take_event() {
   hipEvent_t e = nullptr;
   return hipEventCreate(&e) == hipSuccess ? e : nullptr;
 }
-void give_event(hipEvent_t e) {
+void give_event_locked(hipEvent_t e) {
   if (e) event_pool().push_back(e);
+}
+void give_event(hipEvent_t e) {
+  std::lock_guard<std::mutex> lk(prof_mu());
+  give_event_locked(e);
 }
 size_t round_block(size_t bytes) {
   // 256-B granules below 1 MiB, 1 MiB granules above: bounded waste, high reuse.
@@ -183,20 +194,17 @@ void CuDevice::ReleaseCache() {
   bytes_cached_ = 0;
 }
 
-void *CuDevice::Workspace(size_t bytes) {
-  if (bytes <= ws_bytes_) return ws_;
-  if (ws_) Free(ws_);
-  ws_bytes_ = round_block(bytes);
-  ws_ = Malloc(ws_bytes_);
-  return ws_;
-}
-
 void CuDevice::Synchronize() {
   EnsureInit();
   CU_SAFE_CALL(hipStreamSynchronize(stream_));
 }
 
 void CuDevice::AccuProfile(const std::string &key, double ms) {
+  std::lock_guard<std::mutex> lk(prof_mu());
+  AccuProfileLocked(key, ms);
+}
+
+void CuDevice::AccuProfileLocked(const std::string &key, double ms) {
   auto &e = profile_[key];
   e.first += ms;
   e.second += 1;
@@ -204,13 +212,14 @@ void CuDevice::AccuProfile(const std::string &key, double ms) {
 
 std::string CuDevice::ProfileString() const {
   CuDevice *self = const_cast<CuDevice *>(this);
+  std::lock_guard<std::mutex> lk(prof_mu());
   for (auto &pe : pending()) {
     float ms = 0.0f;
     if (hipEventSynchronize(pe.end) == hipSuccess &&
         hipEventElapsedTime(&ms, pe.beg, pe.end) == hipSuccess)
-      self->AccuProfile(pe.key, ms);
-    give_event(pe.beg);
-    give_event(pe.end);
+      self->AccuProfileLocked(pe.key, ms);
+    give_event_locked(pe.beg);
+    give_event_locked(pe.end);
   }
   pending().clear();
   std::ostringstream os;
@@ -246,6 +255,7 @@ CuProfileScope::~CuProfileScope() {
   if (!beg_) return;
   CuDevice &d = CuDevice::Instantiate();
   (void)hipEventRecord(end_, d.Stream());
+  std::lock_guard<std::mutex> lk(prof_mu());
   pending().push_back({key_, beg_, end_});
 }
 

@@ -65,21 +65,19 @@ class CuDevice {
   size_t BytesInUse() const { return bytes_in_use_; }
   size_t BytesCached() const { return bytes_cached_; }
 
-  // Stream-ordered scratch for kernels (split-K partials etc.).  Valid until
-  // the next call with a larger size; callers on Stream() only.
-  void *Workspace(size_t bytes);
 
   // Profiling: per-function accumulated kernel milliseconds, measured with
   // hipEvents when enabled (KCNN_PROFILE=1 or SetProfiling(true)).
   void SetProfiling(bool on) { profiling_ = on; }
   bool Profiling() const { return profiling_; }
   void AccuProfile(const std::string &key, double ms);
+  void AccuProfileLocked(const std::string &key, double ms);  // caller holds the profile lock
   std::string ProfileString() const;
   void ResetProfile() { profile_.clear(); }
 
-  // AddMatMat's fp32 product: 0 = rocBLAS sgemm, 1 = bf16x6 split kernel
-  // (the "gemm" kernel family, kcnn-knobs.h)
-  void SetGemmMode(int m) { kcnn::set_family(kcnn::kFamGemm, m ? 1 : 0); }
+  // AddMatMat's fp32 product: 0 = rocBLAS sgemm, 1 = bf16x6 split kernel,
+  // 2 = f16x3 split kernel (the "gemm" kernel family, kcnn-knobs.h)
+  void SetGemmMode(int m) { kcnn::set_family(kcnn::kFamGemm, m); }
   int GemmMode() const { return kcnn::family(kcnn::kFamGemm); }
 
   void Synchronize();
@@ -99,8 +97,23 @@ class CuDevice {
   std::multimap<size_t, void *> free_blocks_;
   std::map<void *, size_t> live_blocks_;
   size_t bytes_in_use_ = 0, bytes_cached_ = 0;
-  void *ws_ = nullptr;
-  size_t ws_bytes_ = 0;
+};
+
+// Per-call scratch (split-K partials, GEMM workspaces) from the caching
+// allocator, freed at scope exit.  Every call owns its block, so concurrent
+// const Propagate / Backprop calls from several host threads never share one
+// (SURVEY 8(b) Threading: nnet-train-parallel runs them multi-threaded); the
+// allocator's stream-ordered reuse keeps a freed block away from kernels
+// still to run on Stream().
+struct CuScratch {
+  void *p = nullptr;
+  explicit CuScratch(size_t bytes) {
+    if (bytes) p = CuDevice::Instantiate().Malloc(bytes);
+  }
+  ~CuScratch() { if (p) CuDevice::Instantiate().Free(p); }
+  CuScratch(const CuScratch &) = delete;
+  CuScratch &operator=(const CuScratch &) = delete;
+  float *f() { return static_cast<float *>(p); }
 };
 
 // Times a scope with hipEvents on the device stream when profiling is on.

@@ -28,6 +28,24 @@ size_t kl_gemm_x6_workspace_bytes(int M, int N, int K);
 int kl_gemm_x6(int transA, int transB, int M, int N, int K, float alpha,
                const float *A, int lda, const float *B, int ldb, float beta,
                float *C, int ldc, void *ws, size_t ws_bytes, kcnn_stream_t st);
+/* fp32 GEMM on the f16 MFMAs: two-part f16 split under per-row / per-column
+   power-of-two scales (cu-gemm-f16x3.hip).  kl_absmax writes max |x| bit
+   patterns into st = [flag, 0, 0, 0, rows..., cols...] (zeroed first);
+   kl_gemm_f16x3_st takes them for op(A)'s rows and op(B)'s columns,
+   kl_gemm_f16x3 computes them in its workspace.  Both return
+   hipErrorNotSupported for shapes outside the kernel's addressing limits. */
+int kl_absmax(const float *X, int rows, int cols, int ld, uint32_t *st, int want_rows,
+              int want_cols, kcnn_stream_t st_);
+size_t kl_gemm_f16x3_workspace_bytes(int M, int N, int K);
+int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alpha,
+                     const float *A, int lda, const float *B, int ldb, float beta, float *C,
+                     int ldc, const uint32_t *amax, const uint32_t *aflag,
+                     const uint32_t *bmax, const uint32_t *bflag, void *ws, size_t ws_bytes,
+                     kcnn_stream_t st);
+size_t kl_gemm_f16x3_full_workspace_bytes(int M, int N, int K);
+int kl_gemm_f16x3(int transA, int transB, int M, int N, int K, float alpha,
+                  const float *A, int lda, const float *B, int ldb, float beta, float *C,
+                  int ldc, void *ws, size_t ws_bytes, kcnn_stream_t st);
 /* the same product from operands already split into bf16 planes h, m, l
    (plane p of X at X + p * ps elements); kl_split_planes makes them */
 int kl_split_planes(const float *src, int rows, int cols, int ld, uint16_t *dst, int ldp,

@@ -268,12 +268,14 @@ void CuMatrixBase<Real>::AddMatMat(Real alpha, const CuMatrixBase<Real> &A,
   if (k == 0) { if (beta != 1.0f) Scale(beta); return; }
   CuProfileScope prof("AddMatMat");
   CuDevice &dev0 = CuDevice::Instantiate();
-  if (dev0.GemmMode() == 1) {
-    // fp32 product on the bf16 MFMAs (exact operand split, cu-gemm-x6.hip).
-    // Its 16-B loads need the K-contiguous operands (A untransposed, B
-    // transposed) row-aligned; one that is not (a caller's matrix with an
-    // odd pitch, e.g. an output derivative of 3454 columns) is copied once
-    // into a padded-pitch CuMatrix, which costs far less than the GEMM.
+  const int mode = dev0.GemmMode();
+  if (mode >= 1) {
+    // fp32 product on the f16 (mode 2, cu-gemm-f16x3.hip) or bf16 (mode 1,
+    // cu-gemm-x6.hip) MFMAs from a split of each operand.  Their 16-B loads
+    // need the K-contiguous operands (A untransposed, B transposed)
+    // row-aligned; one that is not (a caller's matrix with an odd pitch,
+    // e.g. an output derivative of 3454 columns) is copied once into a
+    // padded-pitch CuMatrix, which costs far less than the GEMM.
     auto aligned = [](const CuMatrixBase<Real> &X) {
       return X.Stride() % 4 == 0 && reinterpret_cast<uintptr_t>(X.Data()) % 16 == 0;
     };
@@ -281,6 +283,20 @@ void CuMatrixBase<Real>::AddMatMat(Real alpha, const CuMatrixBase<Real> &A,
     const CuMatrixBase<Real> *Ap = &A, *Bp = &B;
     if (transA == kNoTrans && !aligned(A)) { Acopy = A; Ap = &Acopy; }
     if (transB == kTrans && !aligned(B)) { Bcopy = B; Bp = &Bcopy; }
+    if (mode == 2) {
+      const size_t wsf = kl_gemm_f16x3_full_workspace_bytes(m, n, k);
+      void *wf = dev0.Malloc(wsf);
+      const int rc = kl_gemm_f16x3(transA == kTrans, transB == kTrans, m, n, k, alpha,
+                                   Ap->Data(), Ap->Stride(), Bp->Data(), Bp->Stride(), beta,
+                                   data_, stride_, wf, wsf, S());
+      dev0.Free(wf);
+      // past the f16x3 kernel's 32-bit addressing the bf16x6 kernel (same
+      // error bound) takes the product
+      if (rc != (int)hipErrorNotSupported) {
+        CNSL_SAFE_CALL(rc);
+        return;
+      }
+    }
     const size_t wsb = kl_gemm_x6_workspace_bytes(m, n, k);
     void *ws = wsb ? dev0.Malloc(wsb) : nullptr;
     const int rc = kl_gemm_x6(transA == kTrans, transB == kTrans, m, n, k, alpha,

@@ -18,7 +18,7 @@ const FamilyInfo kFamilies[kNumFamilies] = {
     {"bwd_x6", "KCNN_BWD_X6", 1, 1},
     {"igemm_x6", "KCNN_IGEMM_X6", 1, 1},
     {"wgrad_x6", "KCNN_WGRAD_X6", 2, 2},
-    {"gemm", "KCNN_GEMM", 1, 1},
+    {"gemm", "KCNN_GEMM", 2, 2},
 };
 
 int from_env(const FamilyInfo &f) {

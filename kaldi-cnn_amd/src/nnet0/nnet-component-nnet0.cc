@@ -25,15 +25,7 @@ inline kcnn_stream_t S() {
   d.rows = rows; d.cols = cols; d.stride = cols;
   return d;
 }
-// RAII scratch from the caching allocator.
-struct Scratch {
-  void *p = nullptr;
-  explicit Scratch(size_t bytes) {
-    if (bytes) p = CuDevice::Instantiate().Malloc(bytes);
-  }
-  ~Scratch() { if (p) CuDevice::Instantiate().Free(p); }
-  float *f() { return static_cast<float *>(p); }
-};
+using Scratch = CuScratch;  // kaldi-lite/cu-device.h
 }  // namespace
 
 void SetLiteralPath(bool literal) { g_literal = literal; }
@@ -208,11 +200,11 @@ void ConvolutionComponent::Propagate(const ChunkInfo &in_info,
   KALDI_ASSERT(out->NumRows() == in.NumRows() && out->NumCols() == OutputDim());
   if (LiteralPath()) { PropagateLiteral(in_info, in, out); return; }
   CuProfileScope prof("ConvolutionComponent::Propagate");
-  CuDevice &dev = CuDevice::Instantiate();
   const size_t ws_bytes = hipF_conv2d_workspace_bytes(
       in.Dim(), in_height_, in_width_, in_channel_, in_pad_height_,
       in_pad_width_, kernel_height_, kernel_width_, group_);
-  void *ws = ws_bytes ? dev.Workspace(ws_bytes) : nullptr;
+  Scratch ws_s(ws_bytes);
+  void *ws = ws_s.p;
   CNSL_SAFE_CALL(hipF_conv2d(in.Data(), in.Dim(), in_height_, in_width_,
                              in_channel_, in_pad_height_, in_pad_width_,
                              linear_params_.Data(), linear_params_.Dim(),
@@ -354,11 +346,11 @@ void ConvolutionComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
       KALDI_ASSERT(kernel_height_ - 1 - in_pad_height_ >= 0 &&
                    kernel_width_ - 1 - in_pad_width_ >= 0 &&
                    "kernel must exceed the padding");               // :533
-      CuDevice &dev = CuDevice::Instantiate();
       const size_t ws_bytes = hipF_conv2d_dgrad_workspace_bytes(
           out_deriv.Dim(), in_height_, in_width_, in_channel_, in_pad_height_,
           in_pad_width_, kernel_height_, kernel_width_, group_);
-      void *ws = ws_bytes ? dev.Workspace(ws_bytes) : nullptr;
+      Scratch ws_s(ws_bytes);
+  void *ws = ws_s.p;
       CuProfileScope prof("ConvolutionComponent::BackpropData");
       CNSL_SAFE_CALL(hipF_conv2d_dgrad(
           out_deriv.Data(), out_deriv.Dim(), in_height_, in_width_, in_channel_,
@@ -610,11 +602,11 @@ void ConvolutionComponent::ComputeGradient(const CuMatrixBase<BaseFloat> &in_val
                out_deriv.NumCols() == OutputDim() &&
                in_value.NumRows() == out_deriv.NumRows());
   CuProfileScope prof("ConvolutionComponent::ComputeGradient");
-  CuDevice &dev = CuDevice::Instantiate();
   const size_t ws_bytes = hipF_conv2d_wgrad_workspace_bytes(
       in_value.Dim(), in_height_, in_width_, in_channel_, in_pad_height_,
       in_pad_width_, kernel_height_, kernel_width_, group_);
-  void *ws = dev.Workspace(ws_bytes);
+  Scratch ws_s(ws_bytes);
+  void *ws = ws_s.p;
   CNSL_SAFE_CALL(hipF_conv2d_wgrad(
       in_value.Data(), in_value.Dim(), in_height_, in_width_, in_channel_,
       in_pad_height_, in_pad_width_, out_deriv.Data(), out_deriv.Dim(),
@@ -647,11 +639,11 @@ void ConvolutionComponent::BackpropGradient(const ChunkInfo &in_info,
     if (in_deriv->NumRows() != num_chunks || in_deriv->NumCols() != InputDim())
       in_deriv->Resize(num_chunks, InputDim(), kUndefined);
   }
-  CuDevice &dev = CuDevice::Instantiate();
   const size_t ws_bytes = hipF_conv2d_backward_workspace_bytes(
       in_value.Dim(), in_height_, in_width_, in_channel_, in_pad_height_,
       in_pad_width_, kernel_height_, kernel_width_, group_);
-  void *ws = ws_bytes ? dev.Workspace(ws_bytes) : nullptr;
+  Scratch ws_s(ws_bytes);
+  void *ws = ws_s.p;
   CuProfileScope prof("ConvolutionComponent::BackpropGradient");
   MatrixDim idd = in_value.Dim();
   CNSL_SAFE_CALL(hipF_conv2d_backward(
@@ -694,7 +686,6 @@ bool ConvolutionComponent::BackpropPooled(const CuMatrixBase<BaseFloat> &in_valu
     if (in_deriv->NumRows() != num_chunks || in_deriv->NumCols() != InputDim())
       in_deriv->Resize(num_chunks, InputDim(), kUndefined);
   }
-  CuDevice &dev = CuDevice::Instantiate();
   Scratch own(grad == NULL && to_update != NULL
                   ? sizeof(BaseFloat) * (size_t)NumGradientParams() : 0);
   BaseFloat *g = grad ? grad : own.f();
@@ -703,7 +694,8 @@ bool ConvolutionComponent::BackpropPooled(const CuMatrixBase<BaseFloat> &in_valu
                                   in_pad_height_, in_pad_width_, kernel_height_,
                                   kernel_width_, group_)
                             : 0;
-  void *ws = ws_bytes ? dev.Workspace(ws_bytes) : nullptr;
+  Scratch ws_s(ws_bytes);
+  void *ws = ws_s.p;
   MatrixDim idd = in_value.Dim();
   int rc;
   {

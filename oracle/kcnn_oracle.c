@@ -10,6 +10,7 @@
  */
 #include "kcnn_oracle.h"
 
+#include <dlfcn.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -38,9 +39,38 @@ static int fail(const char *fmt, ...) {
                              __func__, __LINE__);               \
   } while (0)
 
+/* Optional CBLAS for the mode-0 GEMMs (the CPU-baseline timing only; the
+ * parity tests keep the sequential-k loops below).  Upstream Kaldi's CPU
+ * AddMatMat is cblas_sgemm (ATLAS / OpenBLAS / MKL); orc_use_blas binds the
+ * OpenBLAS that numpy ships (64-bit-int interface, symbols scipy_*64_).     */
+typedef void (*sgemm64_fn)(int order, int ta, int tb, int64_t m, int64_t n, int64_t k,
+                           float alpha, const float *a, int64_t lda, const float *b,
+                           int64_t ldb, float beta, float *c, int64_t ldc);
+typedef void (*blas_threads_fn)(int64_t n);
+static sgemm64_fn g_sgemm = NULL;
+static blas_threads_fn g_blas_threads = NULL;
+
+int orc_use_blas(const char *path) {
+  if (!path) {
+    g_sgemm = NULL;
+    return 0;
+  }
+  void *h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+  if (!h) return fail("dlopen %s: %s", path, dlerror());
+  g_sgemm = (sgemm64_fn)dlsym(h, "scipy_cblas_sgemm64_");
+  g_blas_threads = (blas_threads_fn)dlsym(h, "scipy_openblas_set_num_threads64_");
+  if (!g_sgemm) return fail("%s has no scipy_cblas_sgemm64_", path);
+  if (g_blas_threads) g_blas_threads(g_threads);
+  return 0;
+}
+int orc_blas_active(void) { return g_sgemm != NULL; }
+
 void orc_set_accum_mode(int mode) { g_accum_mode = mode; }
 int orc_get_accum_mode(void) { return g_accum_mode; }
-void orc_set_num_threads(int n) { g_threads = n < 1 ? 1 : n; }
+void orc_set_num_threads(int n) {
+  g_threads = n < 1 ? 1 : n;
+  if (g_blas_threads) g_blas_threads(g_threads);
+}
 int orc_num_threads(void) { return g_threads; }
 const char *orc_last_error(void) { return g_err; }
 
@@ -70,6 +100,14 @@ int orc_gemm(float alpha, const orc_mat *A, int transA, const orc_mat *B,
   const int N = transB ? B->rows : B->cols;
   CHECK(K == KB && C->rows == M && C->cols == N);
   const int mode = g_accum_mode;
+  if (mode == 0 && g_sgemm) {
+    if (M == 0 || N == 0) return 0;
+    /* CblasRowMajor = 101, CblasNoTrans = 111, CblasTrans = 112 */
+    g_sgemm(101, transA ? 112 : 111, transB ? 112 : 111, M, N, K, alpha, A->data,
+            A->rows > 0 ? A->stride : 1, B->data, B->rows > 0 ? B->stride : 1, beta, C->data,
+            C->stride);
+    return 0;
+  }
   if (mode == 0 && !transB) {
     /* i-k-j loop: per (i,j) still sequential in k, vectorises over j. */
     float *acc_all = NULL;

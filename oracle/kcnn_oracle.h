@@ -43,6 +43,10 @@ void orc_set_accum_mode(int mode);
 int orc_get_accum_mode(void);
 /* OpenMP threads used by the GEMM / im2col loops (1 = scalar reference). */
 void orc_set_num_threads(int n);
+/* Mode-0 GEMMs through a CBLAS sgemm (OpenBLAS's 64-bit-int build, dlopen'ed
+ * from `path`; NULL goes back to the loops).  For the CPU-baseline timing. */
+int orc_use_blas(const char *path);
+int orc_blas_active(void);
 int orc_num_threads(void);
 const char *orc_last_error(void);
 

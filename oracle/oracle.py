@@ -108,6 +108,25 @@ def set_threads(n: int):
     lib().orc_set_num_threads(int(n))
 
 
+def openblas_path():
+    """numpy's bundled OpenBLAS (the CBLAS class upstream Kaldi links), or None."""
+    import glob
+    d = os.path.join(os.path.dirname(np.__file__), "..", "numpy.libs")
+    hits = sorted(glob.glob(os.path.join(d, "libscipy_openblas64_*.so")))
+    return os.path.abspath(hits[0]) if hits else None
+
+
+def use_blas(on: bool = True) -> str | None:
+    """Mode-0 GEMMs through OpenBLAS sgemm (CPU-baseline timing) or, with
+    on=False, the sequential-k loops (the parity tests' reference order).
+    Returns the library used."""
+    path = openblas_path() if on else None
+    if on and path is None:
+        raise OracleError("numpy's OpenBLAS not found")
+    _chk(lib().orc_use_blas(path.encode() if path else None))
+    return path
+
+
 # --- CuMatrixBase extensions ------------------------------------------------
 
 def conv2d(x, k, H, W, C, kh, kw, G, concat=True, out=None):

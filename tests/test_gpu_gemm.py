@@ -1,6 +1,7 @@
-"""CuMatrixBase::AddMatMat on the GPU: the bf16x6 split kernel (gemm mode 1,
-kaldi-lite/cu-gemm-x6.hip) and rocBLAS sgemm (mode 0) against a float64
-product, with the dot-product error bound of SURVEY 8(d):
+"""CuMatrixBase::AddMatMat on the GPU: the f16x3 split kernel (gemm mode 2,
+the default, kaldi-lite/cu-gemm-f16x3.hip), the bf16x6 split kernel (mode 1,
+cu-gemm-x6.hip) and rocBLAS sgemm (mode 0) against a float64 product, with
+the dot-product error bound of SURVEY 8(d):
 |c - t| <= 1e-5 * (|alpha| |op(A)| |op(B)| + |beta| |C0|) elementwise and
 ||c - t|| / ||t|| <= 1e-5.  The float64 truth is torch's fp64 matmul on the
 same device (a plain PyTorch reference of the op, as for every float kernel).
@@ -10,6 +11,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 RTOL = 1e-5
+SPLIT_MODES = [2, 1]   # f16x3, bf16x6
 
 
 def _mats(torch, m, n, k, ta, tb, seed, scale_b=0.01, pitch=0):
@@ -26,62 +28,147 @@ def _mats(torch, m, n, k, ta, tb, seed, scale_b=0.01, pitch=0):
     return a, b, c
 
 
-def _check(torch, kc, m, n, k, ta, tb, alpha=1.0, beta=0.0, mode=1, seed=1, pitch=0):
-    a, b, c0 = _mats(torch, m, n, k, ta, tb, seed, pitch=pitch)
-    c = c0.clone()
+def _gemm_mode(kc, mode, fn):
+    old = kc.get_kernel_family("gemm")
     kc.set_gemm_mode(mode)
     try:
-        kc.gemm(a, b, c, ta, tb, alpha, beta)
+        return fn()
     finally:
-        kc.set_gemm_mode(1)
-    torch.cuda.synchronize()
+        kc.set_gemm_mode(old)
+
+
+def _bound(torch, a, b, c0, c, ta, tb, alpha, beta):
     A = (a.t() if ta else a).double()
     B = (b.t() if tb else b).double()
     t = alpha * (A @ B) + beta * c0.double()
     s = abs(alpha) * (A.abs() @ B.abs()) + abs(beta) * c0.double().abs()
     err = (c.double() - t).abs()
     assert torch.isfinite(c).all()
-    worst = float((err / s.clamp_min(1e-30)).max())
+    worst = float((err / s.clamp_min(1e-300)).max())
     assert worst <= RTOL, f"max err/S {worst:.3e}"
-    rel = float((c.double() - t).norm() / t.norm())
+    rel = float((c.double() - t).norm() / t.norm().clamp_min(1e-300))
     assert rel <= RTOL, f"normwise {rel:.3e}"
+    return worst, rel
+
+
+def _check(torch, kc, m, n, k, ta, tb, alpha=1.0, beta=0.0, mode=2, seed=1, pitch=0):
+    a, b, c0 = _mats(torch, m, n, k, ta, tb, seed, pitch=pitch)
+    c = c0.clone()
+    _gemm_mode(kc, mode, lambda: kc.gemm(a, b, c, ta, tb, alpha, beta))
+    torch.cuda.synchronize()
+    worst, rel = _bound(torch, a, b, c0, c, ta, tb, alpha, beta)
     return c, worst, rel
 
 
+@pytest.mark.parametrize("mode", SPLIT_MODES)
 @pytest.mark.parametrize("ta", [False, True])
 @pytest.mark.parametrize("tb", [False, True])
 @pytest.mark.parametrize("shape", [(1, 1, 1), (7, 5, 3), (33, 17, 40), (300, 129, 77),
-                                   (257, 260, 1000), (64, 11616, 96)])
-def test_gemm_x6_small_and_ragged(kc, ta, tb, shape):
+                                   (257, 260, 1000), (64, 11616, 96), (129, 70, 4133)])
+def test_gemm_x6_small_and_ragged(kc, mode, ta, tb, shape):
     import torch
     m, n, k = shape
-    _check(torch, kc, m, n, k, ta, tb)
+    _check(torch, kc, m, n, k, ta, tb, mode=mode)
 
 
+@pytest.mark.parametrize("mode", SPLIT_MODES)
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
-def test_gemm_x6_alpha_beta_pitched(kc, ta, tb):
+def test_gemm_x6_alpha_beta_pitched(kc, mode, ta, tb):
     import torch
-    _check(torch, kc, 130, 70, 200, ta, tb, alpha=0.37, beta=1.0, pitch=12)
-    _check(torch, kc, 130, 70, 200, ta, tb, alpha=-2.0, beta=0.5, pitch=4)
+    _check(torch, kc, 130, 70, 200, ta, tb, alpha=0.37, beta=1.0, pitch=12, mode=mode)
+    _check(torch, kc, 130, 70, 200, ta, tb, alpha=-2.0, beta=0.5, pitch=4, mode=mode)
 
 
-def test_gemm_x6_split_k_is_deterministic(kc):
+@pytest.mark.parametrize("mode", SPLIT_MODES)
+def test_gemm_x6_split_k_is_deterministic(kc, mode):
     """Thin output, long K: the K split over workgroups with the fixed-order
     partial sum; bitwise equal across runs."""
     import torch
-    c1, _, _ = _check(torch, kc, 256, 256, 9000, False, True, beta=1.0)
-    c2, _, _ = _check(torch, kc, 256, 256, 9000, False, True, beta=1.0)
+    c1, _, _ = _check(torch, kc, 256, 256, 9000, False, True, beta=1.0, mode=mode)
+    c2, _, _ = _check(torch, kc, 256, 256, 9000, False, True, beta=1.0, mode=mode)
     assert torch.equal(c1, c2)
 
 
-def test_gemm_x6_beta_zero_ignores_nan(kc):
+@pytest.mark.parametrize("mode", SPLIT_MODES)
+def test_gemm_x6_beta_zero_ignores_nan(kc, mode):
     import torch
     a = torch.randn(40, 50, device="cuda")
     b = torch.randn(50, 30, device="cuda")
     c = torch.full((40, 30), float("nan"), device="cuda")
-    kc.gemm(a, b, c)
+    _gemm_mode(kc, mode, lambda: kc.gemm(a, b, c))
     torch.cuda.synchronize()
     assert torch.isfinite(c).all()
+
+
+@pytest.mark.parametrize("case", ["spread", "subnormal_a", "huge_a"])
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("shape", [(300, 200, 1000), (256, 256, 9024)])
+def test_gemm_f16x3_row_scales(kc, case, ta, tb, shape):
+    """f16x3 scales each row of op(A) and column of op(B) by its own power of
+    two, so operands anywhere in fp32's range meet the full bar: rows spread
+    over 2^-60..2^60 and columns over 2^-30..2^30 with zero rows / columns and
+    a single-element row; all of A fp32 subnormals (2^-140, B at 2^110); all
+    of A near FLT_MAX / 2 (2^126, B at 2^-120)."""
+    import torch
+    m, n, k = shape
+    a, b, c0 = _mats(torch, m, n, k, ta, tb, seed=7)
+    A = a.t() if ta else a          # views: scaling them scales the stored data
+    B = b.t() if tb else b
+    if case == "spread":
+        g = torch.Generator(device="cuda")
+        g.manual_seed(11)
+        A.mul_(torch.exp2(torch.randint(-60, 61, (m, 1), generator=g, device="cuda").float()))
+        B.mul_(torch.exp2(torch.randint(-30, 31, (1, n), generator=g, device="cuda").float()))
+        A[3].zero_()
+        B[:, 5].zero_()
+        A[7].zero_()
+        A[7, k // 2] = 1.5
+    elif case == "subnormal_a":
+        A.mul_(2.0 ** -140)
+        B.mul_(2.0 ** 110)
+        assert float(A.abs().max()) < 2.0 ** -126   # every element subnormal
+    else:
+        A.mul_(2.0 ** 125)
+        B.mul_(2.0 ** -120)
+    c = c0.clone()
+    kc.gemm(a, b, c, ta, tb, 1.0, 0.0)
+    torch.cuda.synchronize()
+    _bound(torch, a, b, c0, c, ta, tb, 1.0, 0.0)
+
+
+@pytest.mark.parametrize("mode", [2, 0])
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
+def test_gemm_nonfinite_pattern(kc, mode, ta, tb):
+    """Inf and NaN operands give sgemm's IEEE pattern (+Inf, -Inf, NaN, and
+    the finite elements elsewhere within the bound): f16x3 computes the rows
+    and columns they touch as fp32 dot products; rocBLAS for comparison."""
+    import torch
+    m, n, k = 260, 140, 300
+    a, b, c0 = _mats(torch, m, n, k, ta, tb, seed=5)
+    A = a.t() if ta else a
+    B = b.t() if tb else b
+    A[4, 10] = float("inf")
+    A[9, 11] = float("-inf")
+    A[20, 0] = float("nan")
+    A[30, 12] = float("inf"); A[30, 13] = float("-inf")
+    B[12, 7] = float("inf")
+    B[:, 100] = 0.0; B[50, 100] = float("-inf")
+    B[0, 60] = 0.0                     # Inf * 0 in row 20? (NaN anyway)
+    B[10, 3] = 0.0                     # row 4's Inf meets a zero: NaN
+    c = c0.clone()
+    beta = 0.5
+    _gemm_mode(kc, mode, lambda: kc.gemm(a, b, c, ta, tb, 1.0, beta))
+    torch.cuda.synchronize()
+    t = A.double() @ B.double() + beta * c0.double()
+    fin = torch.isfinite(t)
+    assert torch.equal(torch.isnan(c), torch.isnan(t))
+    assert torch.equal(torch.isposinf(c), torch.isposinf(t))
+    assert torch.equal(torch.isneginf(c), torch.isneginf(t))
+    s = A.double().abs().nan_to_num(posinf=0) @ B.double().abs().nan_to_num(posinf=0) + \
+        beta * c0.double().abs()
+    err = (c.double() - t).abs()[fin]
+    assert float((err / s[fin].clamp_min(1e-300)).max()) <= RTOL
 
 
 @pytest.mark.parametrize("name,m,n,k,ta,tb", [
@@ -93,12 +180,16 @@ def test_gemm_x6_beta_zero_ignores_nan(kc):
     ("nnet_fc3_dgrad", 4096, 4096, 3454, False, False),
 ])
 def test_gemm_c2_fc_shapes(kc, name, m, n, k, ta, tb):
-    """The c2 stack's three FC GEMMs at full size: the split kernel meets the
-    bound, and its error is no worse than rocBLAS sgemm's (x 1.5)."""
+    """The c2 stack's three FC GEMMs at full size: both split kernels meet the
+    bound; bf16x6's error is no worse than rocBLAS sgemm's (x 1.5), f16x3's
+    within 8x of it normwise and 2e-6 * S elementwise."""
     import torch
+    _, w3, r3 = _check(torch, kc, m, n, k, ta, tb, mode=2)
     _, w6, r6 = _check(torch, kc, m, n, k, ta, tb, mode=1)
     _, w0, r0 = _check(torch, kc, m, n, k, ta, tb, mode=0)
     assert w6 <= 1.5 * w0 + 1e-8 and r6 <= 1.5 * r0 + 1e-8, (w6, w0, r6, r0)
+    # f16x3 keeps 22 of fp32's 24 bits per operand: within a few times sgemm
+    assert w3 <= 2e-6 and r3 <= 8 * r0 + 1e-8, (w3, w0, r3, r0)
 
 
 @pytest.mark.parametrize("ta", [False, True])
@@ -107,13 +198,15 @@ def test_gemm_c2_fc_shapes(kc, name, m, n, k, ta, tb):
                                          ((300, 1000, 2048), 0), ((256, 256, 9024), 8),
                                          ((1028, 516, 96), 0)])
 def test_gemm_x6_fast_path_shapes(kc, ta, tb, shape, pitch):
+    """(run on the default engine, f16x3, and on bf16x6)"""
     """Shapes the one-block-per-K-step kernel takes (K a multiple of 32, rows
     multiples of 4, 16-B aligned pitches): partial tiles read 0 past M / N
     through the buffer range, split K, both operand layouts."""
     import torch
     m, n, k = shape
-    _check(torch, kc, m, n, k, ta, tb, pitch=pitch)
-    _check(torch, kc, m, n, k, ta, tb, alpha=0.5, beta=1.0, pitch=pitch)
+    for mode in SPLIT_MODES:
+        _check(torch, kc, m, n, k, ta, tb, pitch=pitch, mode=mode)
+        _check(torch, kc, m, n, k, ta, tb, alpha=0.5, beta=1.0, pitch=pitch, mode=mode)
 
 
 def _check_planes(torch, kc, m, n, k, ta, tb, alpha=1.0, beta=0.0, seed=3):

@@ -36,7 +36,8 @@ PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 matrix (dense, spec)
 CONV_FLOP_PER_PASS = 2 * P * G * KH * KW * C          # 2,230,272
 CONV_BYTES_PER_PASS = 4 * (H * W * C + P * G)         # 191,136
 CONV_BWD_BYTES = 4 * (2 * H * W * C + P * G)          # 196,416: X, dY in; dX out
-CONV_BWD_FLOP = 2 * CONV_FLOP_PER_PASS + 2 * P * G    # dgrad + wgrad + bias grad
+CONV_BWD_FLOP = 2 * CONV_FLOP_PER_PASS                # dgrad + wgrad
+CONV_BIAS_GRAD_FLOP = 2 * P * G                        # the bias gradient, reported apart
 POOL_FWD_BYTES = 4 * (P * G + POOL_OUT)               # 232,320
 POOL_BWD_BYTES = 4 * (2 * P * G + 2 * POOL_OUT)       # 464,640
 # Conv -> Maxpool run fused by the kcnn_nnet runtime (kcnn_set_fusion):
@@ -139,6 +140,35 @@ NNET_CONVS = [(40, 21, 1, 40, 4, 128), (1, 18, 128, 1, 3, 128), (1, 16, 128, 1, 
 def nnet_conv_flop():
     return sum(2 * (H - kh + 1) * (W - kw + 1) * G * kh * kw * C
                for H, W, C, kh, kw, G in NNET_CONVS)
+
+
+# the source of each roofline kernel: a PMC byte count (profiles/
+# pmc_traffic.json) is only used while the digest of the source it was taken
+# from still matches
+KERNEL_SOURCES = {
+    "conv_bwd_x6q_kernel": "kaldi-cnn_amd/src/cnslmat/cnsl-conv-x6.hip",
+    "conv_bwd_x6_kernel": "kaldi-cnn_amd/src/cnslmat/cnsl-conv-x6.hip",
+    "conv_fwd_regs_kernel": "kaldi-cnn_amd/src/cnslmat/cnsl-conv-frame.hip",
+    "maxpool_direct_prop_kernel": "kaldi-cnn_amd/src/cnslmat/cnsl-hip-kernels.hip",
+    "maxpool_direct_backprop_kernel": "kaldi-cnn_amd/src/cnslmat/cnsl-hip-kernels.hip",
+    "gemm_f16x3_kernel": "kaldi-cnn_amd/src/kaldi-lite/cu-gemm-f16x3.hip",
+}
+
+
+def kernel_source_digest(kernel):
+    """sha1 of the .hip file that defines `kernel` (name up to '<') and of the
+    headers under src/cnslmat it may include; None for an unknown kernel."""
+    import glob
+    import hashlib
+    src = KERNEL_SOURCES.get(kernel.split("<")[0].strip())
+    if src is None:
+        return None
+    h = hashlib.sha1()
+    for f in [src] + sorted(glob.glob(os.path.join(ROOT, "kaldi-cnn_amd/src/cnslmat/*.h"))):
+        path = f if os.path.isabs(f) else os.path.join(ROOT, f)
+        with open(path, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
 
 
 def parse_profile(text):
@@ -260,6 +290,89 @@ def cpu_baseline(frames_hint, budget_s=12.0):
             "host": {"cpu_model": model, "nproc": os.cpu_count(), "affinity": avail,
                      "threads_note": f"{threads} threads = one GPU's share of the box's "
                                      "host CPUs (the job's allotment)"}}
+
+
+def cpu_baseline_stack(config_text, frames, splice_frames=1, budget_s=8.0):
+    """The reference's CPU path for a whole config (c5, nnet.config): the C
+    oracle's components built from the config lines with random parameters,
+    one fwd + bwd + update step on a small sample of frames, OpenBLAS sgemm
+    for the AddMatMat legs; reported per frame and labelled as an
+    extrapolation from that sample."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    threads = max(1, min(16, avail))
+    O.use_blas(True)
+    O.set_threads(threads)
+    r = np.random.default_rng(2)
+
+    def build():
+        layers = []
+        for line in config_text.strip().splitlines():
+            t, *kvs = line.split()
+            kv = dict(x.split("=", 1) for x in kvs)
+            gi = lambda k, d=0: int(kv.get(k, d))
+            if t == "ConvolutionComponent":
+                c = O.Conv(gi("in-height"), gi("in-width"), gi("in-channel"),
+                           gi("kernel-height"), gi("kernel-width"), gi("group"),
+                           in_pad_height=gi("in-pad-height"), in_pad_width=gi("in-pad-width"))
+                kd = gi("kernel-height") * gi("kernel-width") * gi("in-channel")
+                c.W = (r.standard_normal((kd, gi("group"))) * 0.01).astype(np.float32)
+                c.b = (r.standard_normal(gi("group")) * 0.5).astype(np.float32)
+            elif t == "MaxpoolComponent":
+                c = O.Pool(gi("in-height"), gi("in-width"), gi("in-channel"),
+                           gi("pool-height-dim"), gi("pool-width-dim"), gi("pool-channel-dim"))
+            elif t == "FullyConnectedComponent":
+                c = O.FC(gi("input-dim"), gi("output-dim"))
+                c.W = (r.standard_normal((gi("output-dim"), gi("input-dim"))) * 0.01
+                       ).astype(np.float32)
+                c.b = np.ones(gi("output-dim"), np.float32)
+            elif t == "RectifiedLinearComponent":
+                c = O.ReLU(gi("dim"))
+            elif t == "SpliceComponent":
+                lc, rc = gi("left-context"), gi("right-context")
+                c = O.Splice(gi("input-dim"), tuple(range(-lc, rc + 1)))
+            else:
+                raise ValueError(t)
+            layers.append(c)
+        return layers
+
+    def step(n):
+        layers = build()
+        x = r.standard_normal((n * splice_frames, layers[0].input_dim)).astype(np.float32)
+        t0 = time.perf_counter()
+        ins = []
+        a = x
+        for c in layers:
+            ins.append(a)
+            a = c.propagate(a)
+        d = (r.standard_normal(a.shape) * 1e-2).astype(np.float32)
+        for c, a_in, a_out in zip(reversed(layers), reversed(ins), reversed(ins[1:] + [a])):
+            if isinstance(c, O.Pool):
+                d = c.backprop(a_in, a_out, d)
+            elif isinstance(c, O.ReLU):
+                d = c.backprop(a_out, d)
+            elif isinstance(c, O.Splice):
+                d = c.backprop(d)
+            else:
+                d = c.backprop(a_in, d, update=True)
+        return time.perf_counter() - t0
+
+    step(4)
+    t_small = step(8)
+    n = int(max(8, min(frames, 8 * budget_s / max(t_small, 1e-3))))
+    n = max(8, (n // 8) * 8)
+    t = step(n)
+    O.use_blas(False)
+    return {"value": round(n / t, 2), "unit": "frames/sec", "cores": threads, "kind": "port",
+            "sample": f"{n} frames, one fwd+bwd+update step of the whole config on the C "
+                      f"oracle with {threads} threads (OpenBLAS sgemm for AddMatMat); "
+                      f"per-frame rate extrapolated from this sample to the "
+                      f"{frames}-frame batch"}
 
 
 def baseline_config(frames_per_gpu, world):
@@ -475,8 +588,22 @@ def main():
                                                     PEAK_BF16_MFMA_TFLOPS, 4) if conv_ms else None},
                 "scopes_ms_per_step": scopes,
             }
+            if conv_ms:
+                # the convolution layers (implicit GEMM, weight gradient, frame
+                # kernels) as one MFMA-bound scope: fp32 work of fwd + dgrad +
+                # wgrad over the fp32 MFMA peak, no PMC pass of these configs
+                result["roofline"] = {
+                    "kernel": "conv layers (every ConvolutionComponent scope)", "bound": "mfma",
+                    "achieved": round(conv_flop / conv_ms / 1e9, 2),
+                    "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(conv_flop / conv_ms / 1e9 / PEAK_FP32_MFMA_TFLOPS, 4),
+                    "traffic": None, "algorithmic_flop_per_step": conv_flop}
             if dp:
                 result["dp"] = dp
+            if not args.no_cpu_baseline and world == 1:
+                text = NNET_CONFIG if args.config == "nnet" else c5_config()[0]
+                result["cpu_baseline"] = cpu_baseline_stack(
+                    text, B, splice_frames=21 if args.config == "nnet" else 1)
             line = json.dumps(result)
             print(line, flush=True)
             if args.json_out:
@@ -547,15 +674,18 @@ def main():
     roofline = None
     if dom:
         dk = kernels[dom]
-        traffic = None
+        traffic, traffic_kernel = None, None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        # the counter passes (scripts/gpu_profiles.sh) profile the default c2 step
+        # the counter passes (scripts/gpu_profiles.sh) profile the default c2
+        # step; their bytes count only for the same role, frame count and
+        # kernel source (a changed kernel makes them stale: traffic null)
         if os.path.exists(pmc) and not (args.no_fusion or args.store_conv_out):
             try:
                 ent = json.load(open(pmc)).get(dom, {})
-                # PMC bytes are per launch of the profiled run: only for that size
-                if ent.get("frames") == B:
+                if ent.get("frames") == B and ent.get("source_sha1") and \
+                        ent["source_sha1"] == kernel_source_digest(ent.get("kernel", "")):
                     traffic = ent.get("hbm_bytes_per_launch")
+                    traffic_kernel = ent.get("kernel")
             except Exception:
                 traffic = None
         if dk["bound"] == "mfma":
@@ -564,7 +694,7 @@ def main():
             achieved, peak, unit = dk["bytes"] / dk["ms"] / 1e6, PEAK_HBM_GBS, "GB/s"
         roofline = {"kernel": dom, "bound": dk["bound"], "achieved": round(achieved, 2),
                     "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
-                    "traffic": traffic,
+                    "traffic": traffic, "traffic_kernel": traffic_kernel,
                     "algorithmic_bytes_per_launch": dk["bytes"],
                     "algorithmic_flop_per_launch": dk["flop"],
                     "launch_ms": dk["ms"]}

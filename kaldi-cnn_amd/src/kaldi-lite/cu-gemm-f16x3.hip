@@ -28,8 +28,9 @@
 // near FLT_MAX or below 2^-110 is scaled like any other (the bf16x6 split
 // loses bits there).
 //
-// The scales come from per-row / per-column max |x| (kl_absmax: the bit
-// patterns of |x|, whose unsigned order is the magnitude order).  A row of
+// The scales come from per-row / per-column max |x| (kl_absmax_rows /
+// kl_absmax_cols: the bit patterns of |x|, whose unsigned order is the
+// magnitude order).  A row of
 // op(A) or a column of op(B) holding Inf or NaN has no scale; every C
 // element in it is Inf or NaN in IEEE arithmetic.  The kernels leave those
 // elements alone and gemm_f16x3_fixup_kernel computes them as plain fp32 dot
@@ -56,6 +57,9 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int BM = 256, BN = 128, BK = 32, NT = 512;
 constexpr int ROWB = BK * 2;                  // bytes per LDS row of one plane
@@ -79,6 +83,13 @@ struct GemmF16Args {
 __device__ __forceinline__ int swz(int r, int c) {
   return r * ROWB + ((c ^ ((r >> 2) & 3)) << 4);
 }
+// offset of (k, col) in a [k][R] image of 16-bit values, 16-B chunks XOR-
+// swizzled by (k & 3) << 2 so the four k-rows of one transposed read hit
+// four disjoint 16-bank groups (cu-gemm-x6.hip's fast kernel)
+template <int R>
+__device__ __forceinline__ int tswz(int k, int col) {
+  return k * (R * 2) + ((((col >> 3) ^ ((k & 3) << 2))) << 4) + ((col & 7) << 1);
+}
 
 // the scale exponent s for a row whose largest |x| has the bit pattern mb:
 // max |x| * 2^s in [2^14, 2^15)
@@ -90,50 +101,79 @@ __device__ __forceinline__ int scale_exp(uint32_t mb) {
   return 14 - e;
 }
 
-// (x0, x1) * 2^e -> packed f16 pairs hi, lo
-__device__ __forceinline__ void split2h(float x0, float x1, int e, uint32_t &h, uint32_t &l) {
-  const float a = __builtin_amdgcn_ldexpf(x0, e), b = __builtin_amdgcn_ldexpf(x1, e);
-  const f16x2 hp = __builtin_convertvector((f32x2){a, b}, f16x2);
-  const f16x2 lp = __builtin_convertvector((f32x2){a - (float)hp[0], b - (float)hp[1]}, f16x2);
-  h = __builtin_bit_cast(uint32_t, hp);
-  l = __builtin_bit_cast(uint32_t, lp);
+// a - (float)f16 half of h, in one v_fma_mix_f32 (a * 1.0 - h, exact here:
+// h is a's f16 rounding, so the difference is an fp32 number)
+__device__ __forceinline__ float sub_h0(float a, uint32_t h) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(r) : "v"(a), "v"(h));
+  return r;
+}
+__device__ __forceinline__ float sub_h1(float a, uint32_t h) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r)
+      : "v"(a), "v"(h));
+  return r;
+}
+// (x0 * 2^e0, x1 * 2^e1) -> packed f16 pairs hi, lo: 6 VALU
+__device__ __forceinline__ void split2h(float x0, float x1, int e0, int e1, uint32_t &h,
+                                        uint32_t &l) {
+  const float a = __builtin_amdgcn_ldexpf(x0, e0), b = __builtin_amdgcn_ldexpf(x1, e1);
+  h = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, f16x2));
+  l = __builtin_bit_cast(uint32_t,
+                         __builtin_convertvector((f32x2){sub_h0(a, h), sub_h1(b, h)}, f16x2));
 }
 
-// One operand tile (R rows of C's side x BK) per K step, gemm_x6d_kernel's
-// TileLoaderD with a two-plane f16 split.
-//   KC (K-contiguous source, element (row, k) at src[row * ld + k]):
-//     unit = (row, 8-k chunk), two 16-B loads;
-//   !KC (source stored [k][row]): unit = (row, KPT consecutive k), lanes
-//     along the row so each load instruction reads a contiguous run.
-// A thread's units keep their rows for the whole kernel, so each has one
-// scale exponent.
-template <int R, bool KC>
+// Operand tile loaders (R rows of C's side x BK per K step), loads two steps
+// ahead by branch-free buffer loads (gemm_x6d_kernel's TileLoaderD), split in
+// registers into the hi / lo planes.  Three source layouts:
+//   LK  K-contiguous (element (row, k) at src[row * ld + k]): unit = (row,
+//       8-k chunk), two 16-B loads; [row][k] image (swz), fragments by
+//       ds_read_b128;
+//   LR  row-contiguous ([k][row]) with one dword per lane: unit = (row, KPT
+//       consecutive k), lanes along the row; [row][k] image;
+//   LT  row-contiguous with 16-B loads along the rows (ld % 4 == 0, 16-B
+//       base, the row count a multiple of 4): unit = (4 rows, KQ k); [k][row]
+//       image (tswz), fragments by ds_read_b64_tr_b16.
+// Every row of a unit has its own scale exponent (e[]).
+enum { LK = 0, LR = 1, LT = 2 };
+
+template <int R, int MODE>
 struct Loader {
-  static constexpr int KPT = KC ? 8 : R * BK / NT;
-  static constexpr int UNITS = KC ? R * 4 : R * BK / KPT;
+  static constexpr int KPT = MODE == LK ? 8 : MODE == LR ? R * BK / NT : R * BK / (NT * 4);
+  static constexpr int UNITS = MODE == LK ? R * 4 : MODE == LR ? R * BK / KPT : NT;
   static constexpr int UPT = (UNITS + NT - 1) / NT;
-  static_assert(UNITS % NT == 0 && KPT % 8 == 0, "tile shape");
-  float v[UPT][KPT];
+  static constexpr int NE = MODE == LT ? 4 : UPT;  // exponents per thread
+  static_assert(UNITS % NT == 0, "tile shape");
+  static_assert(MODE != LR || KPT % 8 == 0, "tile shape");
+  static_assert(MODE != LT || (R / 4) * (BK / KPT) == NT, "tile shape");
+  static constexpr int NV = MODE == LT ? 4 * KPT : KPT;  // values per unit
+  float v[UPT][NV];
+  int e[NE];
 
-  __device__ static __forceinline__ int row_of(int u, int tid) {
-    const int unit = tid + u * NT;
-    return KC ? unit >> 2 : unit % R;
+  // first row of exponent i
+  __device__ static __forceinline__ int row_of(int i, int tid) {
+    if constexpr (MODE == LT) return 4 * (tid % (R / 4)) + i;
+    const int unit = tid + i * NT;
+    return MODE == LK ? unit >> 2 : unit % R;
   }
-  __device__ static __forceinline__ int k_of(int u, int tid) {
-    const int unit = tid + u * NT;
-    return KC ? (unit & 3) * 8 : (unit / R) * KPT;
+  __device__ __forceinline__ void init_exp(const int *sexp, int tid) {
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int s = sexp[row_of(i, tid)];
+      e[i] = s == SKIP ? 0 : s;
+    }
   }
 
-  // base: KC, the tile's first row (src + row0 * ld); !KC, the split's first
-  // k and the tile's first column (src + kbeg * ld + row0).  Rows past the
-  // matrix read past the buffer's range (0).
+  // base: LK, the tile's first row (src + row0 * ld); LR / LT, the split's
+  // first k and the tile's first column (src + kbeg * ld + row0).  Rows past
+  // the matrix read past the buffer's range (0).
   __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, int ld, int vrows, int kk,
                                        int tid) {
     constexpr unsigned OOB = 0x80000000u;
 #pragma unroll
     for (int u = 0; u < UPT; ++u) {
       const int unit = tid + u * NT;
-      if constexpr (KC) {
+      if constexpr (MODE == LK) {
         const int r = unit >> 2, k = kk + (unit & 3) * 8;
         const unsigned off = r < vrows ? (unsigned)(r * ld + k) * 4u : OOB;
         const auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
@@ -143,12 +183,21 @@ struct Loader {
           v[u][j] = __uint_as_float(a[j]);
           v[u][4 + j] = __uint_as_float(b[j]);
         }
-      } else {
+      } else if constexpr (MODE == LR) {
         const int r = unit % R, k = kk + (unit / R) * KPT;
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
           const unsigned off = r < vrows ? (unsigned)((k + j) * ld + r) * 4u : OOB;
           v[u][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+        }
+      } else {
+        const int rq = unit % (R / 4), k = kk + (unit / (R / 4)) * KPT;
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+          const unsigned off = 4 * rq < vrows ? (unsigned)((k + j) * ld + 4 * rq) * 4u : OOB;
+          const auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[u][4 * j + i] = __uint_as_float(a[i]);
         }
       }
     }
@@ -158,38 +207,125 @@ struct Loader {
   // tile is the last, partial one and its k >= kv are zeroed (they are the
   // next row's values or a pitch's padding)
   template <int PL>
-  __device__ __forceinline__ void store(char *lds, int tid, const int (&e)[UPT],
-                                        int kv) const {
+  __device__ __forceinline__ void store(char *lds, int tid, int kv) const {
 #pragma unroll
     for (int u = 0; u < UPT; ++u) {
       const int unit = tid + u * NT;
-      int r, c0;
-      if constexpr (KC) {
+      float x[NV];
+#pragma unroll
+      for (int j = 0; j < NV; ++j) x[j] = v[u][j];
+      if constexpr (MODE == LT) {
+        const int rq = unit % (R / 4), kq = unit / (R / 4);
+        if (kv < BK) {
+#pragma unroll
+          for (int j = 0; j < KPT; ++j)
+            if (kq * KPT + j >= kv)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) x[4 * j + i] = 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+          uint32_t h0, l0, h1, l1;
+          split2h(x[4 * j], x[4 * j + 1], e[0], e[1], h0, l0);
+          split2h(x[4 * j + 2], x[4 * j + 3], e[2], e[3], h1, l1);
+          const int o = tswz<R>(kq * KPT + j, 4 * rq);
+          *reinterpret_cast<uint2 *>(lds + o) = make_uint2(h0, h1);
+          *reinterpret_cast<uint2 *>(lds + PL + o) = make_uint2(l0, l1);
+        }
+      } else {
+        int r, c0, kb;
+        if constexpr (MODE == LK) {
+          r = unit >> 2;
+          c0 = unit & 3;
+          kb = c0 * 8;
+        } else {
+          r = unit % R;
+          c0 = (unit / R) * (KPT / 8);
+          kb = (unit / R) * KPT;
+        }
+        if (kv < BK) {
+#pragma unroll
+          for (int j = 0; j < KPT; ++j)
+            if (kb + j >= kv) x[j] = 0.0f;
+        }
+#pragma unroll
+        for (int cc = 0; cc < KPT / 8; ++cc) {
+          uint32_t h[4], l[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            split2h(x[cc * 8 + 2 * i], x[cc * 8 + 2 * i + 1], e[u], e[u], h[i], l[i]);
+          const int off = swz(r, c0 + cc);
+          *reinterpret_cast<uint4 *>(lds + off) = make_uint4(h[0], h[1], h[2], h[3]);
+          *reinterpret_cast<uint4 *>(lds + PL + off) = make_uint4(l[0], l[1], l[2], l[3]);
+        }
+      }
+    }
+  }
+
+  // The split of store() in NPIECE pieces of one pair each, for the fast
+  // kernel's interleaving with MFMAs: piece pc splits one pair into the
+  // caller's temporaries; a unit's (LK, LR) or a k-row's (LT) plane writes go
+  // with its last piece
+  static constexpr int NPIECE = MODE == LT ? 2 * KPT : UPT * (KPT / 2);
+  template <int PL>
+  __device__ __forceinline__ void piece(char *lds, int tid, int pc, int kv, uint32_t (&ph)[4],
+                                        uint32_t (&pl)[4]) const {
+    if constexpr (MODE == LT) {
+      const int j = pc >> 1, hf = pc & 1;
+      const int unit = tid;
+      const int rq = unit % (R / 4), kq = unit / (R / 4);
+      float x0 = v[0][4 * j + 2 * hf], x1 = v[0][4 * j + 2 * hf + 1];
+      if (kv < BK && kq * KPT + j >= kv) x0 = x1 = 0.0f;
+      split2h(x0, x1, e[2 * hf], e[2 * hf + 1], ph[hf], pl[hf]);
+      if (hf == 1) {
+        const int o = tswz<R>(kq * KPT + j, 4 * rq);
+        *reinterpret_cast<uint2 *>(lds + o) = make_uint2(ph[0], ph[1]);
+        *reinterpret_cast<uint2 *>(lds + PL + o) = make_uint2(pl[0], pl[1]);
+      }
+    } else {
+      constexpr int PPU = KPT / 2;  // pieces per unit
+      const int u = pc / PPU, q = pc % PPU;
+      const int unit = tid + u * NT;
+      int r, c0, kb;
+      if constexpr (MODE == LK) {
         r = unit >> 2;
         c0 = unit & 3;
+        kb = c0 * 8;
       } else {
         r = unit % R;
         c0 = (unit / R) * (KPT / 8);
+        kb = (unit / R) * KPT;
       }
-      float x[KPT];
-#pragma unroll
-      for (int j = 0; j < KPT; ++j) x[j] = v[u][j];
+      float x0 = v[u][2 * q], x1 = v[u][2 * q + 1];
       if (kv < BK) {
-        const int kb = k_of(u, tid);
-#pragma unroll
-        for (int j = 0; j < KPT; ++j)
-          if (kb + j >= kv) x[j] = 0.0f;
+        if (kb + 2 * q >= kv) x0 = 0.0f;
+        if (kb + 2 * q + 1 >= kv) x1 = 0.0f;
       }
-#pragma unroll
-      for (int cc = 0; cc < KPT / 8; ++cc) {
-        uint32_t h[4], l[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          split2h(x[cc * 8 + 2 * i], x[cc * 8 + 2 * i + 1], e[u], h[i], l[i]);
-        const int off = swz(r, c0 + cc);
-        *reinterpret_cast<uint4 *>(lds + off) = make_uint4(h[0], h[1], h[2], h[3]);
-        *reinterpret_cast<uint4 *>(lds + PL + off) = make_uint4(l[0], l[1], l[2], l[3]);
+      split2h(x0, x1, e[u], e[u], ph[q & 3], pl[q & 3]);
+      if ((q & 3) == 3) {
+        const int off = swz(r, c0 + (q >> 2));
+        *reinterpret_cast<uint4 *>(lds + off) = make_uint4(ph[0], ph[1], ph[2], ph[3]);
+        *reinterpret_cast<uint4 *>(lds + PL + off) = make_uint4(pl[0], pl[1], pl[2], pl[3]);
       }
+    }
+  }
+  // fragment reads per MFMA fragment (LT: two transposed 8-B reads)
+  static constexpr int NRD = MODE == LT ? 2 : 1;
+
+  // MFMA fragment: 32 rows from rb, k16 half s (lane l: row l & 31, k 8 (l >> 5) + 0..7)
+  __device__ static __forceinline__ f16x8 frag(const char *plane, int rb, int s, int lane) {
+    if constexpr (MODE != LT) {
+      return *reinterpret_cast<const f16x8 *>(plane + swz(rb + (lane & 31), 2 * s + (lane >> 5)));
+    } else {
+      const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+      const int k = 16 * s + 8 * (g >> 1) + q;
+      const int col = rb + 16 * (g & 1) + 4 * pp;
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s16x4 *)(plane + tswz<R>(k, col)));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s16x4 *)(plane + tswz<R>(k + 4, col)));
+      const s16x8 c = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      return __builtin_bit_cast(f16x8, c);
     }
   }
 };
@@ -198,8 +334,9 @@ __device__ __forceinline__ f32x16 mfma(const f16x8 &a, const f16x8 &b, const f32
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-template <bool A_KC, bool B_KC>
+template <int AM, int BMODE>
 __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
+  constexpr bool A_KC = AM == LK, B_KC = BMODE == LK;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int *sexp = reinterpret_cast<int *>(lds + 2 * BUF);  // [BM] rows, then [BN] columns
   const int tid = threadIdx.x;
@@ -244,8 +381,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
   // k of tile t relative to the base (clamped to the last tile: a re-read)
   auto kk = [&](int t, bool kc) { return (kc ? kbeg : 0) + min(t, T - 1) * BK; };
 
-  using LA = Loader<BM, A_KC>;
-  using LB = Loader<BN, B_KC>;
+  using LA = Loader<BM, AM>;
+  using LB = Loader<BN, BMODE>;
   LA la[2];
   LB lb[2];
   f32x16 acc[2][2];
@@ -256,23 +393,16 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
 #pragma unroll
       for (int g = 0; g < 16; ++g) acc[i][j][g] = 0.0f;
   __syncthreads();  // sexp
-  int ea[LA::UPT], eb[LB::UPT];
-#pragma unroll
-  for (int u = 0; u < LA::UPT; ++u) {
-    const int s = sexp[LA::row_of(u, tid)];
-    ea[u] = s == SKIP ? 0 : s;
-  }
-#pragma unroll
-  for (int u = 0; u < LB::UPT; ++u) {
-    const int s = sexp[BM + LB::row_of(u, tid)];
-    eb[u] = s == SKIP ? 0 : s;
-  }
+  la[0].init_exp(sexp, tid);
+  la[1].init_exp(sexp, tid);
+  lb[0].init_exp(sexp + BM, tid);
+  lb[1].init_exp(sexp + BM, tid);
 
   if (T > 0) {
     la[0].load(rsA, p.lda, vra, kk(0, A_KC), tid);
     lb[0].load(rsB, p.ldb, vrb, kk(0, B_KC), tid);
-    la[0].template store<A_PLANE>(lds, tid, ea, T == 1 ? klast : BK);
-    lb[0].template store<B_PLANE>(lds + 2 * A_PLANE, tid, eb, T == 1 ? klast : BK);
+    la[0].template store<A_PLANE>(lds, tid, T == 1 ? klast : BK);
+    lb[0].template store<B_PLANE>(lds + 2 * A_PLANE, tid, T == 1 ? klast : BK);
     // tiles 1, 2 into sets 1, 0 (as at every later loop entry)
     __builtin_amdgcn_sched_barrier(0);
     la[1].load(rsA, p.lda, vra, kk(1, A_KC), tid);
@@ -282,19 +412,17 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
     lb[0].load(rsB, p.ldb, vrb, kk(2, B_KC), tid);
     __syncthreads();
 
-    const int ar = wm * 64 + (lane & 31), br = wn * 64 + (lane & 31);
-    const int half = lane >> 5;
-    // one k16 half of a step: 8 fragment reads, 12 MFMAs
+    const int ar = wm * 64, br = wn * 64;
+    // one k16 half of a step: 8 fragments, 12 MFMAs
     auto half_step = [&](const char *bufA, int s) {
       const char *bufB = bufA + 2 * A_PLANE;
       f16x8 a[2][2], bb[2][2];
-      const int c = 2 * s + half;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int pl = 0; pl < 2; ++pl) {
-          a[i][pl] = *reinterpret_cast<const f16x8 *>(bufA + pl * A_PLANE + swz(ar + 32 * i, c));
-          bb[i][pl] = *reinterpret_cast<const f16x8 *>(bufB + pl * B_PLANE + swz(br + 32 * i, c));
+          a[i][pl] = LA::frag(bufA + pl * A_PLANE, ar + 32 * i, s, lane);
+          bb[i][pl] = LB::frag(bufB + pl * B_PLANE, br + 32 * i, s, lane);
         }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -320,13 +448,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
         const int kv = t + 2 == T ? klast : BK;
         half_step(buf, 0);
         if (!late && t + 1 < T) {
-          lan.template store<A_PLANE>(nA, tid, ea, kv);
-          lbn.template store<B_PLANE>(nA + 2 * A_PLANE, tid, eb, kv);
+          lan.template store<A_PLANE>(nA, tid, kv);
+          lbn.template store<B_PLANE>(nA + 2 * A_PLANE, tid, kv);
         }
         half_step(buf, 1);
         if (late && t + 1 < T) {
-          lan.template store<A_PLANE>(nA, tid, ea, kv);
-          lbn.template store<B_PLANE>(nA + 2 * A_PLANE, tid, eb, kv);
+          lan.template store<A_PLANE>(nA, tid, kv);
+          lbn.template store<B_PLANE>(nA + 2 * A_PLANE, tid, kv);
         }
       }
       lan.load(rsA, p.lda, vra, kk(t + 3, A_KC), tid);
@@ -341,6 +469,182 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
 
   // C/D map of 32x32x16: register g of lane l holds
   // row (g & 3) + 8 (g >> 2) + 4 (l >> 5), column l & 31.
+  float *out = p.partial ? p.C + (int64_t)split * p.M * p.N : p.C;
+  const int ldo = p.partial ? p.N : p.ldc;
+  const int half2 = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int cl = wn * 64 + j * 32 + (lane & 31);
+      const int col = col0 + cl;
+      const int ec = sexp[BM + cl];
+      if (col >= p.N || ec == SKIP) continue;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int rl = wm * 64 + i * 32 + (g & 3) + 8 * (g >> 2) + 4 * half2;
+        const int row = row0 + rl;
+        const int er = sexp[rl];
+        if (row >= p.M || er == SKIP) continue;
+        const float v = __builtin_amdgcn_ldexpf(acc[i][j][g], -(er + ec));
+        float *o = out + (int64_t)row * ldo + col;
+        if (p.partial) *o = v;
+        else *o = p.beta == 0.0f ? p.alpha * v : p.alpha * v + p.beta * *o;
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// gemm_f16x3_fast_kernel: gemm_f16x3_kernel's arithmetic (the same images,
+// fragments and MFMA order into every accumulator: bitwise the same C) with
+// one barrier per K step in its middle and the LDS traffic moved under the
+// MFMAs.  K step t:
+//   phase A: the 12 k16-half-0 MFMAs (fragments F0, read in the previous
+//            phase B); beside them the split of tile t+1 into the other
+//            buffer (one pair per MFMA) and the reads of the half-1
+//            fragments F1;
+//   barrier: tile t+1 written, buffer t & 1 read by every wave;
+//   phase B: the 12 half-1 MFMAs; beside them the F0 reads of step t+1 (from
+//            the other buffer) and the HBM loads of tile t+3.
+// Each MFMA and the work placed after it are fenced (sched_barrier), so this
+// is the issue order.  The bf16x6 kernel of this shape (cu-gemm-x6.hip
+// gemm_x6_fast_kernel) measured no faster: its six products held the chip at
+// its power limit.  f16x3's three leave the clock up, and the MFMA pipe idles
+// on LDS latency instead (35-44 % busy at 2.1-2.3 GHz with the two-phase
+// loop).
+template <int AM, int BMODE>
+__global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
+  constexpr bool A_KC = AM == LK, B_KC = BMODE == LK;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  int *sexp = reinterpret_cast<int *>(lds + 2 * BUF);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, q = nb >> 3, rr = nb & 7;
+  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
+  const int split = lid % p.ksplit;
+  const int rest = lid / p.ksplit;
+  const int tn = rest % p.tiles_n, tm = rest / p.tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const int kbeg = split * p.kps;
+  const int kend = min(p.K, kbeg + p.kps);
+  const int T = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  const int klast = kend - kbeg - (T - 1) * BK;
+
+  for (int i = tid; i < BM + BN; i += NT) {
+    int s = 0;
+    if (i < BM) {
+      if (row0 + i < p.M) s = scale_exp(p.amax[row0 + i]);
+    } else if (col0 + i - BM < p.N) {
+      s = scale_exp(p.bmax[col0 + i - BM]);
+    }
+    sexp[i] = s;
+  }
+  const float *baseA = A_KC ? p.A + (int64_t)row0 * p.lda : p.A + (int64_t)kbeg * p.lda + row0;
+  const float *baseB = B_KC ? p.B + (int64_t)col0 * p.ldb : p.B + (int64_t)kbeg * p.ldb + col0;
+  const int vra = p.M - row0, vrb = p.N - col0;
+  const int64_t endA = A_KC ? ((int64_t)(vra - 1) * p.lda + p.K) * 4
+                            : ((int64_t)(p.K - 1 - kbeg) * p.lda + vra) * 4;
+  const int64_t endB = B_KC ? ((int64_t)(vrb - 1) * p.ldb + p.K) * 4
+                            : ((int64_t)(p.K - 1 - kbeg) * p.ldb + vrb) * 4;
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)baseA, (short)0, (int)(endA < 0x7fffffff ? endA : 0x7fffffff), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)baseB, (short)0, (int)(endB < 0x7fffffff ? endB : 0x7fffffff), 0x00020000);
+  auto kk = [&](int t, bool kc) { return (kc ? kbeg : 0) + min(t, T - 1) * BK; };
+
+  using LA = Loader<BM, AM>;
+  using LB = Loader<BN, BMODE>;
+  LA la[2];
+  LB lb[2];
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) acc[i][j][g] = 0.0f;
+  __syncthreads();  // sexp
+  la[0].init_exp(sexp, tid);
+  la[1].init_exp(sexp, tid);
+  lb[0].init_exp(sexp + BM, tid);
+  lb[1].init_exp(sexp + BM, tid);
+
+  const int ar = wm * 64, br = wn * 64;
+  f16x8 fa0[2][2], fb0[2][2], fa1[2][2], fb1[2][2];
+  // r-th fragment of half s: A fragments (i, plane) first, then B
+  auto read_frag = [&](const char *buf, int s, int r, f16x8 (&fa)[2][2], f16x8 (&fb)[2][2]) {
+    if (r < 4) {
+      const int i = r >> 1, pl = r & 1;
+      fa[i][pl] = LA::frag(buf + pl * A_PLANE, ar + 32 * i, s, lane);
+    } else {
+      const int i = (r - 4) >> 1, pl = (r - 4) & 1;
+      fb[i][pl] = LB::frag(buf + 2 * A_PLANE + pl * B_PLANE, br + 32 * i, s, lane);
+    }
+  };
+  // n-th MFMA of a half: accumulator (n / 6, (n / 3) % 2), lo.hi, hi.lo, hi.hi
+  auto mfma_n = [&](int n, const f16x8 (&fa)[2][2], const f16x8 (&fb)[2][2]) {
+    const int i = n / 6, j = (n / 3) & 1, pr = n % 3;
+    constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};
+    acc[i][j] = mfma(fa[i][PA[pr]], fb[j][PB[pr]], acc[i][j]);
+  };
+
+  if (T > 0) {
+    la[0].load(rsA, p.lda, vra, kk(0, A_KC), tid);
+    lb[0].load(rsB, p.ldb, vrb, kk(0, B_KC), tid);
+    la[0].template store<A_PLANE>(lds, tid, T == 1 ? klast : BK);
+    lb[0].template store<B_PLANE>(lds + 2 * A_PLANE, tid, T == 1 ? klast : BK);
+    __builtin_amdgcn_sched_barrier(0);
+    la[1].load(rsA, p.lda, vra, kk(1, A_KC), tid);
+    lb[1].load(rsB, p.ldb, vrb, kk(1, B_KC), tid);
+    __builtin_amdgcn_sched_barrier(0);
+    la[0].load(rsA, p.lda, vra, kk(2, A_KC), tid);
+    lb[0].load(rsB, p.ldb, vrb, kk(2, B_KC), tid);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) read_frag(lds, 0, r, fa0, fb0);
+
+    // step t: tile t+1 is in set (t+1) & 1 (split in phase A), which then
+    // takes tile t+3 (phase B; a step past T issues its clamped loads too)
+    auto step = [&](int t, LA &lan, LB &lbn) {
+      const char *buf = lds + (t & 1) * BUF;
+      char *nbuf = lds + ((t + 1) & 1) * BUF;
+      const bool more = t + 1 < T;  // uniform
+      const int kv = t + 2 == T ? klast : BK;
+      uint32_t ph[4], pl[4];
+      // phase A
+#pragma unroll
+      for (int n = 0; n < 12; ++n) {
+        mfma_n(n, fa0, fb0);
+        if (more) {
+          if (n < LA::NPIECE)
+            lan.template piece<A_PLANE>(nbuf, tid, n, kv, ph, pl);
+          else if (n - LA::NPIECE < LB::NPIECE)
+            lbn.template piece<B_PLANE>(nbuf + 2 * A_PLANE, tid, n - LA::NPIECE, kv, ph, pl);
+        }
+        if (n >= 2 && n < 10) read_frag(buf, 1, n - 2, fa1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __syncthreads();
+      // phase B
+#pragma unroll
+      for (int n = 0; n < 12; ++n) {
+        mfma_n(n, fa1, fb1);
+        if (n == 1) lan.load(rsA, p.lda, vra, kk(t + 3, A_KC), tid);
+        if (n == 3) lbn.load(rsB, p.ldb, vrb, kk(t + 3, B_KC), tid);
+        if (more && n >= 2 && n < 10) read_frag(nbuf, 0, n - 2, fa0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    int t = 0;
+    for (; t + 1 < T; t += 2) {
+      step(t, la[1], lb[1]);
+      step(t + 1, la[0], lb[0]);
+    }
+    if (t < T) step(t, la[1], lb[1]);
+  }
+
   float *out = p.partial ? p.C + (int64_t)split * p.M * p.N : p.C;
   const int ldo = p.partial ? p.N : p.ldc;
   const int half2 = lane >> 5;
@@ -408,16 +712,25 @@ __global__ void gemm_f16x3_reduce_kernel(const float *__restrict__ part, int S, 
 struct FixupArgs {
   const float *A, *B;
   float *C;
-  const uint32_t *amax, *bmax, *aflag, *bflag;
+  const uint32_t *amax, *bmax;
   int M, N, K, lda, ldb, ldc, transA, transB;
   float alpha, beta;
 };
 
 // The C elements of every row of op(A) / column of op(B) holding Inf or
 // NaN, as fp32 dot products in increasing k (IEEE: the reference sgemm's
-// Inf / NaN pattern).  Returns at once when no operand holds one.
-__global__ void gemm_f16x3_fixup_kernel(FixupArgs f) {
-  if ((*f.aflag | *f.bflag) == 0) return;
+// Inf / NaN pattern).  Each block first scans the M + N maxima (from L2) and
+// returns at once when none is Inf / NaN.
+__global__ __launch_bounds__(256) void gemm_f16x3_fixup_kernel(FixupArgs f) {
+  __shared__ int any;
+  if (threadIdx.x == 0) any = 0;
+  __syncthreads();
+  bool bad = false;
+  for (int e = threadIdx.x; e < f.M + f.N; e += blockDim.x)
+    bad |= (e < f.M ? f.amax[e] : f.bmax[e - f.M]) >= NONFINITE;
+  if (bad) any = 1;
+  __syncthreads();
+  if (!any) return;
   const int64_t total = (int64_t)f.M * f.N;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -434,64 +747,123 @@ __global__ void gemm_f16x3_fixup_kernel(FixupArgs f) {
   }
 }
 
-// Per-row and per-column max |x| of a pitched fp32 matrix as float bit
-// patterns (atomicMax on the unsigned bits: order-independent, so the result
-// is deterministic), and *flag = 1 when an element is Inf or NaN.  A block
-// covers rb rows x AM_CW columns: thread t reads float4 t + 256 j (j <
-// AM_NV) of each row (16-B loads when aligned, 1 KiB per wave instruction),
-// keeps its 16 column maxima in registers over the rows, and the row maximum
-// takes one wave reduction per row; the column maxima go out once per block.
-constexpr int AM_NV = 4, AM_CW = 1024 * AM_NV;
+// Max |x| per row or per column of a pitched fp32 matrix, as the bit
+// patterns of |x| (unsigned order = magnitude order, Inf / NaN above every
+// finite value; max is order-independent, so the results are deterministic).
+//  absmax_rows_kernel: one wave per row, 16-B loads four at a time, one wave
+//    reduction per row, a plain store (no atomics, no initialisation);
+//  absmax_cols_kernel: block (cb, rc) covers 1024 columns (4 per thread) of
+//    a chunk of rows and stores its column maxima as partial rc;
+//    absmax_cols_finalize_kernel takes the maxima over the chunks (64
+//    columns x 4 chunk groups per block, combined through LDS).
 template <bool VEC>
-__global__ __launch_bounds__(256) void absmax_kernel(const float *__restrict__ X, int rows,
-                                                    int cols, int ld, int rb, uint32_t *rmax,
-                                                    uint32_t *cmax, uint32_t *flag) {
-  const int c0 = blockIdx.x * AM_CW + threadIdx.x * 4;
-  const int r0 = blockIdx.y * rb;
-  const int rend = min(rows, r0 + rb);
-  uint32_t cm[AM_NV][4];
+__global__ __launch_bounds__(256) void absmax_rows_kernel(const float *__restrict__ X, int rows,
+                                                         int cols, int ld, uint32_t *rmax) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const float *x = X + (int64_t)r * ld;
+  uint32_t m = 0;
+  int c = lane * 4;
+  if (VEC) {
+    for (; c + 3 * 256 + 4 <= cols; c += 4 * 256) {
+      float4 q[4];
 #pragma unroll
-  for (int j = 0; j < AM_NV; ++j)
+      for (int j = 0; j < 4; ++j) q[j] = *reinterpret_cast<const float4 *>(x + c + j * 256);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) cm[j][i] = 0u;
-  for (int r = r0; r < rend; ++r) {
-    const float *x = X + (int64_t)r * ld;
-    uint32_t m = 0;
-#pragma unroll
-    for (int j = 0; j < AM_NV; ++j) {
-      const int c = c0 + j * 1024;
-      uint32_t v[4];
-      if (VEC && c + 4 <= cols) {
-        const float4 q = *reinterpret_cast<const float4 *>(x + c);
-        v[0] = __float_as_uint(q.x); v[1] = __float_as_uint(q.y);
-        v[2] = __float_as_uint(q.z); v[3] = __float_as_uint(q.w);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = c + i < cols ? __float_as_uint(x[c + i]) : 0u;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v[i] &= 0x7fffffffu;
-        cm[j][i] = max(cm[j][i], v[i]);
-        m = max(m, v[i]);
-      }
+      for (int j = 0; j < 4; ++j)
+        m = max(max(max(m, __float_as_uint(q[j].x) & 0x7fffffffu),
+                    max(__float_as_uint(q[j].y) & 0x7fffffffu,
+                        __float_as_uint(q[j].z) & 0x7fffffffu)),
+                __float_as_uint(q[j].w) & 0x7fffffffu);
     }
-    if (rmax) {
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
-      if ((threadIdx.x & 63) == 0 && m) atomicMax(rmax + r, m);
+    for (; c + 4 <= cols; c += 256) {
+      const float4 q = *reinterpret_cast<const float4 *>(x + c);
+      m = max(max(max(m, __float_as_uint(q.x) & 0x7fffffffu),
+                  max(__float_as_uint(q.y) & 0x7fffffffu, __float_as_uint(q.z) & 0x7fffffffu)),
+              __float_as_uint(q.w) & 0x7fffffffu);
     }
   }
-  uint32_t all = 0;
+  for (; c < cols; c += 256)
 #pragma unroll
-  for (int j = 0; j < AM_NV; ++j)
+    for (int i = 0; i < 4; ++i)
+      if (c + i < cols) m = max(m, __float_as_uint(x[c + i]) & 0x7fffffffu);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = c0 + j * 1024 + i;
-      all = max(all, cm[j][i]);
-      if (cmax && c < cols && cm[j][i]) atomicMax(cmax + c, cm[j][i]);
+  for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
+  if (lane == 0) rmax[r] = m;
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void absmax_cols_kernel(const float *__restrict__ X, int rows,
+                                                         int cols, int ld, int rb,
+                                                         uint32_t *part) {
+  const int c0 = blockIdx.x * 1024 + threadIdx.x * 4;
+  const int r0 = blockIdx.y * rb, rend = min(rows, r0 + rb);
+  if (c0 >= cols) return;
+  uint32_t cm[4] = {0u, 0u, 0u, 0u};
+  auto take = [&](const uint32_t (&v)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cm[i] = max(cm[i], v[i] & 0x7fffffffu);
+  };
+  auto load = [&](int r, uint32_t (&v)[4]) {
+    const float *x = X + (int64_t)r * ld + c0;
+    if (VEC && c0 + 4 <= cols) {
+      const float4 q = *reinterpret_cast<const float4 *>(x);
+      v[0] = __float_as_uint(q.x); v[1] = __float_as_uint(q.y);
+      v[2] = __float_as_uint(q.z); v[3] = __float_as_uint(q.w);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = c0 + i < cols ? __float_as_uint(x[i]) : 0u;
     }
-  if (all >= NONFINITE) atomicOr(flag, 1u);
+  };
+  int r = r0;
+  for (; r + 4 <= rend; r += 4) {
+    uint32_t v0[4], v1[4], v2[4], v3[4];
+    load(r, v0); load(r + 1, v1); load(r + 2, v2); load(r + 3, v3);
+    take(v0); take(v1); take(v2); take(v3);
+  }
+  for (; r < rend; ++r) {
+    uint32_t v[4];
+    load(r, v);
+    take(v);
+  }
+  uint32_t *dst = part + (size_t)blockIdx.y * cols + c0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (c0 + i < cols) dst[i] = cm[i];
+}
+
+__global__ __launch_bounds__(256) void absmax_cols_finalize_kernel(const uint32_t *part,
+                                                                  int nchunk, int cols,
+                                                                  uint32_t *cmax) {
+  __shared__ uint32_t red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
+  uint32_t m = 0;
+  if (c < cols) {
+    int p = grp;
+    for (; p + 12 < nchunk; p += 16)
+      m = max(max(m, part[(size_t)p * cols + c]),
+              max(max(part[(size_t)(p + 4) * cols + c], part[(size_t)(p + 8) * cols + c]),
+                  part[(size_t)(p + 12) * cols + c]));
+    for (; p < nchunk; p += 4) m = max(m, part[(size_t)p * cols + c]);
+  }
+  red[grp][threadIdx.x & 63] = m;
+  __syncthreads();
+  if (grp == 0 && c < cols)
+    cmax[c] = max(max(red[0][threadIdx.x], red[1][threadIdx.x]),
+                  max(red[2][threadIdx.x], red[3][threadIdx.x]));
+}
+
+struct ColsPlan {
+  int cb, rbk, rb;
+};
+// about 1024 blocks of at least 16 rows, at most 256 row chunks
+ColsPlan cols_plan(int rows, int cols) {
+  ColsPlan p;
+  p.cb = (cols + 1023) / 1024;
+  p.rbk = std::max(1, std::min(256, std::min((rows + 15) / 16, (1024 + p.cb - 1) / p.cb)));
+  p.rb = (rows + p.rbk - 1) / p.rbk;
+  p.rbk = (rows + p.rb - 1) / p.rb;
+  return p;
 }
 
 int choose_ksplit(int64_t tiles, int K) {
@@ -507,15 +879,44 @@ int choose_ksplit(int64_t tiles, int K) {
   return best;
 }
 
-template <bool A_KC, bool B_KC>
-void launch(const GemmF16Args &a, unsigned blocks, hipStream_t st) {
+// KCNN_F16X3_FAST (experiment build): 1 (default) the one-barrier fast
+// kernel where no operand is LR, 0 the two-phase kernel (bitwise the same C)
+template <int AM, int BMODE>
+void launch_t(const GemmF16Args &a, unsigned blocks, hipStream_t st) {
+  static const int fast = KCNN_KNOB("KCNN_F16X3_FAST", 1);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_f16x3_kernel<A_KC, B_KC>),
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_f16x3_kernel<AM, BMODE>),
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                LDS_BYTES) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL((gemm_f16x3_kernel<A_KC, B_KC>), dim3(blocks), dim3(NT), LDS_BYTES, st, a);
+  // (an LR operand's 16 loaded values per thread and K step spill there)
+  if constexpr (AM != LR && BMODE != LR) {
+    static bool fattr = [] {
+      return hipFuncSetAttribute(
+                 reinterpret_cast<const void *>(&gemm_f16x3_fast_kernel<AM, BMODE>),
+                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
+    }();
+    (void)fattr;
+    if (fast) {
+      hipLaunchKernelGGL((gemm_f16x3_fast_kernel<AM, BMODE>), dim3(blocks), dim3(NT),
+                         LDS_BYTES, st, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((gemm_f16x3_kernel<AM, BMODE>), dim3(blocks), dim3(NT), LDS_BYTES, st, a);
+}
+void launch(int am, int bm, const GemmF16Args &a, unsigned blocks, hipStream_t st) {
+  // am: LK or a row-contiguous mode; bm likewise
+  if (am == LK && bm == LK) launch_t<LK, LK>(a, blocks, st);
+  else if (am == LK && bm == LT) launch_t<LK, LT>(a, blocks, st);
+  else if (am == LK) launch_t<LK, LR>(a, blocks, st);
+  else if (am == LT && bm == LK) launch_t<LT, LK>(a, blocks, st);
+  else if (am == LT && bm == LT) launch_t<LT, LT>(a, blocks, st);
+  else if (am == LT) launch_t<LT, LR>(a, blocks, st);
+  else if (bm == LK) launch_t<LR, LK>(a, blocks, st);
+  else if (bm == LT) launch_t<LR, LT>(a, blocks, st);
+  else launch_t<LR, LR>(a, blocks, st);
 }
 
 size_t align16(size_t b) { return (b + 15) & ~(size_t)15; }
@@ -524,36 +925,51 @@ size_t partial_bytes(int M, int N, int K) {
   const int s = choose_ksplit(tiles, K);
   return s > 1 ? align16(sizeof(float) * (size_t)s * M * N) : 0;
 }
-size_t stats_words(int rows, int cols) { return 4 + (size_t)rows + cols; }
-
 }  // namespace
 
-extern "C" int kl_absmax(const float *X, int rows, int cols, int ld, uint32_t *st,
-                         int want_rows, int want_cols, kcnn_stream_t stream) {
-  if (rows < 0 || cols < 0 || ld < cols || !st) return (int)hipErrorInvalidValue;
+extern "C" int kl_absmax_rows(const float *X, int rows, int cols, int ld, uint32_t *rmax,
+                              kcnn_stream_t stream) {
+  if (rows < 0 || cols < 0 || ld < cols || !rmax) return (int)hipErrorInvalidValue;
+  if (rows == 0) return 0;
   hipStream_t s = kcnn::as_stream(stream);
-  hipError_t e = hipMemsetAsync(st, 0, sizeof(uint32_t) * stats_words(rows, cols), s);
-  if (e != hipSuccess) return (int)e;
-  if (rows == 0 || cols == 0) return 0;
-  // about 512 blocks of at least 8 rows (each block sends its AM_CW column
-  // maxima out by atomics, so taller blocks for tall matrices)
-  const int cb = (cols + AM_CW - 1) / AM_CW;
-  const int rb = (int)std::max<int64_t>(8, ((int64_t)rows * cb + 511) / 512);
-  const dim3 grid(cb, (rows + rb - 1) / rb);
-  uint32_t *rm = want_rows ? st + 4 : nullptr;
-  uint32_t *cm = want_cols ? st + 4 + rows : nullptr;
+  const dim3 grid((rows + 3) / 4);
   if (ld % 4 == 0 && (uintptr_t)X % 16 == 0)
-    hipLaunchKernelGGL(absmax_kernel<true>, grid, dim3(256), 0, s, X, rows, cols, ld, rb, rm, cm,
-                       st);
+    hipLaunchKernelGGL(absmax_rows_kernel<true>, grid, dim3(256), 0, s, X, rows, cols, ld, rmax);
   else
-    hipLaunchKernelGGL(absmax_kernel<false>, grid, dim3(256), 0, s, X, rows, cols, ld, rb, rm,
-                       cm, st);
+    hipLaunchKernelGGL(absmax_rows_kernel<false>, grid, dim3(256), 0, s, X, rows, cols, ld,
+                       rmax);
+  return kcnn::launch_status();
+}
+
+extern "C" size_t kl_absmax_cols_words(int rows, int cols) {
+  if (rows <= 0 || cols <= 0) return 0;
+  return (size_t)cols_plan(rows, cols).rbk * cols;
+}
+extern "C" int kl_absmax_cols(const float *X, int rows, int cols, int ld, uint32_t *cmax,
+                              uint32_t *part, kcnn_stream_t stream) {
+  if (rows < 0 || cols < 0 || ld < cols || !cmax) return (int)hipErrorInvalidValue;
+  if (cols == 0) return 0;
+  hipStream_t s = kcnn::as_stream(stream);
+  if (rows == 0) return (int)hipMemsetAsync(cmax, 0, sizeof(uint32_t) * cols, s);
+  if (!part) return (int)hipErrorInvalidValue;
+  const ColsPlan p = cols_plan(rows, cols);
+  const dim3 grid(p.cb, p.rbk);
+  if (ld % 4 == 0 && (uintptr_t)X % 16 == 0)
+    hipLaunchKernelGGL(absmax_cols_kernel<true>, grid, dim3(256), 0, s, X, rows, cols, ld, p.rb,
+                       part);
+  else
+    hipLaunchKernelGGL(absmax_cols_kernel<false>, grid, dim3(256), 0, s, X, rows, cols, ld,
+                       p.rb, part);
+  int rc = kcnn::launch_status();
+  if (rc) return rc;
+  hipLaunchKernelGGL(absmax_cols_finalize_kernel, dim3((cols + 63) / 64), dim3(256), 0, s, part,
+                     p.rbk, cols, cmax);
   return kcnn::launch_status();
 }
 
 // C[M x N] = alpha * op(A) op(B) + beta * C with the operands' max |x| given:
-// amax[i] for row i of op(A), bmax[j] for column j of op(B) (kl_absmax bit
-// patterns), aflag / bflag their Inf / NaN flags.  Needs 16-B aligned
+// amax[i] for row i of op(A), bmax[j] for column j of op(B) (bit patterns of
+// max |x|, kl_absmax_rows / kl_absmax_cols).  Needs 16-B aligned
 // K-contiguous operands (A untransposed, B transposed) with pitches % 4 == 0
 // and every workgroup's buffer offsets below 2^31; returns
 // hipErrorNotSupported otherwise (the caller uses kl_gemm_x6).
@@ -562,9 +978,8 @@ extern "C" size_t kl_gemm_f16x3_workspace_bytes(int M, int N, int K) {
 }
 extern "C" int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alpha,
                                 const float *A, int lda, const float *B, int ldb, float beta,
-                                float *C, int ldc, const uint32_t *amax, const uint32_t *aflag,
-                                const uint32_t *bmax, const uint32_t *bflag, void *ws,
-                                size_t ws_bytes, kcnn_stream_t stream) {
+                                float *C, int ldc, const uint32_t *amax, const uint32_t *bmax,
+                                void *ws, size_t ws_bytes, kcnn_stream_t stream) {
   if (M < 0 || N < 0 || K < 0) return (int)hipErrorInvalidValue;
   if (M == 0 || N == 0 || K == 0) return (int)hipErrorNotSupported;
   const bool a_kc = !transA, b_kc = transB != 0;
@@ -593,10 +1008,14 @@ extern "C" int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, flo
   };
   if (!fits(a_kc, lda, BM) || !fits(b_kc, ldb, BN)) return (int)hipErrorNotSupported;
   hipStream_t st = kcnn::as_stream(stream);
-  if (a_kc && b_kc) launch<true, true>(a, (unsigned)nb, st);
-  else if (a_kc) launch<true, false>(a, (unsigned)nb, st);
-  else if (b_kc) launch<false, true>(a, (unsigned)nb, st);
-  else launch<false, false>(a, (unsigned)nb, st);
+  // a row-contiguous operand takes 16-B loads along its rows when they are
+  // aligned and its row count (M or N) is a multiple of 4
+  auto mode = [](bool kc, const float *ptr, int ld, int rows) {
+    if (kc) return (int)LK;
+    static const int tr = KCNN_KNOB("KCNN_F16X3_TR", 1);
+    return tr && ld % 4 == 0 && (uintptr_t)ptr % 16 == 0 && rows % 4 == 0 ? (int)LT : (int)LR;
+  };
+  launch(mode(a_kc, A, lda, M), mode(b_kc, B, ldb, N), a, (unsigned)nb, st);
   int rc = kcnn::launch_status();
   if (rc) return rc;
   if (s > 1) {
@@ -612,19 +1031,29 @@ extern "C" int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, flo
     if (rc) return rc;
   }
   FixupArgs f;
-  f.A = A; f.B = B; f.C = C; f.amax = amax; f.bmax = bmax; f.aflag = aflag; f.bflag = bflag;
+  f.A = A; f.B = B; f.C = C; f.amax = amax; f.bmax = bmax;
   f.M = M; f.N = N; f.K = K; f.lda = lda; f.ldb = ldb; f.ldc = ldc;
   f.transA = transA != 0; f.transB = transB != 0; f.alpha = alpha; f.beta = beta;
   hipLaunchKernelGGL(gemm_f16x3_fixup_kernel, dim3(64), dim3(256), 0, st, f);
   return kcnn::launch_status();
 }
 
-// The same with the operand statistics computed here (two kl_absmax passes
-// into the workspace after the partial slabs).
+// The same with the operand statistics computed here: A's rows (its columns
+// when transposed) and B's columns (rows when transposed), into the
+// workspace after the partial slabs.
+namespace {
+size_t stats_ws_words(int M, int N, int K, int transA, int transB) {
+  // maxima of op(A)'s rows and op(B)'s columns, then the column partials
+  const size_t pa = transA ? kl_absmax_cols_words(K, M) : 0;
+  const size_t pb = transB ? 0 : kl_absmax_cols_words(K, N);
+  return (size_t)M + N + 4 + (pa > pb ? pa : pb);
+}
+}  // namespace
 extern "C" size_t kl_gemm_f16x3_full_workspace_bytes(int M, int N, int K) {
-  // A's statistics cover its stored shape (M x K or K x M), B's (K x N or N x K)
-  return partial_bytes(M, N, K) + align16(sizeof(uint32_t) * stats_words(M, K)) +
-         align16(sizeof(uint32_t) * stats_words(K, N));
+  size_t w = 0;
+  for (int ta = 0; ta < 2; ++ta)
+    for (int tb = 0; tb < 2; ++tb) w = std::max(w, stats_ws_words(M, N, K, ta, tb));
+  return partial_bytes(M, N, K) + align16(sizeof(uint32_t) * w);
 }
 extern "C" int kl_gemm_f16x3(int transA, int transB, int M, int N, int K, float alpha,
                              const float *A, int lda, const float *B, int ldb, float beta,
@@ -633,20 +1062,19 @@ extern "C" int kl_gemm_f16x3(int transA, int transB, int M, int N, int K, float 
   if (M < 0 || N < 0 || K < 0) return (int)hipErrorInvalidValue;
   if (M == 0 || N == 0 || K == 0) return (int)hipErrorNotSupported;
   const size_t pb = partial_bytes(M, N, K);
-  const size_t sa = align16(sizeof(uint32_t) * stats_words(M, K));
   if (!ws || ws_bytes < kl_gemm_f16x3_full_workspace_bytes(M, N, K))
     return (int)hipErrorInvalidValue;
-  uint32_t *stA = reinterpret_cast<uint32_t *>(static_cast<char *>(ws) + pb);
-  uint32_t *stB = reinterpret_cast<uint32_t *>(static_cast<char *>(ws) + pb + sa);
-  // op(A) rows: rows of A (M x K), or its columns when A is stored K x M
-  const int ar = transA ? K : M, ac = transA ? M : K;
-  const int br = transB ? N : K, bc = transB ? K : N;
-  int rc = kl_absmax(A, ar, ac, lda, stA, !transA, transA, stream);
+  uint32_t *amax = reinterpret_cast<uint32_t *>(static_cast<char *>(ws) + pb);
+  uint32_t *bmax = amax + M;
+  uint32_t *part = bmax + N + 4;
+  // op(A)'s rows: A's rows (stored M x K), or its columns (stored K x M)
+  int rc = transA ? kl_absmax_cols(A, K, M, lda, amax, part, stream)
+                  : kl_absmax_rows(A, M, K, lda, amax, stream);
   if (rc) return rc;
-  rc = kl_absmax(B, br, bc, ldb, stB, transB, !transB, stream);
+  // op(B)'s columns: B's columns (stored K x N), or its rows (stored N x K)
+  rc = transB ? kl_absmax_rows(B, N, K, ldb, bmax, stream)
+              : kl_absmax_cols(B, K, N, ldb, bmax, part, stream);
   if (rc) return rc;
-  const uint32_t *amax = transA ? stA + 4 + ar : stA + 4;
-  const uint32_t *bmax = transB ? stB + 4 : stB + 4 + br;
   return kl_gemm_f16x3_st(transA, transB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, amax,
-                          stA, bmax, stB, pb ? ws : nullptr, pb, stream);
+                          bmax, pb ? ws : nullptr, pb, stream);
 }

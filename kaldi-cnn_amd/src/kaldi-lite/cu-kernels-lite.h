@@ -29,19 +29,22 @@ int kl_gemm_x6(int transA, int transB, int M, int N, int K, float alpha,
                const float *A, int lda, const float *B, int ldb, float beta,
                float *C, int ldc, void *ws, size_t ws_bytes, kcnn_stream_t st);
 /* fp32 GEMM on the f16 MFMAs: two-part f16 split under per-row / per-column
-   power-of-two scales (cu-gemm-f16x3.hip).  kl_absmax writes max |x| bit
-   patterns into st = [flag, 0, 0, 0, rows..., cols...] (zeroed first);
-   kl_gemm_f16x3_st takes them for op(A)'s rows and op(B)'s columns,
-   kl_gemm_f16x3 computes them in its workspace.  Both return
-   hipErrorNotSupported for shapes outside the kernel's addressing limits. */
-int kl_absmax(const float *X, int rows, int cols, int ld, uint32_t *st, int want_rows,
-              int want_cols, kcnn_stream_t st_);
+   power-of-two scales (cu-gemm-f16x3.hip).  kl_absmax_rows / kl_absmax_cols
+   write max |x| bit patterns per row / column (the column form needs
+   kl_absmax_cols_words of scratch); kl_gemm_f16x3_st takes them for op(A)'s
+   rows and op(B)'s columns, kl_gemm_f16x3 computes them in its workspace.
+   Both return hipErrorNotSupported for shapes outside the kernel's
+   addressing limits. */
+int kl_absmax_rows(const float *X, int rows, int cols, int ld, uint32_t *rmax,
+                   kcnn_stream_t st);
+size_t kl_absmax_cols_words(int rows, int cols);
+int kl_absmax_cols(const float *X, int rows, int cols, int ld, uint32_t *cmax, uint32_t *part,
+                   kcnn_stream_t st);
 size_t kl_gemm_f16x3_workspace_bytes(int M, int N, int K);
 int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alpha,
                      const float *A, int lda, const float *B, int ldb, float beta, float *C,
-                     int ldc, const uint32_t *amax, const uint32_t *aflag,
-                     const uint32_t *bmax, const uint32_t *bflag, void *ws, size_t ws_bytes,
-                     kcnn_stream_t st);
+                     int ldc, const uint32_t *amax, const uint32_t *bmax, void *ws,
+                     size_t ws_bytes, kcnn_stream_t st);
 size_t kl_gemm_f16x3_full_workspace_bytes(int M, int N, int K);
 int kl_gemm_f16x3(int transA, int transB, int M, int N, int K, float alpha,
                   const float *A, int lda, const float *B, int ldb, float beta, float *C,

@@ -193,23 +193,37 @@ int kn_relu_backprop(const float *out_value, MatrixDim ov_dim, const float *out_
   return kcnn::launch_status();
 }
 
-int kn_splice_prop(const float *in, MatrixDim in_dim, float *out, MatrixDim out_dim,
-                   kn_splice_geom g, kcnn_stream_t st) {
+}  // extern "C"
+
+namespace {
+// The geometry checks both splice directions share: shapes against the
+// chunk layout, and every input row a table (or a contiguous range) names
+// inside the input chunk, the table within its kernel-argument array.
+bool splice_geom_ok(MatrixDim in_dim, MatrixDim out_dim, const kn_splice_geom &g) {
   if (g.num_splice <= 0 || g.num_splice > KN_SPLICE_MAX_CONTEXT ||
       in_dim.rows != g.num_chunks * g.in_cs || out_dim.rows != g.num_chunks * g.out_cs ||
       in_dim.cols != g.dim + g.const_dim ||
       out_dim.cols != g.num_splice * g.dim + g.const_dim)
-    return (int)hipErrorInvalidValue;
+    return false;
   if (g.table) {
-    if ((int64_t)g.num_splice * g.out_cs > KN_SPLICE_MAX_TAB) return (int)hipErrorInvalidValue;
+    if ((int64_t)g.num_splice * g.out_cs > KN_SPLICE_MAX_TAB) return false;
     for (int e = 0; e < g.num_splice * g.out_cs; e++)
-      if (g.in_index[e] < 0 || g.in_index[e] >= g.in_cs) return (int)hipErrorInvalidValue;
+      if (g.in_index[e] < 0 || g.in_index[e] >= g.in_cs) return false;
   } else {
     for (int c = 0; c < g.num_splice; c++) {
       const int lo = g.out_first + g.context[c] - g.in_first;
-      if (lo < 0 || lo + g.out_cs > g.in_cs) return (int)hipErrorInvalidValue;
+      if (lo < 0 || lo + g.out_cs > g.in_cs) return false;
     }
   }
+  return true;
+}
+}  // namespace
+
+extern "C" {
+
+int kn_splice_prop(const float *in, MatrixDim in_dim, float *out, MatrixDim out_dim,
+                   kn_splice_geom g, kcnn_stream_t st) {
+  if (!splice_geom_ok(in_dim, out_dim, g)) return (int)hipErrorInvalidValue;
   const int64_t total = (int64_t)out_dim.rows * out_dim.cols;
   if (total == 0) return 0;
   if (total >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
@@ -221,11 +235,7 @@ int kn_splice_prop(const float *in, MatrixDim in_dim, float *out, MatrixDim out_
 
 int kn_splice_backprop(const float *out_deriv, MatrixDim od_dim, float *in_deriv,
                        MatrixDim id_dim, kn_splice_geom g, kcnn_stream_t st) {
-  if (g.num_splice <= 0 || g.num_splice > KN_SPLICE_MAX_CONTEXT ||
-      id_dim.rows != g.num_chunks * g.in_cs || od_dim.rows != g.num_chunks * g.out_cs ||
-      id_dim.cols != g.dim + g.const_dim ||
-      od_dim.cols != g.num_splice * g.dim + g.const_dim)
-    return (int)hipErrorInvalidValue;
+  if (!splice_geom_ok(id_dim, od_dim, g)) return (int)hipErrorInvalidValue;
   const int64_t total = (int64_t)id_dim.rows * id_dim.cols;
   if (total == 0) return 0;
   if (total >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;

@@ -1,7 +1,9 @@
-"""Bitwise comparison of the FC GEMM kernels: run the c2 FC products (and a
-ragged shape) once per kernel generation in the experiment build
-(KCNN_X6_DEEP=0: gemm_x6_kernel, 1: gemm_x6d_kernel), each in its own
-process, and compare the outputs bit for bit.
+"""Bitwise comparison of FC GEMM kernel generations: run the c2 FC products
+(and ragged shapes) once per value of an experiment switch in the
+experiment build (libkcnn_timing.so), each in its own process, and compare
+the outputs bit for bit.  Default: KCNN_X6_DEEP=0/1 on the bf16x6 engine
+(gemm_x6_kernel vs gemm_x6d_kernel); VAR=KCNN_F16X3_FAST GEMM=2 compares
+the f16x3 two-phase and fast kernels.
 
   python scripts/gemm_deep_bitwise.py            # driver: both runs + compare
   python scripts/gemm_deep_bitwise.py run OUT    # one run (env selects the kernel)
@@ -19,6 +21,8 @@ SHAPES = [  # (name, trans_a, trans_b, m, n, k): c2 FC forward, dgrad, wgrad; ra
     ("fc_dgrad", False, False, 4096, 11616, 1024),
     ("fc_wgrad", True, False, 1024, 11616, 4096),
     ("ragged", False, False, 1000, 1000, 512),
+    ("ragged_k", False, True, 1000, 520, 1003),
+    ("ragged_t", True, False, 520, 1000, 2021),
 ]
 
 
@@ -26,6 +30,7 @@ def run(out):
     sys.path.insert(0, os.path.join(ROOT, "kaldi-cnn_amd"))
     import torch
     import kcnn
+    kcnn.set_gemm_mode(int(os.environ.get("GEMM", "1")))
     g = torch.Generator(device="cuda")
     g.manual_seed(7)
     res = {}
@@ -44,7 +49,8 @@ def main():
     outs = []
     for v in (0, 1):
         out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"gemm_deep{v}.npz")
-        env = dict(os.environ, KCNN_LIB=lib, KCNN_X6_DEEP=str(v))
+        env = dict(os.environ, KCNN_LIB=lib)
+        env[os.environ.get("VAR", "KCNN_X6_DEEP")] = str(v)
         subprocess.run([sys.executable, __file__, "run", out], env=env, check=True, timeout=300)
         outs.append(np.load(out))
     bad = 0

@@ -18,6 +18,10 @@ import json
 import os
 import re
 import shutil
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402  (kernel_source_digest)
 
 # hot-path kernel (regex on the demangled name) -> bench.py kernel-table key;
 # first match wins
@@ -118,6 +122,9 @@ def main():
             v["hbm_bytes_per_launch"] = round(v["hbm_bytes_per_launch"])
             v["run"] = a.tag
             v["frames"] = a.frames
+            # the digest of the kernel's source: bench.py uses these bytes only
+            # while the source is unchanged
+            v["source_sha1"] = bench.kernel_source_digest(v["kernel"])
         path = os.path.join(a.out, "pmc_traffic.json")
         merged = json.load(open(path)) if os.path.exists(path) else {}
         merged.update(traffic)  # kernels of several runs (fused / unfused)

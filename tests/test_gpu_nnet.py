@@ -296,3 +296,33 @@ def test_conv_relu_fusion_is_exact(kc, name):
     assert np.array_equal(a[3][0], b[3][0]) and np.array_equal(a[3][1], b[3][1])
     assert a[3][2] == b[3][2]
     assert (a[0][1] >= 0).all()
+
+
+# The pooled backward (conv_bwd_x6q_kernel) carries state from one frame to
+# the next inside a workgroup (the next frame's im2col gather in the last
+# slab's P_A, the previous frame's col2im spread over P_A, n1/n2 wrap-around);
+# that loop runs only when the frames outnumber the grid (256 workgroups).
+# 601 frames (not a multiple of 256, more than 2 frames per workgroup) run
+# every variant through it: fusion on/off bitwise (the unfused backward is a
+# different kernel, conv_bwd_x6_kernel, also grid-striding) and the whole step
+# (outputs, input derivatives, the update) against the oracle.
+CROSS_FRAME = ["halfB_G64_pc8", "halfB_G96_2x1x4", "win_2x1x4_G96", "c5_P1_3x1x4", "pc8_G64"]
+
+
+@pytest.mark.parametrize("name", CROSS_FRAME)
+def test_pooled_backward_across_frames(kc, name):
+    from _stack import check_step
+    cfg = STACKS[name]
+    N = 601
+    a = run(kc, cfg, fused=True, N=N)
+    b = run(kc, cfg, fused=False, N=N)
+    for k, (u, v) in enumerate(zip(a[1], b[1])):
+        assert_same(u, v, f"{name} input deriv {k} at {N} frames")
+    for k, (u, v) in enumerate(zip(a[2], b[2])):
+        assert_same(u, v, f"{name} param {k} at {N} frames")
+    kc.set_fusion(1)
+    net = build(kc, cfg, seed=11)
+    r = rng(3)
+    x = dev(randn(r, (N, net.components[0].InputDim())))
+    dy = dev(randn(r, (N, net.components[2].OutputDim()), 0.1))
+    check_step(kc, stack(*cfg)[0], net, x, dy, what=f"{name} N={N}")

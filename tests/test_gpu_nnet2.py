@@ -191,6 +191,16 @@ def test_gapped_splice_stack(kc):
     assert_same(outs[0], a0, "Splice 1 (gapped chunk offsets)")
     assert_same(outs[1], a1, "ReLU")
     assert_same(outs[2], a2, "Splice 2")
+    # known answer, derived by hand (independent of oracle.chunk_offsets):
+    # 11 input frames 0..10 per chunk; the first splice (-2..2) produces the
+    # frames at offsets 2, 5, 8, i.e. output row 3n + j is input rows
+    # 11n + 3j + 0..4 side by side; the second (-3, 0, 3) reads those three
+    # rows of its chunk for its one output frame (offset 5)
+    kat1 = np.stack([np.concatenate([x[11 * n + 3 * j + c] for c in range(5)])
+                     for n in range(N) for j in range(3)])
+    assert_same(outs[0], kat1, "Splice 1 known answer")
+    kat2 = np.stack([np.concatenate([outs[1][3 * n + j] for j in range(3)]) for n in range(N)])
+    assert_same(outs[2], kat2, "Splice 2 known answer")
     with O.accum(1):
         y_t = of.propagate(a2)
     np.testing.assert_allclose(outs[3], y_t, rtol=1e-5, atol=1e-6)

@@ -32,17 +32,18 @@
 // kl_absmax_cols: the bit patterns of |x|, whose unsigned order is the
 // magnitude order).  A row of
 // op(A) or a column of op(B) holding Inf or NaN has no scale; every C
-// element in it is Inf or NaN in IEEE arithmetic.  The kernels leave those
-// elements alone and gemm_f16x3_fixup_kernel computes them as plain fp32 dot
-// products, which gives sgemm's IEEE pattern (+Inf, -Inf or NaN); with no
-// Inf / NaN among the operands it returns at once.
+// element in it is Inf or NaN in IEEE arithmetic.  The main loop leaves
+// those elements alone and the tile's split-0 workgroup computes them as
+// plain fp32 dot products (tile_epilogue), which gives sgemm's IEEE pattern
+// (+Inf, -Inf or NaN).
 //
 // Structure: gemm_x6d_kernel's (cu-gemm-x6.hip): 512 threads, a 256 x 128
 // tile of C per workgroup (8 waves of 2 x 2 accumulators of 32 x 32), K steps
 // of 32, operands loaded as fp32 by branch-free buffer loads two steps ahead,
 // split in registers into two f16 planes of swizzled [row][k] LDS images
 // (double-buffered, 2 x 48 KB), one barrier per step.  Thin outputs split K
-// over workgroups; the partial tiles are summed in a fixed order.
+// over workgroups; the last workgroup of a tile sums the partial tiles in a
+// fixed order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -72,12 +73,12 @@ constexpr int SKIP = 0x40000000;              // scale of an Inf / NaN row or co
 
 struct GemmF16Args {
   const float *A, *B;
-  float *C;                      // direct output, or the partial slabs [ksplit][M][N]
+  float *C;                      // the output
+  float *part;                   // ksplit > 1: the partial slabs [ksplit][M][N]
   const uint32_t *amax, *bmax;   // max |x| bits per row of op(A), per column of op(B)
   int M, N, K, lda, ldb, ldc;
   int kps, ksplit, tiles_m, tiles_n;
   float alpha, beta;
-  int partial;
 };
 
 __device__ __forceinline__ int swz(int r, int c) {
@@ -334,6 +335,84 @@ __device__ __forceinline__ f32x16 mfma(const f16x8 &a, const f16x8 &b, const f32
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
+// The scale exponents of the tile's rows and columns into sexp; true (for
+// the whole block) when one of them is an Inf / NaN row or column
+__device__ __forceinline__ bool tile_scales(const GemmF16Args &p, int *sexp, int row0, int col0,
+                                            int tid) {
+  int skip = 0;
+  for (int i = tid; i < BM + BN; i += NT) {
+    int s = 0;
+    if (i < BM) {
+      if (row0 + i < p.M) s = scale_exp(p.amax[row0 + i]);
+    } else if (col0 + i - BM < p.N) {
+      s = scale_exp(p.bmax[col0 + i - BM]);
+    }
+    sexp[i] = s;
+    skip |= s == SKIP;
+  }
+  return __syncthreads_or(skip) != 0;
+}
+
+// The tile's results.  C/D map of 32x32x16: register g of lane l holds row
+// (g & 3) + 8 (g >> 2) + 4 (l >> 5), column l & 31.  Each value is unscaled
+// by 2^-(s_row + s_col) (exact).
+//  - One split: C = alpha * v + beta * C.
+//  - ksplit > 1: the split's values go to its partial slab, which
+//    gemm_f16x3_reduce_kernel adds in increasing split order.  (Adding them
+//    in the tile's last-arriving workgroup instead needs a device-scope
+//    release fence per workgroup, which on gfx950 writes back the XCD's L2:
+//    the c2 FC forward went 330 -> 436 us and the weight gradient 368 ->
+//    654 us with it.)
+//  - Elements of an Inf / NaN row or column are skipped above; split 0's
+//    workgroup computes them here as fp32 dot products in increasing k
+//    (IEEE Inf / NaN, the reference sgemm's pattern).
+template <bool A_KC, bool B_KC>
+__device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *sexp,
+                                              const f32x16 (&acc)[2][2], int split, int row0,
+                                              int col0, bool skip, int tid) {
+  const int lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int half2 = lane >> 5;
+  const bool partial = p.ksplit > 1;
+  float *slab = partial ? p.part + (int64_t)split * p.M * p.N : p.C;
+  const int ldo = partial ? p.N : p.ldc;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int cl = wn * 64 + j * 32 + (lane & 31);
+      const int col = col0 + cl;
+      const int ec = sexp[BM + cl];
+      if (col >= p.N || ec == SKIP) continue;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int rl = wm * 64 + i * 32 + (g & 3) + 8 * (g >> 2) + 4 * half2;
+        const int row = row0 + rl;
+        const int er = sexp[rl];
+        if (row >= p.M || er == SKIP) continue;
+        const float v = __builtin_amdgcn_ldexpf(acc[i][j][g], -(er + ec));
+        float *o = slab + (int64_t)row * ldo + col;
+        if (partial) *o = v;
+        else *o = p.beta == 0.0f ? p.alpha * v : p.alpha * v + p.beta * *o;
+      }
+    }
+  if (skip && split == 0) {
+    for (int e = tid; e < BM * BN; e += NT) {
+      const int rl = e / BN, cl = e - rl * BN;
+      const int row = row0 + rl, col = col0 + cl;
+      if (row >= p.M || col >= p.N) continue;
+      if (sexp[rl] != SKIP && sexp[BM + cl] != SKIP) continue;
+      float sum = 0.0f;
+      for (int k = 0; k < p.K; ++k) {
+        const float a = A_KC ? p.A[(int64_t)row * p.lda + k] : p.A[(int64_t)k * p.lda + row];
+        const float b = B_KC ? p.B[(int64_t)col * p.ldb + k] : p.B[(int64_t)k * p.ldb + col];
+        sum = fmaf(a, b, sum);
+      }
+      float *o = p.C + (int64_t)row * p.ldc + col;
+      *o = p.beta == 0.0f ? p.alpha * sum : p.alpha * sum + p.beta * *o;
+    }
+  }
+}
+
 template <int AM, int BMODE>
 __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
   constexpr bool A_KC = AM == LK, B_KC = BMODE == LK;
@@ -355,15 +434,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
   const int T = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   const int klast = kend - kbeg - (T - 1) * BK;  // valid k of the last tile
 
-  for (int i = tid; i < BM + BN; i += NT) {
-    int s = 0;
-    if (i < BM) {
-      if (row0 + i < p.M) s = scale_exp(p.amax[row0 + i]);
-    } else if (col0 + i - BM < p.N) {
-      s = scale_exp(p.bmax[col0 + i - BM]);
-    }
-    sexp[i] = s;
-  }
+  const bool skip = tile_scales(p, sexp, row0, col0, tid);
 
   // descriptors whose range ends at the operand's last element: a partial
   // last tile reads 0 past it (and the split zeroes the pitch's padding)
@@ -392,7 +463,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int g = 0; g < 16; ++g) acc[i][j][g] = 0.0f;
-  __syncthreads();  // sexp
   la[0].init_exp(sexp, tid);
   la[1].init_exp(sexp, tid);
   lb[0].init_exp(sexp + BM, tid);
@@ -467,31 +537,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
     }
   }
 
-  // C/D map of 32x32x16: register g of lane l holds
-  // row (g & 3) + 8 (g >> 2) + 4 (l >> 5), column l & 31.
-  float *out = p.partial ? p.C + (int64_t)split * p.M * p.N : p.C;
-  const int ldo = p.partial ? p.N : p.ldc;
-  const int half2 = lane >> 5;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int cl = wn * 64 + j * 32 + (lane & 31);
-      const int col = col0 + cl;
-      const int ec = sexp[BM + cl];
-      if (col >= p.N || ec == SKIP) continue;
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const int rl = wm * 64 + i * 32 + (g & 3) + 8 * (g >> 2) + 4 * half2;
-        const int row = row0 + rl;
-        const int er = sexp[rl];
-        if (row >= p.M || er == SKIP) continue;
-        const float v = __builtin_amdgcn_ldexpf(acc[i][j][g], -(er + ec));
-        float *o = out + (int64_t)row * ldo + col;
-        if (p.partial) *o = v;
-        else *o = p.beta == 0.0f ? p.alpha * v : p.alpha * v + p.beta * *o;
-      }
-    }
+  tile_epilogue<A_KC, B_KC>(p, sexp, acc, split, row0, col0, skip, tid);
 }
 
 // ---------------------------------------------------------------------------
@@ -532,15 +578,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
   const int T = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   const int klast = kend - kbeg - (T - 1) * BK;
 
-  for (int i = tid; i < BM + BN; i += NT) {
-    int s = 0;
-    if (i < BM) {
-      if (row0 + i < p.M) s = scale_exp(p.amax[row0 + i]);
-    } else if (col0 + i - BM < p.N) {
-      s = scale_exp(p.bmax[col0 + i - BM]);
-    }
-    sexp[i] = s;
-  }
+  const bool skip = tile_scales(p, sexp, row0, col0, tid);
   const float *baseA = A_KC ? p.A + (int64_t)row0 * p.lda : p.A + (int64_t)kbeg * p.lda + row0;
   const float *baseB = B_KC ? p.B + (int64_t)col0 * p.ldb : p.B + (int64_t)kbeg * p.ldb + col0;
   const int vra = p.M - row0, vrb = p.N - col0;
@@ -565,7 +603,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int g = 0; g < 16; ++g) acc[i][j][g] = 0.0f;
-  __syncthreads();  // sexp
   la[0].init_exp(sexp, tid);
   la[1].init_exp(sexp, tid);
   lb[0].init_exp(sexp + BM, tid);
@@ -645,33 +682,197 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
     if (t < T) step(t, la[1], lb[1]);
   }
 
-  float *out = p.partial ? p.C + (int64_t)split * p.M * p.N : p.C;
-  const int ldo = p.partial ? p.N : p.ldc;
-  const int half2 = lane >> 5;
+  tile_epilogue<A_KC, B_KC>(p, sexp, acc, split, row0, col0, skip, tid);
+}
+
+// Max |x| per row or per column of a pitched fp32 matrix, as the bit
+// patterns of |x| (unsigned order = magnitude order, Inf / NaN above every
+// finite value; max is order-independent, so the results are deterministic).
+// A GEMM needs op(A)'s rows and op(B)'s columns; both operands' statistics
+// go in one launch (stats_kernel: blocks [0, a.blocks) for A, then B's) and
+// one more (stats_finalize_kernel) when either is per column:
+//  rows, cols >= 2048: a block per row (thread t reads float4 t + 256 i,
+//    four in flight), a wave reduction and an LDS step;
+//  rows, shorter rows: a wave per row;
+//  columns: block (cb, rc) covers 1024 columns (4 per thread) of a chunk of
+//    rows (8 in flight) and stores its column maxima as partial rc; the
+//    finalize takes the maxima over the chunks (64 columns x 4 chunk groups
+//    per block, combined through LDS).
+struct StatOp {
+  const float *X;
+  uint32_t *out;   // maxima per row (mode 0) or per column (mode 1)
+  uint32_t *part;  // mode 1: [rbk][cols] partials
+  int rows, cols, ld, mode, vec;
+  int blocks;      // of stats_kernel
+  int rpb;         // mode 0: rows per block (4: a wave each; 1: a block)
+  int cb, rbk, rb; // mode 1: column blocks, row chunks, rows per chunk
+  int fblocks;     // mode 1: blocks of stats_finalize_kernel
+};
+__device__ __forceinline__ const float *X_row(const StatOp &o, int r) {
+  return o.X + (int64_t)r * o.ld;
+}
+
+__device__ __forceinline__ uint32_t amax4(uint32_t m, float4 q) {
+  return max(max(m, __float_as_uint(q.x) & 0x7fffffffu),
+             max(max(__float_as_uint(q.y) & 0x7fffffffu, __float_as_uint(q.z) & 0x7fffffffu),
+                 __float_as_uint(q.w) & 0x7fffffffu));
+}
+
+__device__ __forceinline__ void stats_rows(const StatOp &o, int blk, uint32_t *red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool wide = o.rpb == 1;
+  const int r = wide ? blk : blk * 4 + wave;
+  if (r >= o.rows) return;  // (wide: uniform over the block)
+  const float *x = X_row(o, r);
+  const int step = wide ? 1024 : 256;  // floats per sweep of the row
+  int c = (wide ? threadIdx.x : lane) * 4;
+  uint32_t m = 0;
+  if (o.vec) {
+    for (; c + 3 * step + 4 <= o.cols; c += 4 * step) {
+      float4 q[4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < 4; ++j) q[j] = *reinterpret_cast<const float4 *>(x + c + j * step);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int cl = wn * 64 + j * 32 + (lane & 31);
-      const int col = col0 + cl;
-      const int ec = sexp[BM + cl];
-      if (col >= p.N || ec == SKIP) continue;
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const int rl = wm * 64 + i * 32 + (g & 3) + 8 * (g >> 2) + 4 * half2;
-        const int row = row0 + rl;
-        const int er = sexp[rl];
-        if (row >= p.M || er == SKIP) continue;
-        const float v = __builtin_amdgcn_ldexpf(acc[i][j][g], -(er + ec));
-        float *o = out + (int64_t)row * ldo + col;
-        if (p.partial) *o = v;
-        else *o = p.beta == 0.0f ? p.alpha * v : p.alpha * v + p.beta * *o;
-      }
+      for (int j = 0; j < 4; ++j) m = amax4(m, q[j]);
     }
+    for (; c + 4 <= o.cols; c += step) m = amax4(m, *reinterpret_cast<const float4 *>(x + c));
+  }
+  for (; c < o.cols; c += step)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (c + i < o.cols) m = max(m, __float_as_uint(x[c + i]) & 0x7fffffffu);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
+  if (!wide) {
+    if (lane == 0) o.out[r] = m;
+    return;
+  }
+  if (lane == 0) red[wave] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) o.out[r] = max(max(red[0], red[1]), max(red[2], red[3]));
+}
+
+__device__ __forceinline__ void stats_cols(const StatOp &o, int blk) {
+  const int cbi = blk % o.cb, rci = blk / o.cb;
+  const int c0 = cbi * 1024 + threadIdx.x * 4;
+  const int r0 = rci * o.rb, rend = min(o.rows, r0 + o.rb);
+  if (c0 >= o.cols) return;
+  const bool v4 = o.vec && c0 + 4 <= o.cols;
+  uint32_t cm[4] = {0u, 0u, 0u, 0u};
+  auto load = [&](int r) {
+    const float *x = X_row(o, r) + c0;
+    if (v4) return *reinterpret_cast<const float4 *>(x);
+    float4 q;
+    q.x = x[0];
+    q.y = c0 + 1 < o.cols ? x[1] : 0.0f;
+    q.z = c0 + 2 < o.cols ? x[2] : 0.0f;
+    q.w = c0 + 3 < o.cols ? x[3] : 0.0f;
+    return q;
+  };
+  auto take = [&](float4 q) {
+    cm[0] = max(cm[0], __float_as_uint(q.x) & 0x7fffffffu);
+    cm[1] = max(cm[1], __float_as_uint(q.y) & 0x7fffffffu);
+    cm[2] = max(cm[2], __float_as_uint(q.z) & 0x7fffffffu);
+    cm[3] = max(cm[3], __float_as_uint(q.w) & 0x7fffffffu);
+  };
+  int r = r0;
+  for (; r + 8 <= rend; r += 8) {
+    float4 q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q[j] = load(r + j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) take(q[j]);
+  }
+  for (; r < rend; ++r) take(load(r));
+  uint32_t *dst = o.part + (size_t)rci * o.cols + c0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (c0 + i < o.cols) dst[i] = cm[i];
+}
+
+__global__ __launch_bounds__(256) void stats_kernel(StatOp a, StatOp b) {
+  __shared__ uint32_t red[4];
+  const bool isa = (int)blockIdx.x < a.blocks;  // uniform
+  const StatOp &o = isa ? a : b;
+  const int blk = isa ? blockIdx.x : blockIdx.x - a.blocks;
+  if (o.mode == 0) stats_rows(o, blk, red);
+  else stats_cols(o, blk);
+}
+
+__global__ __launch_bounds__(256) void stats_finalize_kernel(StatOp a, StatOp b) {
+  __shared__ uint32_t red[4][64];
+  const int fa = a.mode == 1 ? a.fblocks : 0;
+  const bool isa = (int)blockIdx.x < fa;
+  const StatOp &o = isa ? a : b;
+  const int blk = isa ? blockIdx.x : blockIdx.x - fa;
+  const int c = blk * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
+  uint32_t m = 0;
+  if (c < o.cols) {
+    int q = grp;
+    for (; q + 12 < o.rbk; q += 16)
+      m = max(max(m, o.part[(size_t)q * o.cols + c]),
+              max(max(o.part[(size_t)(q + 4) * o.cols + c], o.part[(size_t)(q + 8) * o.cols + c]),
+                  o.part[(size_t)(q + 12) * o.cols + c]));
+    for (; q < o.rbk; q += 4) m = max(m, o.part[(size_t)q * o.cols + c]);
+  }
+  red[grp][threadIdx.x & 63] = m;
+  __syncthreads();
+  if (grp == 0 && c < o.cols)
+    o.out[c] = max(max(red[0][threadIdx.x], red[1][threadIdx.x]),
+                   max(red[2][threadIdx.x], red[3][threadIdx.x]));
+}
+
+// a statistics pass over X (rows x cols, pitch ld): mode 0 per row, 1 per
+// column (partials at part, stat_part_words of them)
+StatOp stat_op(const float *X, int rows, int cols, int ld, int mode, uint32_t *out,
+               uint32_t *part) {
+  StatOp o{};
+  o.X = X; o.out = out; o.part = part;
+  o.rows = rows; o.cols = cols; o.ld = ld; o.mode = mode;
+  o.vec = ld % 4 == 0 && (uintptr_t)X % 16 == 0;
+  if (rows <= 0 || cols <= 0) return o;  // blocks 0
+  if (mode == 0) {
+    o.rpb = cols >= 2048 ? 1 : 4;
+    o.blocks = (rows + o.rpb - 1) / o.rpb;
+  } else {
+    o.cb = (cols + 1023) / 1024;
+    // about 1024 blocks of at least 16 rows, at most 256 row chunks
+    o.rbk = std::max(1, std::min(256, std::min((rows + 15) / 16, (1024 + o.cb - 1) / o.cb)));
+    o.rb = (rows + o.rbk - 1) / o.rbk;
+    o.rbk = (rows + o.rb - 1) / o.rb;
+    o.blocks = o.cb * o.rbk;
+    o.fblocks = (cols + 63) / 64;
+  }
+  return o;
+}
+size_t stat_part_words(int rows, int cols, int mode) {
+  if (mode == 0) return 0;
+  const StatOp o = stat_op(nullptr, rows, cols, cols, 1, nullptr, nullptr);
+  return (size_t)o.rbk * cols;
+}
+int stats_launch(const StatOp &a, const StatOp &b, hipStream_t st) {
+  // empty operands: maxima 0 (no scale)
+  for (const StatOp *o : {&a, &b})
+    if (o->blocks == 0 && o->out) {
+      const size_t n = o->mode == 0 ? (size_t)std::max(o->rows, 0) : (size_t)std::max(o->cols, 0);
+      if (n && hipMemsetAsync(o->out, 0, n * 4, st) != hipSuccess) return (int)hipGetLastError();
+    }
+  const int nb = a.blocks + b.blocks;
+  if (nb == 0) return 0;
+  hipLaunchKernelGGL(stats_kernel, dim3(nb), dim3(256), 0, st, a, b);
+  int rc = kcnn::launch_status();
+  if (rc) return rc;
+  const int nf = (a.mode == 1 && a.blocks ? a.fblocks : 0) + (b.mode == 1 && b.blocks ? b.fblocks : 0);
+  if (nf == 0) return 0;
+  StatOp a2 = a, b2 = b;
+  if (a2.blocks == 0) a2.mode = 0;  // nothing to finalize
+  if (b2.blocks == 0) b2.mode = 0;
+  hipLaunchKernelGGL(stats_finalize_kernel, dim3(nf), dim3(256), 0, st, a2, b2);
+  return kcnn::launch_status();
 }
 
 // C = alpha * sum_s part[s] + beta * C, the splits added in increasing s;
-// elements of an Inf / NaN row or column are the fixup kernel's
+// elements of an Inf / NaN row or column are the epilogue's (split 0)
 template <bool VEC>
 __global__ void gemm_f16x3_reduce_kernel(const float *__restrict__ part, int S, int M, int N,
                                          float alpha, float beta, float *C, int ldc,
@@ -707,163 +908,6 @@ __global__ void gemm_f16x3_reduce_kernel(const float *__restrict__ part, int S, 
       o[i] = beta == 0.0f ? alpha * s[i] : alpha * s[i] + beta * o[i];
     }
   }
-}
-
-struct FixupArgs {
-  const float *A, *B;
-  float *C;
-  const uint32_t *amax, *bmax;
-  int M, N, K, lda, ldb, ldc, transA, transB;
-  float alpha, beta;
-};
-
-// The C elements of every row of op(A) / column of op(B) holding Inf or
-// NaN, as fp32 dot products in increasing k (IEEE: the reference sgemm's
-// Inf / NaN pattern).  Each block first scans the M + N maxima (from L2) and
-// returns at once when none is Inf / NaN.
-__global__ __launch_bounds__(256) void gemm_f16x3_fixup_kernel(FixupArgs f) {
-  __shared__ int any;
-  if (threadIdx.x == 0) any = 0;
-  __syncthreads();
-  bool bad = false;
-  for (int e = threadIdx.x; e < f.M + f.N; e += blockDim.x)
-    bad |= (e < f.M ? f.amax[e] : f.bmax[e - f.M]) >= NONFINITE;
-  if (bad) any = 1;
-  __syncthreads();
-  if (!any) return;
-  const int64_t total = (int64_t)f.M * f.N;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = e / f.N, c = e - r * f.N;
-    if (f.amax[r] < NONFINITE && f.bmax[c] < NONFINITE) continue;
-    float s = 0.0f;
-    for (int k = 0; k < f.K; ++k) {
-      const float a = f.transA ? f.A[(int64_t)k * f.lda + r] : f.A[r * f.lda + k];
-      const float b = f.transB ? f.B[c * f.ldb + k] : f.B[(int64_t)k * f.ldb + c];
-      s = fmaf(a, b, s);
-    }
-    float *o = f.C + r * f.ldc + c;
-    *o = f.beta == 0.0f ? f.alpha * s : f.alpha * s + f.beta * *o;
-  }
-}
-
-// Max |x| per row or per column of a pitched fp32 matrix, as the bit
-// patterns of |x| (unsigned order = magnitude order, Inf / NaN above every
-// finite value; max is order-independent, so the results are deterministic).
-//  absmax_rows_kernel: one wave per row, 16-B loads four at a time, one wave
-//    reduction per row, a plain store (no atomics, no initialisation);
-//  absmax_cols_kernel: block (cb, rc) covers 1024 columns (4 per thread) of
-//    a chunk of rows and stores its column maxima as partial rc;
-//    absmax_cols_finalize_kernel takes the maxima over the chunks (64
-//    columns x 4 chunk groups per block, combined through LDS).
-template <bool VEC>
-__global__ __launch_bounds__(256) void absmax_rows_kernel(const float *__restrict__ X, int rows,
-                                                         int cols, int ld, uint32_t *rmax) {
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (r >= rows) return;
-  const float *x = X + (int64_t)r * ld;
-  uint32_t m = 0;
-  int c = lane * 4;
-  if (VEC) {
-    for (; c + 3 * 256 + 4 <= cols; c += 4 * 256) {
-      float4 q[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) q[j] = *reinterpret_cast<const float4 *>(x + c + j * 256);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        m = max(max(max(m, __float_as_uint(q[j].x) & 0x7fffffffu),
-                    max(__float_as_uint(q[j].y) & 0x7fffffffu,
-                        __float_as_uint(q[j].z) & 0x7fffffffu)),
-                __float_as_uint(q[j].w) & 0x7fffffffu);
-    }
-    for (; c + 4 <= cols; c += 256) {
-      const float4 q = *reinterpret_cast<const float4 *>(x + c);
-      m = max(max(max(m, __float_as_uint(q.x) & 0x7fffffffu),
-                  max(__float_as_uint(q.y) & 0x7fffffffu, __float_as_uint(q.z) & 0x7fffffffu)),
-              __float_as_uint(q.w) & 0x7fffffffu);
-    }
-  }
-  for (; c < cols; c += 256)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (c + i < cols) m = max(m, __float_as_uint(x[c + i]) & 0x7fffffffu);
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
-  if (lane == 0) rmax[r] = m;
-}
-
-template <bool VEC>
-__global__ __launch_bounds__(256) void absmax_cols_kernel(const float *__restrict__ X, int rows,
-                                                         int cols, int ld, int rb,
-                                                         uint32_t *part) {
-  const int c0 = blockIdx.x * 1024 + threadIdx.x * 4;
-  const int r0 = blockIdx.y * rb, rend = min(rows, r0 + rb);
-  if (c0 >= cols) return;
-  uint32_t cm[4] = {0u, 0u, 0u, 0u};
-  auto take = [&](const uint32_t (&v)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) cm[i] = max(cm[i], v[i] & 0x7fffffffu);
-  };
-  auto load = [&](int r, uint32_t (&v)[4]) {
-    const float *x = X + (int64_t)r * ld + c0;
-    if (VEC && c0 + 4 <= cols) {
-      const float4 q = *reinterpret_cast<const float4 *>(x);
-      v[0] = __float_as_uint(q.x); v[1] = __float_as_uint(q.y);
-      v[2] = __float_as_uint(q.z); v[3] = __float_as_uint(q.w);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = c0 + i < cols ? __float_as_uint(x[i]) : 0u;
-    }
-  };
-  int r = r0;
-  for (; r + 4 <= rend; r += 4) {
-    uint32_t v0[4], v1[4], v2[4], v3[4];
-    load(r, v0); load(r + 1, v1); load(r + 2, v2); load(r + 3, v3);
-    take(v0); take(v1); take(v2); take(v3);
-  }
-  for (; r < rend; ++r) {
-    uint32_t v[4];
-    load(r, v);
-    take(v);
-  }
-  uint32_t *dst = part + (size_t)blockIdx.y * cols + c0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (c0 + i < cols) dst[i] = cm[i];
-}
-
-__global__ __launch_bounds__(256) void absmax_cols_finalize_kernel(const uint32_t *part,
-                                                                  int nchunk, int cols,
-                                                                  uint32_t *cmax) {
-  __shared__ uint32_t red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
-  uint32_t m = 0;
-  if (c < cols) {
-    int p = grp;
-    for (; p + 12 < nchunk; p += 16)
-      m = max(max(m, part[(size_t)p * cols + c]),
-              max(max(part[(size_t)(p + 4) * cols + c], part[(size_t)(p + 8) * cols + c]),
-                  part[(size_t)(p + 12) * cols + c]));
-    for (; p < nchunk; p += 4) m = max(m, part[(size_t)p * cols + c]);
-  }
-  red[grp][threadIdx.x & 63] = m;
-  __syncthreads();
-  if (grp == 0 && c < cols)
-    cmax[c] = max(max(red[0][threadIdx.x], red[1][threadIdx.x]),
-                  max(red[2][threadIdx.x], red[3][threadIdx.x]));
-}
-
-struct ColsPlan {
-  int cb, rbk, rb;
-};
-// about 1024 blocks of at least 16 rows, at most 256 row chunks
-ColsPlan cols_plan(int rows, int cols) {
-  ColsPlan p;
-  p.cb = (cols + 1023) / 1024;
-  p.rbk = std::max(1, std::min(256, std::min((rows + 15) / 16, (1024 + p.cb - 1) / p.cb)));
-  p.rb = (rows + p.rbk - 1) / p.rbk;
-  p.rbk = (rows + p.rb - 1) / p.rb;
-  return p;
 }
 
 int choose_ksplit(int64_t tiles, int K) {
@@ -925,46 +969,25 @@ size_t partial_bytes(int M, int N, int K) {
   const int s = choose_ksplit(tiles, K);
   return s > 1 ? align16(sizeof(float) * (size_t)s * M * N) : 0;
 }
+
 }  // namespace
 
 extern "C" int kl_absmax_rows(const float *X, int rows, int cols, int ld, uint32_t *rmax,
                               kcnn_stream_t stream) {
   if (rows < 0 || cols < 0 || ld < cols || !rmax) return (int)hipErrorInvalidValue;
-  if (rows == 0) return 0;
-  hipStream_t s = kcnn::as_stream(stream);
-  const dim3 grid((rows + 3) / 4);
-  if (ld % 4 == 0 && (uintptr_t)X % 16 == 0)
-    hipLaunchKernelGGL(absmax_rows_kernel<true>, grid, dim3(256), 0, s, X, rows, cols, ld, rmax);
-  else
-    hipLaunchKernelGGL(absmax_rows_kernel<false>, grid, dim3(256), 0, s, X, rows, cols, ld,
-                       rmax);
-  return kcnn::launch_status();
+  return stats_launch(stat_op(X, rows, cols, ld, 0, rmax, nullptr), StatOp{},
+                      kcnn::as_stream(stream));
 }
-
 extern "C" size_t kl_absmax_cols_words(int rows, int cols) {
   if (rows <= 0 || cols <= 0) return 0;
-  return (size_t)cols_plan(rows, cols).rbk * cols;
+  return stat_part_words(rows, cols, 1);
 }
 extern "C" int kl_absmax_cols(const float *X, int rows, int cols, int ld, uint32_t *cmax,
                               uint32_t *part, kcnn_stream_t stream) {
   if (rows < 0 || cols < 0 || ld < cols || !cmax) return (int)hipErrorInvalidValue;
-  if (cols == 0) return 0;
-  hipStream_t s = kcnn::as_stream(stream);
-  if (rows == 0) return (int)hipMemsetAsync(cmax, 0, sizeof(uint32_t) * cols, s);
-  if (!part) return (int)hipErrorInvalidValue;
-  const ColsPlan p = cols_plan(rows, cols);
-  const dim3 grid(p.cb, p.rbk);
-  if (ld % 4 == 0 && (uintptr_t)X % 16 == 0)
-    hipLaunchKernelGGL(absmax_cols_kernel<true>, grid, dim3(256), 0, s, X, rows, cols, ld, p.rb,
-                       part);
-  else
-    hipLaunchKernelGGL(absmax_cols_kernel<false>, grid, dim3(256), 0, s, X, rows, cols, ld,
-                       p.rb, part);
-  int rc = kcnn::launch_status();
-  if (rc) return rc;
-  hipLaunchKernelGGL(absmax_cols_finalize_kernel, dim3((cols + 63) / 64), dim3(256), 0, s, part,
-                     p.rbk, cols, cmax);
-  return kcnn::launch_status();
+  if (rows > 0 && cols > 0 && !part) return (int)hipErrorInvalidValue;
+  return stats_launch(stat_op(X, rows, cols, ld, 1, cmax, part), StatOp{},
+                      kcnn::as_stream(stream));
 }
 
 // C[M x N] = alpha * op(A) op(B) + beta * C with the operands' max |x| given:
@@ -985,8 +1008,9 @@ extern "C" int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, flo
   const bool a_kc = !transA, b_kc = transB != 0;
   if ((a_kc && (lda % 4 || (uintptr_t)A % 16)) || (b_kc && (ldb % 4 || (uintptr_t)B % 16)))
     return (int)hipErrorNotSupported;
-  GemmF16Args a;
-  a.A = A; a.B = B; a.amax = amax; a.bmax = bmax;
+  hipStream_t st = kcnn::as_stream(stream);
+  GemmF16Args a{};
+  a.A = A; a.B = B; a.C = C; a.amax = amax; a.bmax = bmax;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.alpha = alpha; a.beta = beta;
   a.tiles_m = (M + BM - 1) / BM;
@@ -995,10 +1019,9 @@ extern "C" int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, flo
   int s = choose_ksplit(tiles, K);
   const size_t need = s > 1 ? sizeof(float) * (size_t)s * M * N : 0;
   if (need > ws_bytes || !ws) s = 1;
+  if (s > 1) a.part = static_cast<float *>(ws);
   a.ksplit = s;
   a.kps = ((K + s - 1) / s + BK - 1) / BK * BK;
-  a.partial = s > 1;
-  a.C = s > 1 ? static_cast<float *>(ws) : C;
   const int64_t nb = tiles * s;
   if (nb >= ((int64_t)1 << 31)) return (int)hipErrorNotSupported;
   // every offset a workgroup forms (rows of its tile, k up to K + 2 BK) < 2^31
@@ -1007,7 +1030,6 @@ extern "C" int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, flo
     return (int64_t)(a.kps + 2 * BK) * ld * 4 + (int64_t)R * 4 < ((int64_t)1 << 31);
   };
   if (!fits(a_kc, lda, BM) || !fits(b_kc, ldb, BN)) return (int)hipErrorNotSupported;
-  hipStream_t st = kcnn::as_stream(stream);
   // a row-contiguous operand takes 16-B loads along its rows when they are
   // aligned and its row count (M or N) is a multiple of 4
   auto mode = [](bool kc, const float *ptr, int ld, int rows) {
@@ -1017,36 +1039,25 @@ extern "C" int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, flo
   };
   launch(mode(a_kc, A, lda, M), mode(b_kc, B, ldb, N), a, (unsigned)nb, st);
   int rc = kcnn::launch_status();
-  if (rc) return rc;
-  if (s > 1) {
-    if (N % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0)
-      hipLaunchKernelGGL(gemm_f16x3_reduce_kernel<true>,
-                         dim3(kcnn::grid_for((int64_t)M * (N / 4))), dim3(256), 0, st,
-                         (const float *)ws, s, M, N, alpha, beta, C, ldc, amax, bmax);
-    else
-      hipLaunchKernelGGL(gemm_f16x3_reduce_kernel<false>, dim3(kcnn::grid_for((int64_t)M * N)),
-                         dim3(256), 0, st, (const float *)ws, s, M, N, alpha, beta, C, ldc,
-                         amax, bmax);
-    rc = kcnn::launch_status();
-    if (rc) return rc;
-  }
-  FixupArgs f;
-  f.A = A; f.B = B; f.C = C; f.amax = amax; f.bmax = bmax;
-  f.M = M; f.N = N; f.K = K; f.lda = lda; f.ldb = ldb; f.ldc = ldc;
-  f.transA = transA != 0; f.transB = transB != 0; f.alpha = alpha; f.beta = beta;
-  hipLaunchKernelGGL(gemm_f16x3_fixup_kernel, dim3(64), dim3(256), 0, st, f);
+  if (rc || s == 1) return rc;
+  if (N % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0)
+    hipLaunchKernelGGL(gemm_f16x3_reduce_kernel<true>, dim3(kcnn::grid_for((int64_t)M * (N / 4))),
+                       dim3(256), 0, st, a.part, s, M, N, alpha, beta, C, ldc, amax, bmax);
+  else
+    hipLaunchKernelGGL(gemm_f16x3_reduce_kernel<false>, dim3(kcnn::grid_for((int64_t)M * N)),
+                       dim3(256), 0, st, a.part, s, M, N, alpha, beta, C, ldc, amax, bmax);
   return kcnn::launch_status();
 }
 
-// The same with the operand statistics computed here: A's rows (its columns
-// when transposed) and B's columns (rows when transposed), into the
-// workspace after the partial slabs.
+// The same with the operand statistics computed here (op(A)'s rows: A's rows,
+// or its columns when transposed; op(B)'s columns: B's columns, or its rows
+// when transposed), one launch for both (two with a per-column one), into
+// the workspace after the partial slabs.
 namespace {
 size_t stats_ws_words(int M, int N, int K, int transA, int transB) {
-  // maxima of op(A)'s rows and op(B)'s columns, then the column partials
-  const size_t pa = transA ? kl_absmax_cols_words(K, M) : 0;
-  const size_t pb = transB ? 0 : kl_absmax_cols_words(K, N);
-  return (size_t)M + N + 4 + (pa > pb ? pa : pb);
+  const size_t pa = transA ? stat_part_words(K, M, 1) : 0;
+  const size_t pb = transB ? 0 : stat_part_words(K, N, 1);
+  return (size_t)M + N + 4 + pa + pb;
 }
 }  // namespace
 extern "C" size_t kl_gemm_f16x3_full_workspace_bytes(int M, int N, int K) {
@@ -1066,14 +1077,13 @@ extern "C" int kl_gemm_f16x3(int transA, int transB, int M, int N, int K, float 
     return (int)hipErrorInvalidValue;
   uint32_t *amax = reinterpret_cast<uint32_t *>(static_cast<char *>(ws) + pb);
   uint32_t *bmax = amax + M;
-  uint32_t *part = bmax + N + 4;
-  // op(A)'s rows: A's rows (stored M x K), or its columns (stored K x M)
-  int rc = transA ? kl_absmax_cols(A, K, M, lda, amax, part, stream)
-                  : kl_absmax_rows(A, M, K, lda, amax, stream);
-  if (rc) return rc;
-  // op(B)'s columns: B's columns (stored K x N), or its rows (stored N x K)
-  rc = transB ? kl_absmax_rows(B, N, K, ldb, bmax, stream)
-              : kl_absmax_cols(B, K, N, ldb, bmax, part, stream);
+  uint32_t *parta = bmax + N + 4;
+  uint32_t *partb = parta + (transA ? stat_part_words(K, M, 1) : 0);
+  const StatOp sa = transA ? stat_op(A, K, M, lda, 1, amax, parta)
+                           : stat_op(A, M, K, lda, 0, amax, nullptr);
+  const StatOp sb = transB ? stat_op(B, N, K, ldb, 0, bmax, nullptr)
+                           : stat_op(B, K, N, ldb, 1, bmax, partb);
+  const int rc = stats_launch(sa, sb, kcnn::as_stream(stream));
   if (rc) return rc;
   return kl_gemm_f16x3_st(transA, transB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, amax,
                           bmax, pb ? ws : nullptr, pb, stream);

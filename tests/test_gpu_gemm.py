@@ -139,12 +139,14 @@ def test_gemm_f16x3_row_scales(kc, case, ta, tb, shape):
 
 @pytest.mark.parametrize("mode", [2, 0])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
-def test_gemm_nonfinite_pattern(kc, mode, ta, tb):
+@pytest.mark.parametrize("shape", [(260, 140, 300), (300, 260, 4500)])
+def test_gemm_nonfinite_pattern(kc, mode, ta, tb, shape):
     """Inf and NaN operands give sgemm's IEEE pattern (+Inf, -Inf, NaN, and
     the finite elements elsewhere within the bound): f16x3 computes the rows
-    and columns they touch as fp32 dot products; rocBLAS for comparison."""
+    and columns they touch as fp32 dot products; rocBLAS for comparison.
+    The second shape splits K over workgroups (in-kernel reduction)."""
     import torch
-    m, n, k = 260, 140, 300
+    m, n, k = shape
     a, b, c0 = _mats(torch, m, n, k, ta, tb, seed=5)
     A = a.t() if ta else a
     B = b.t() if tb else b

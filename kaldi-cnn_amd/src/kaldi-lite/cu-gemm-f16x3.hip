@@ -207,7 +207,10 @@ struct Loader {
   // split and write the two planes (plane stride PL bytes); kv < BK: the
   // tile is the last, partial one and its k >= kv are zeroed (they are the
   // next row's values or a pitch's padding)
-  template <int PL>
+  // (RAG: K is not a whole number of BK steps, so the last tile can be
+  // partial; without it no masking code is emitted -- the compiler turns
+  // the uniform kv test into per-element selects)
+  template <int PL, bool RAG>
   __device__ __forceinline__ void store(char *lds, int tid, int kv) const {
 #pragma unroll
     for (int u = 0; u < UPT; ++u) {
@@ -217,7 +220,7 @@ struct Loader {
       for (int j = 0; j < NV; ++j) x[j] = v[u][j];
       if constexpr (MODE == LT) {
         const int rq = unit % (R / 4), kq = unit / (R / 4);
-        if (kv < BK) {
+        if (RAG && kv < BK) {
 #pragma unroll
           for (int j = 0; j < KPT; ++j)
             if (kq * KPT + j >= kv)
@@ -244,7 +247,7 @@ struct Loader {
           c0 = (unit / R) * (KPT / 8);
           kb = (unit / R) * KPT;
         }
-        if (kv < BK) {
+        if (RAG && kv < BK) {
 #pragma unroll
           for (int j = 0; j < KPT; ++j)
             if (kb + j >= kv) x[j] = 0.0f;
@@ -268,7 +271,7 @@ struct Loader {
   // caller's temporaries; a unit's (LK, LR) or a k-row's (LT) plane writes go
   // with its last piece
   static constexpr int NPIECE = MODE == LT ? 2 * KPT : UPT * (KPT / 2);
-  template <int PL>
+  template <int PL, bool RAG>
   __device__ __forceinline__ void piece(char *lds, int tid, int pc, int kv, uint32_t (&ph)[4],
                                         uint32_t (&pl)[4]) const {
     if constexpr (MODE == LT) {
@@ -276,7 +279,7 @@ struct Loader {
       const int unit = tid;
       const int rq = unit % (R / 4), kq = unit / (R / 4);
       float x0 = v[0][4 * j + 2 * hf], x1 = v[0][4 * j + 2 * hf + 1];
-      if (kv < BK && kq * KPT + j >= kv) x0 = x1 = 0.0f;
+      if (RAG && kv < BK && kq * KPT + j >= kv) x0 = x1 = 0.0f;
       split2h(x0, x1, e[2 * hf], e[2 * hf + 1], ph[hf], pl[hf]);
       if (hf == 1) {
         const int o = tswz<R>(kq * KPT + j, 4 * rq);
@@ -298,7 +301,7 @@ struct Loader {
         kb = (unit / R) * KPT;
       }
       float x0 = v[u][2 * q], x1 = v[u][2 * q + 1];
-      if (kv < BK) {
+      if (RAG && kv < BK) {
         if (kb + 2 * q >= kv) x0 = 0.0f;
         if (kb + 2 * q + 1 >= kv) x1 = 0.0f;
       }
@@ -413,7 +416,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
   }
 }
 
-template <int AM, int BMODE>
+template <int AM, int BMODE, bool RAG>
 __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
   constexpr bool A_KC = AM == LK, B_KC = BMODE == LK;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -471,8 +474,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
   if (T > 0) {
     la[0].load(rsA, p.lda, vra, kk(0, A_KC), tid);
     lb[0].load(rsB, p.ldb, vrb, kk(0, B_KC), tid);
-    la[0].template store<A_PLANE>(lds, tid, T == 1 ? klast : BK);
-    lb[0].template store<B_PLANE>(lds + 2 * A_PLANE, tid, T == 1 ? klast : BK);
+    la[0].template store<A_PLANE, RAG>(lds, tid, T == 1 ? klast : BK);
+    lb[0].template store<B_PLANE, RAG>(lds + 2 * A_PLANE, tid, T == 1 ? klast : BK);
     // tiles 1, 2 into sets 1, 0 (as at every later loop entry)
     __builtin_amdgcn_sched_barrier(0);
     la[1].load(rsA, p.lda, vra, kk(1, A_KC), tid);
@@ -518,13 +521,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
         const int kv = t + 2 == T ? klast : BK;
         half_step(buf, 0);
         if (!late && t + 1 < T) {
-          lan.template store<A_PLANE>(nA, tid, kv);
-          lbn.template store<B_PLANE>(nA + 2 * A_PLANE, tid, kv);
+          lan.template store<A_PLANE, RAG>(nA, tid, kv);
+          lbn.template store<B_PLANE, RAG>(nA + 2 * A_PLANE, tid, kv);
         }
         half_step(buf, 1);
         if (late && t + 1 < T) {
-          lan.template store<A_PLANE>(nA, tid, kv);
-          lbn.template store<B_PLANE>(nA + 2 * A_PLANE, tid, kv);
+          lan.template store<A_PLANE, RAG>(nA, tid, kv);
+          lbn.template store<B_PLANE, RAG>(nA + 2 * A_PLANE, tid, kv);
         }
       }
       lan.load(rsA, p.lda, vra, kk(t + 3, A_KC), tid);
@@ -558,7 +561,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
 // its power limit.  f16x3's three leave the clock up, and the MFMA pipe idles
 // on LDS latency instead (35-44 % busy at 2.1-2.3 GHz with the two-phase
 // loop).
-template <int AM, int BMODE>
+template <int AM, int BMODE, bool RAG>
 __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
   constexpr bool A_KC = AM == LK, B_KC = BMODE == LK;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -630,8 +633,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
   if (T > 0) {
     la[0].load(rsA, p.lda, vra, kk(0, A_KC), tid);
     lb[0].load(rsB, p.ldb, vrb, kk(0, B_KC), tid);
-    la[0].template store<A_PLANE>(lds, tid, T == 1 ? klast : BK);
-    lb[0].template store<B_PLANE>(lds + 2 * A_PLANE, tid, T == 1 ? klast : BK);
+    la[0].template store<A_PLANE, RAG>(lds, tid, T == 1 ? klast : BK);
+    lb[0].template store<B_PLANE, RAG>(lds + 2 * A_PLANE, tid, T == 1 ? klast : BK);
     __builtin_amdgcn_sched_barrier(0);
     la[1].load(rsA, p.lda, vra, kk(1, A_KC), tid);
     lb[1].load(rsB, p.ldb, vrb, kk(1, B_KC), tid);
@@ -656,9 +659,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
         mfma_n(n, fa0, fb0);
         if (more) {
           if (n < LA::NPIECE)
-            lan.template piece<A_PLANE>(nbuf, tid, n, kv, ph, pl);
+            lan.template piece<A_PLANE, RAG>(nbuf, tid, n, kv, ph, pl);
           else if (n - LA::NPIECE < LB::NPIECE)
-            lbn.template piece<B_PLANE>(nbuf + 2 * A_PLANE, tid, n - LA::NPIECE, kv, ph, pl);
+            lbn.template piece<B_PLANE, RAG>(nbuf + 2 * A_PLANE, tid, n - LA::NPIECE, kv, ph, pl);
         }
         if (n >= 2 && n < 10) read_frag(buf, 1, n - 2, fa1, fb1);
         __builtin_amdgcn_sched_barrier(0);
@@ -925,42 +928,48 @@ int choose_ksplit(int64_t tiles, int K) {
 
 // KCNN_F16X3_FAST (experiment build): 1 (default) the one-barrier fast
 // kernel where no operand is LR, 0 the two-phase kernel (bitwise the same C)
-template <int AM, int BMODE>
+template <int AM, int BMODE, bool RAG>
 void launch_t(const GemmF16Args &a, unsigned blocks, hipStream_t st) {
   static const int fast = KCNN_KNOB("KCNN_F16X3_FAST", 1);
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void *>(&gemm_f16x3_kernel<AM, BMODE>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                               LDS_BYTES) == hipSuccess;
+    return hipFuncSetAttribute(
+               reinterpret_cast<const void *>(&gemm_f16x3_kernel<AM, BMODE, RAG>),
+               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   }();
   (void)attr;
   // (an LR operand's 16 loaded values per thread and K step spill there)
   if constexpr (AM != LR && BMODE != LR) {
     static bool fattr = [] {
       return hipFuncSetAttribute(
-                 reinterpret_cast<const void *>(&gemm_f16x3_fast_kernel<AM, BMODE>),
+                 reinterpret_cast<const void *>(&gemm_f16x3_fast_kernel<AM, BMODE, RAG>),
                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
     }();
     (void)fattr;
     if (fast) {
-      hipLaunchKernelGGL((gemm_f16x3_fast_kernel<AM, BMODE>), dim3(blocks), dim3(NT),
+      hipLaunchKernelGGL((gemm_f16x3_fast_kernel<AM, BMODE, RAG>), dim3(blocks), dim3(NT),
                          LDS_BYTES, st, a);
       return;
     }
   }
-  hipLaunchKernelGGL((gemm_f16x3_kernel<AM, BMODE>), dim3(blocks), dim3(NT), LDS_BYTES, st, a);
+  hipLaunchKernelGGL((gemm_f16x3_kernel<AM, BMODE, RAG>), dim3(blocks), dim3(NT), LDS_BYTES, st,
+                     a);
+}
+template <bool RAG>
+void launch_r(int am, int bm, const GemmF16Args &a, unsigned blocks, hipStream_t st) {
+  // am: LK or a row-contiguous mode; bm likewise
+  if (am == LK && bm == LK) launch_t<LK, LK, RAG>(a, blocks, st);
+  else if (am == LK && bm == LT) launch_t<LK, LT, RAG>(a, blocks, st);
+  else if (am == LK) launch_t<LK, LR, RAG>(a, blocks, st);
+  else if (am == LT && bm == LK) launch_t<LT, LK, RAG>(a, blocks, st);
+  else if (am == LT && bm == LT) launch_t<LT, LT, RAG>(a, blocks, st);
+  else if (am == LT) launch_t<LT, LR, RAG>(a, blocks, st);
+  else if (bm == LK) launch_t<LR, LK, RAG>(a, blocks, st);
+  else if (bm == LT) launch_t<LR, LT, RAG>(a, blocks, st);
+  else launch_t<LR, LR, RAG>(a, blocks, st);
 }
 void launch(int am, int bm, const GemmF16Args &a, unsigned blocks, hipStream_t st) {
-  // am: LK or a row-contiguous mode; bm likewise
-  if (am == LK && bm == LK) launch_t<LK, LK>(a, blocks, st);
-  else if (am == LK && bm == LT) launch_t<LK, LT>(a, blocks, st);
-  else if (am == LK) launch_t<LK, LR>(a, blocks, st);
-  else if (am == LT && bm == LK) launch_t<LT, LK>(a, blocks, st);
-  else if (am == LT && bm == LT) launch_t<LT, LT>(a, blocks, st);
-  else if (am == LT) launch_t<LT, LR>(a, blocks, st);
-  else if (bm == LK) launch_t<LR, LK>(a, blocks, st);
-  else if (bm == LT) launch_t<LR, LT>(a, blocks, st);
-  else launch_t<LR, LR>(a, blocks, st);
+  if (a.K % BK) launch_r<true>(am, bm, a, blocks, st);
+  else launch_r<false>(am, bm, a, blocks, st);
 }
 
 size_t align16(size_t b) { return (b + 15) & ~(size_t)15; }

@@ -76,9 +76,11 @@ int kcnn_set_fusion(int mode);
  * Env KCNN_GEMM (0/1/2) sets the initial mode. */
 int kcnn_set_gemm_mode(int mode);
 /* Kernel-family selectors (kaldi-lite/kcnn-knobs.h): each picks
- * one of two implementations of the same fp32 math, the bf16x6 kernels on
- * the bf16 matrix cores (default) or the fp32-input MFMA kernels.
- *   "fwd_x6"   frame-resident conv forward      1 (default) / 0
+ * one of the implementations of the same fp32 math: the split-operand
+ * kernels on the f16 / bf16 matrix cores (f16x3: two f16 parts under a
+ * power-of-two scale, three products; bf16x6: three bf16 parts, six
+ * products) or the fp32-input MFMA kernels (0).
+ *   "fwd_x6"   frame-resident conv forward      2 (default, f16x3) / 1 / 0
  *   "bwd_x6"   fused conv backward              1 (default) / 0
  *   "igemm_x6" implicit-GEMM forward and dgrad  1 (default) / 0
  *   "wgrad_x6" long-kernel weight gradient      2 (default, wide) / 1 / 0

@@ -152,8 +152,9 @@ def set_gemm_mode(mode: int):
 
 
 def set_kernel_family(name: str, value: int):
-    """Kernel-family selector (kcnn.h): "fwd_x6", "bwd_x6", "igemm_x6",
-    "wgrad_x6" (2 wide / 1 / 0) or "gemm"; 0 = the fp32-MFMA kernels."""
+    """Kernel-family selector (kcnn.h): "fwd_x6" (2 f16x3 / 1 bf16x6 / 0),
+    "bwd_x6", "igemm_x6", "wgrad_x6" (2 wide / 1 / 0) or "gemm" (2 f16x3 /
+    1 bf16x6 / 0 rocBLAS); 0 = the fp32-MFMA kernels."""
     check(lib().kcnn_set_kernel_family(name.encode(), int(value)))
 
 

@@ -27,6 +27,7 @@
 #include <stdlib.h>
 
 #include "conv-geom.h"
+#include "f16-split.h"
 #include "x6-util.h"
 
 using namespace kcnn;
@@ -233,33 +234,131 @@ __global__ __launch_bounds__(256) void conv_fwd_slab_kernel(
 // Kdim against a constant-1 row of B, so the accumulators hold conv + bias
 // and no epilogue add remains; B = the gathered im2col values, split in
 // registers once per frame and tile.  Unpadded maps only (host check).
+// F16 (AR = 2): the products on the f16 matrix cores (f16-split.h), three
+// per k16 step.  A = W^T scaled by 2^sa (one exponent for the whole kernel,
+// from the wave's max |W|: every wave holds all of W), split once per kernel
+// into hi / lo planes; B = the gathered im2col values of one position scaled
+// by 2^sb(p) (the position's own max |x| over its taps: lanes l and l + 32
+// hold the two halves of a column), split per frame and tile.  The bias is
+// not a row of the product: y = fma(acc, 2^-(sa + sb(p)), b) exactly unscales
+// and adds it in one rounding.  A tile whose column max is Inf, or whose
+// unscale factor would leave fp32's range, sends the wave's whole frame to
+// fwd_item_fp32 (plain fp32 sums, the reference's IEEE Inf / NaN pattern);
+// a kernel with Inf in W sends every frame.  The decision is per (frame,
+// wave) in every epilogue, so fused and unfused runs compute the same y.
 struct PoolWin {
   int ph, pw, pc, oh2, OP;
   FastDiv div_OP, div_oh2;
 };
 
-template <int KS, int FT, int PC, bool X6>
+// The F16 fallback for one item (32 filters gb*32.. x the 32 positions of
+// p's tile) in fp32: y = sum_k W[k][g] x_k(p), then + b[g] (the reference's
+// GEMM then bias add, conv2D.cc:138-145), the accumulator layout of the MFMA.
+__device__ __forceinline__ floatx16 fwd_item_fp32(
+    const ConvGeom &g, const float *__restrict__ K, int ks, const float *__restrict__ bias,
+    const float *Xs, const int2 *koff, int gb, int tile, int lane) {
+  const int h = lane >> 5;
+  const int p = min(tile * 32 + (lane & 31), g.P - 1);
+  uint32_t px, py;
+  g.div_oh.divmod((uint32_t)p, px, py);
+  const int pb = (int)px * g.H + (int)py;
+  floatx16 y;
+#pragma unroll
+  for (int r = 0; r < 16; r++) y[r] = 0.0f;
+  for (int k = 0; k < g.Kdim; k++) {
+    const float x = Xs[koff[k].x + pb];
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int gg = gb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      y[r] = fmaf(gg < g.G ? K[(int64_t)k * ks + gg] : 0.0f, x, y[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const int gg = gb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    y[r] = y[r] + (bias && gg < g.G ? bias[gg] : 0.0f);
+  }
+  return y;
+}
+
+// The routing mask of a 4-way pool group, bit c = (v_c == mx): the four
+// compares first, then the four selects, so each select reads a compare
+// result three VALU later and needs no wait states (hipcc's order, compare /
+// select pairs, pads every pair with s_nop 1).
+__device__ __forceinline__ unsigned tie_mask4(float v0, float v1, float v2, float v3, float mx) {
+  unsigned m, t0, t1, t2, t3;
+  uint64_t c0, c1, c2, c3;
+  asm("v_cmp_eq_f32_e64 %5, %9, %13\n\t"
+      "v_cmp_eq_f32_e64 %6, %10, %13\n\t"
+      "v_cmp_eq_f32_e64 %7, %11, %13\n\t"
+      "v_cmp_eq_f32_e64 %8, %12, %13\n\t"
+      "v_cndmask_b32_e64 %1, 0, 1, %5\n\t"
+      "v_cndmask_b32_e64 %2, 0, 2, %6\n\t"
+      "v_cndmask_b32_e64 %3, 0, 4, %7\n\t"
+      "v_cndmask_b32_e64 %4, 0, 8, %8\n\t"
+      "v_or3_b32 %0, %1, %2, %3\n\t"
+      "v_or_b32_e32 %0, %0, %4"
+      : "=v"(m), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&s"(c0), "=&s"(c1),
+        "=&s"(c2), "=&s"(c3)
+      : "v"(v0), "v"(v1), "v"(v2), "v"(v3), "v"(mx));
+  return m;
+}
+
+// RP: the register-pooled form only (out == nullptr, PC 2 or 4, G = 128 and
+// every wave with FT position tiles: c2), without the generic item loop and
+// the LDS epilogue, whose uniform conditions otherwise overflow the SGPRs.
+template <int KS, int FT, int PC, int AR, bool RP = false>
 __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
     ConvGeom g, const float *__restrict__ X, int xs,
     const float *__restrict__ K, int ks, const float *__restrict__ bias,
     float *__restrict__ out, int os, int vec_ok, int dbg,
     float *__restrict__ pool, int ps, unsigned char *__restrict__ mask, int ms,
     PoolWin pw3) {
+  constexpr bool X6 = AR == 1, F16 = AR == 2, SPL = AR != 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float *T = reinterpret_cast<float *>(smem);                 // [32][P]
   float *Bs = T + ((32 * g.P + 3) & ~3);                      // [128] bias
-  int2 *koff = reinterpret_cast<int2 *>(Bs + 128);             // [2*KS] taps
-  constexpr int NKT = X6 ? 16 * KS : 2 * KS;                    // tap entries (<= 32)
+  float *Bz = Bs + 128;                                       // [32] -0 (F16 fp32 items)
+  int2 *koff = reinterpret_cast<int2 *>(Bs + 160);             // [2*KS] taps
+  constexpr int NKT = SPL ? 16 * KS : 2 * KS;                   // tap entries (<= 32)
   float *Xs = reinterpret_cast<float *>(koff + NKT);            // [C*HW]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = lane & 31, h = lane >> 5;
   const int NG = (g.G + 31) >> 5;  // <= 4 (host check)
   if (tid < 128) Bs[tid] = (bias && tid < g.G) ? bias[tid] : 0.0f;
+  if (tid < 32) Bz[tid] = -0.0f;
   // A operand: W[k = 2s + h][gb*32 + l]
   float wreg[X6 ? 1 : 4][X6 ? 1 : KS];
   // X6: W^T[gb*32 + l][k = 16s + 8h + e] (e < 8), the bias at k = Kdim
   x6::bf16x8 w6[X6 ? 4 : 1][X6 ? KS : 1][3];
+  // F16: W^T[gb*32 + l][k = 16s + 8h + e] * 2^sa, hi and lo planes
+  f16x3::f16x8 wh[F16 ? 4 : 1][F16 ? KS : 1], wl[F16 ? 4 : 1][F16 ? KS : 1];
+  int sa = 0;
+  bool wslow = false;  // Inf in W: every item in fp32
+  if constexpr (F16) {
+    float wv[4][KS][8];
+    float m = 0.0f;
+#pragma unroll
+    for (int gb = 0; gb < 4; gb++)
+#pragma unroll
+      for (int s = 0; s < KS; s++)
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          const int k = 16 * s + 8 * h + e, gg = gb * 32 + l;
+          wv[gb][s][e] = gg < g.G && k < g.Kdim ? K[(int64_t)k * ks + gg] : 0.0f;
+          m = fmaxf(m, fabsf(wv[gb][s][e]));  // NaN ignored: it propagates by itself
+        }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    const int s0 = f16x3::scale_exp(__builtin_amdgcn_readfirstlane(__float_as_uint(m)));
+    wslow = s0 == f16x3::SKIP;
+    sa = wslow ? 0 : s0;
+#pragma unroll
+    for (int gb = 0; gb < 4; gb++)
+#pragma unroll
+      for (int s = 0; s < KS; s++) f16x3::split8h(wv[gb][s], sa, wh[gb][s], wl[gb][s]);
+  }
   if constexpr (X6) {
 #pragma unroll
     for (int gb = 0; gb < 4; gb++)
@@ -293,7 +392,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
       uint32_t c, r, qx, qy;
       g.div_khkw.divmod((uint32_t)tid, c, r);
       g.div_kh.divmod(r, qx, qy);
-      v = X6 ? make_int2((int)c * g.HW + (int)qx * g.H + (int)qy, 0)
+      v = SPL ? make_int2((int)c * g.HW + (int)qx * g.H + (int)qy, 0)
              : make_int2((int)c * g.HW, (int)((qx << 16) | qy));
     }
     koff[tid] = v;
@@ -304,7 +403,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
   // (c2's 8 x 1 kernel: taps c*8 + ky at c*HW + ky)?  Then a group's 8 values
   // are read at one offset + e, without the per-tap table reads
   bool run8 = false;
-  if constexpr (X6) {
+  if constexpr (SPL) {
     run8 = !(dbg & 64);
     for (int k = 0; k + 1 < g.Kdim && run8; k++) {
       if ((k + 1) % 8 == 0) continue;
@@ -338,6 +437,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
     // they overflow the register file)
     int tid_f = tid;
     asm volatile("" : "+v"(tid_f));
+    int wave_q = wave;  // likewise the wave id (held, the wave-derived item
+    asm volatile("" : "+s"(wave_q));  // constants overflow the SGPRs)
     const int lane_f = tid_f & 63, l_f = lane_f & 31, h_f = lane_f >> 5;
     __syncthreads();  // previous frame's Xs / T reads done
     KCNN_TMARK(5)
@@ -352,17 +453,62 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
     }
     __syncthreads();
     KCNN_TMARK(0)
-    float bx[X6 ? 1 : FT][X6 ? 1 : KS];
+    float bx[SPL ? 1 : FT][SPL ? 1 : KS];
     x6::bf16x8 bx6[X6 ? FT : 1][X6 ? KS : 1][3];
+    f16x3::f16x8 bxh[F16 ? FT : 1][F16 ? KS : 1], bxl[F16 ? FT : 1][F16 ? KS : 1];
+    float ft[F16 ? FT : 1];  // F16: the unscale factor 2^-(sa + sb(p)) of tile t
+    bool slow = false;       // F16: this wave_q's items of the frame in fp32
 #pragma unroll
     for (int t = 0; t < FT; t++) {
+      if constexpr (F16) {
+        // B[k = 16s + 8h + e][p] = x_k(p) for k < Kdim, 0 past it
+        if ((wave_q + 4 * t) * 32 >= g.P) continue;  // wave_q-uniform: no tile
+        const int p = min((wave_q + 4 * t) * 32 + l_f, g.P - 1);
+        uint32_t px, py;
+        g.div_oh.divmod((uint32_t)p, px, py);
+        const int pb = (int)px * g.H + (int)py;
+        float v[KS][8];
+        float m = 0.0f;
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+          const int k0 = 16 * s + 8 * h_f;
+          if (run8) {  // uniform
+            const float *xr = Xs + koff[k0].x + pb;
+#pragma unroll
+            for (int e = 0; e < 8; e++) v[s][e] = xr[e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; e++) v[s][e] = Xs[koff[k0 + e].x + pb];
+          }
+#pragma unroll
+          for (int e = 0; e < 8; e++) {
+            v[s][e] = k0 + e < g.Kdim ? v[s][e] : 0.0f;
+            m = fmaxf(m, fabsf(v[s][e]));
+          }
+        }
+        // the column's other half: lane l ^ 32, through ds_bpermute.  (With
+        // v_permlane32_swap here, one accumulator register of 16 lanes of a
+        // wave's last item came out wrong in about one call in four of a
+        // 601-frame forward, G = 96, Kdim 12; experiments/diag_det2.py.)
+        m = fmaxf(m, __shfl_xor(m, 32));
+        const uint32_t mb = __float_as_uint(m);
+        int sb = mb == 0 ? -sa : f16x3::scale_exp(mb);
+        const int E = -(sa + sb);
+        const bool bad = sb == f16x3::SKIP || E < -149 || E > 127;
+        if (bad) sb = 0;
+        ft[t] = __builtin_amdgcn_ldexpf(1.0f, bad ? 0 : E);
+        if (__builtin_amdgcn_ballot_w64(bad) != 0) slow = true;
+#pragma unroll
+        for (int s = 0; s < KS; s++) f16x3::split8h(v[s], sb, bxh[t][s], bxl[t][s]);
+        continue;
+      }
       if constexpr (X6) {
         // B[k = 16s + 8h + e][p]: the map value of tap k at p (one add: the
         // maps are unpadded, so every tap of a valid position is inside),
         // 1 at k = Kdim (the bias row), 0 past it; positions past P read a
         // clamped position and are never stored
-        if ((wave + 4 * t) * 32 >= g.P) continue;  // wave-uniform: no tile
-        const int p = min((wave + 4 * t) * 32 + l_f, g.P - 1);
+        if ((wave_q + 4 * t) * 32 >= g.P) continue;  // wave_q-uniform: no tile
+        const int p = min((wave_q + 4 * t) * 32 + l_f, g.P - 1);
         uint32_t px, py;
         g.div_oh.divmod((uint32_t)p, px, py);
         const int pb = (int)px * g.H + (int)py;
@@ -389,7 +535,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
         }
         continue;
       }
-      const int p = (wave + 4 * t) * 32 + l_f;
+      const int p = (wave_q + 4 * t) * 32 + l_f;
       const bool pv = p < g.P;
       uint32_t px = 0, py = 0;
       g.div_oh.divmod((uint32_t)(pv ? p : 0), px, py);
@@ -403,32 +549,24 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
         bx[t][s] = ok ? v : 0.0f;
       }
     }
+    if constexpr (F16) slow = slow || wslow;
     KCNN_TMARK(1)
-    if constexpr (X6 && (PC == 2 || PC == 4)) {
+    if constexpr (SPL && (PC == 2 || PC == 4)) {
       if (out == nullptr) {  // uniform: pooled straight from the registers
         // items (gb, t) in order; the MFMA chain of item i is issued before
         // the pooling of item i - 1, so that VALU work runs under the chain
         constexpr int NI = 4 * FT;
-        floatx16 accp[2];
         const int npool = g.G / PC * g.P;  // pooled values of one frame row
         const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(pool + (int64_t)n * ps), (short)0, npool * 4, 0x00020000);
         const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(mask + (int64_t)n * ms), (short)0, npool, 0x00020000);
-        auto valid = [&](int i) { return i / FT < NG && wave + 4 * (i % FT) < ntile; };
-#pragma unroll
-        for (int i = 0; i <= NI; i++) {
-          if (i < NI && valid(i)) {
-            const int gb = i / FT, t = i % FT;
-            floatx16 a = zero16();
-#pragma unroll
-            for (int s = 0; s < KS; s++) a = x6::mfma6(w6[gb][s], bx6[t][s], a);
-            accp[i & 1] = a;
-          }
-          if (i == 0 || !valid(i - 1)) continue;
-          const int gb = (i - 1) / FT, t = (i - 1) % FT;
-          const floatx16 &acc = accp[(i - 1) & 1];
-          const int p = (wave + 4 * t) * 32 + l_f;
+        auto valid = [&](int i) { return i / FT < NG && wave_q + 4 * (i % FT) < ntile; };
+        // the pooling of one item's accumulators (F16: y = acc * 2^-(sa +
+        // sb(p)) + b first, in one rounding; fp32 items: acc * 1 + -0, i.e.
+        // acc itself)
+        auto pool_item = [&](floatx16 &acc, int gb, int t, bool sl) {
+          const int p = (wave_q + 4 * t) * 32 + l_f;
           // accumulator r = 4k + i of lane (l, h) is filter 8k + 4h + i at
           // position p: a pool group is PC consecutive registers (the
           // compares and order of the LDS epilogue, so the same bits).  Its
@@ -438,28 +576,135 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
           // multiple of 32), get a voffset past the descriptors' ranges and
           // are dropped (the range check covers voffset, not soffset).
           const unsigned vo = p < g.P ? (unsigned)(h_f * (4 / PC) * g.P + p) : 0x3ffffff0u;
+          // the rows' soffsets U * P recomputed per item (SALU) instead of
+          // hoisted out of the frame loop (held, they spill SGPRs)
+          int Pq = g.P;
+          asm volatile("" : "+s"(Pq));
+          const float fct = F16 && !sl ? ft[F16 ? t : 0] : 1.0f;
+          // the bias rows' offset made opaque per item: the loads are not
+          // hoisted or shared across items (held for all four filter groups
+          // they would take 64 VGPRs and spill)
+          int boff = (sl ? 128 : gb * 32) + 4 * h_f;  // Bz = Bs + 128
+          asm volatile("" : "+v"(boff));
+          const float *bb = Bs + boff;
+          if constexpr (F16) {
+            // y = acc * 2^-(sa + sb(p)) + b in one rounding (fp32 items:
+            // acc * 1 + -0, i.e. acc itself)
 #pragma unroll
-          for (int r0 = 0; r0 < 16; r0 += PC) {
+            for (int k = 0; k < 4; k++) {
+              const float4 b4 = *reinterpret_cast<const float4 *>(bb + 8 * k);
+              acc[4 * k + 0] = fmaf(acc[4 * k + 0], fct, b4.x);
+              acc[4 * k + 1] = fmaf(acc[4 * k + 1], fct, b4.y);
+              acc[4 * k + 2] = fmaf(acc[4 * k + 2], fct, b4.z);
+              acc[4 * k + 3] = fmaf(acc[4 * k + 3], fct, b4.w);
+            }
+          }
+          // The pool value by IEEE max (v_max3: NaN skipped like the
+          // reference's `val < x` test, ties between equal nonzero values
+          // are the same bits).  The one case max and the reference's
+          // first-wins scan differ is a +0 / -0 tie: any group whose max is
+          // zero is rescanned the reference's way (uniform branch, rare).
+          constexpr int NGP = 16 / PC;
+          float mx[NGP];
+          unsigned msk[NGP];
+          bool anyz = false;
+#pragma unroll
+          for (int j = 0; j < NGP; j++) {
+            float m = fmaxf(-1e20f, acc[j * PC]);
+#pragma unroll
+            for (int c = 1; c < PC; c++) m = fmaxf(m, acc[j * PC + c]);
+            mx[j] = m;
+            anyz |= m == 0.0f;
+          }
+          if (__builtin_expect(anyz, 0)) {
+#pragma unroll
+            for (int j = 0; j < NGP; j++) {
+              if (mx[j] == 0.0f) {
+                float m = -1e20f;
+#pragma unroll
+                for (int c = 0; c < PC; c++)
+                  if (m < acc[j * PC + c]) m = acc[j * PC + c];
+                mx[j] = m;
+              }
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < NGP; j++) {
+            if constexpr (PC == 4) {
+              msk[j] = tie_mask4(acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3], mx[j]);
+            } else {
+              unsigned m = 0;
+#pragma unroll
+              for (int c = 0; c < PC; c++) m |= (acc[j * PC + c] == mx[j] ? 1u : 0u) << c;
+              msk[j] = m;
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < NGP; j++) {
+            const int r0 = j * PC;
             const int U = (gb * 32 + (r0 & 3) + 8 * (r0 >> 2)) / PC;
             const unsigned vv =
                 g.G % 32 == 0 || U + h_f * (4 / PC) < g.G / PC ? vo : 0x3ffffff0u;
-            float mx = -1e20f;
+#ifdef KCNN_EXPERIMENTS  // store A/B: dbg & 256 drops the pooled values, & 512 the masks
+            if (!(dbg & 256))
+#endif
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mx[j]), prs, vv * 4u,
+                                                  (unsigned)(U * Pq) * 4u, 0);
+#ifdef KCNN_EXPERIMENTS
+            if (!(dbg & 512))
+#endif
+            __builtin_amdgcn_raw_buffer_store_b8((unsigned char)msk[j], mrs, vv,
+                                                 (unsigned)(U * Pq), 0);
+          }
+        };
+        if constexpr (F16) {
+          if (slow) {  // uniform: the frame's items in fp32 (rare: Inf, range)
+#pragma unroll 1
+            for (int i = 0; i < NI; i++) {
+              if (!valid(i)) continue;
+              const int gb = i / FT, t = i % FT;
+              floatx16 a = fwd_item_fp32(g, K, ks, bias, Xs, koff, gb, wave_q + 4 * t, lane_f);
+              pool_item(a, gb, t, true);
+            }
+            KCNN_TMARK(2)
+            continue;  // next frame
+          }
+        }
+        auto chain = [&](int gb, int t) {
+          floatx16 a = zero16();
 #pragma unroll
-            for (int c = 0; c < PC; c++)
-              if (mx < acc[r0 + c]) mx = acc[r0 + c];
-            unsigned m = 0;
+          for (int s = 0; s < KS; s++) {
+            if constexpr (F16)
+              a = f16x3::mfma3(wh[gb][s], wl[gb][s], bxh[t][s], bxl[t][s], a);
+            else
+              a = x6::mfma6(w6[gb][s], bx6[t][s], a);
+          }
+          return a;
+        };
+        if (RP || (NG == 4 && wave_q + 4 * (FT - 1) < ntile)) {
+          // every item valid (c2: G = 128, P = 363): one straight-line
+          // sequence, the MFMA chain of item i beside the pooling of i - 1
+          floatx16 prev = chain(0, 0);
 #pragma unroll
-            for (int c = 0; c < PC; c++) m |= (acc[r0 + c] == mx ? 1u : 0u) << c;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mx), prs, vv * 4u,
-                                                  (unsigned)(U * g.P) * 4u, 0);
-            __builtin_amdgcn_raw_buffer_store_b8((unsigned char)m, mrs, vv,
-                                                 (unsigned)(U * g.P), 0);
+          for (int i = 1; i <= NI; i++) {
+            floatx16 cur;
+            if (i < NI) cur = chain(i / FT, i % FT);
+            pool_item(prev, (i - 1) / FT, (i - 1) % FT, false);
+            if (i < NI) prev = cur;
+          }
+        } else if constexpr (!RP) {
+#pragma unroll
+          for (int i = 0; i < NI; i++) {
+            if (!valid(i)) continue;  // uniform
+            floatx16 a = chain(i / FT, i % FT);
+            pool_item(a, i / FT, i % FT, false);
           }
         }
         KCNN_TMARK(2)
         continue;  // next frame
       }
     }
+    if constexpr (RP) continue;  // (never reached: host check)
 #pragma unroll
     for (int gb = 0; gb < 4; gb++) {
       if (gb >= NG) break;
@@ -468,10 +713,20 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
       for (int r = 0; r < 16; r++) bsv[r] = X6 ? 0.0f : Bs[gb * 32 + mfma32_row(r, lane_f)];
 #pragma unroll
       for (int t = 0; t < FT; t++) {
-        const int pt = wave + 4 * t;
-        if (pt >= ntile) continue;  // wave-uniform
+        const int pt = wave_q + 4 * t;
+        if (pt >= ntile) continue;  // wave_q-uniform
         floatx16 acc = zero16();
-        if constexpr (X6) {
+        if constexpr (F16) {
+          if (slow) {
+            acc = fwd_item_fp32(g, K, ks, bias, Xs, koff, gb, pt, lane_f);
+          } else {
+#pragma unroll
+            for (int s = 0; s < KS; s++)
+              acc = f16x3::mfma3(wh[gb][s], wl[gb][s], bxh[t][s], bxl[t][s], acc);
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[r] = fmaf(acc[r], ft[t], bsv[r]);
+          }
+        } else if constexpr (X6) {
 #pragma unroll
           for (int s = 0; s < KS; s++) acc = x6::mfma6(w6[gb][s], bx6[t][s], acc);
         } else {
@@ -496,7 +751,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
                 float mx = -1e20f, v[PC];
 #pragma unroll
                 for (int c = 0; c < PC; c++) {
-                  v[c] = X6 ? acc[r0 + c] : acc[r0 + c] + bsv[r0 + c];
+                  v[c] = SPL ? acc[r0 + c] : acc[r0 + c] + bsv[r0 + c];
                   if (mx < v[c]) mx = v[c];
                 }
                 unsigned m = 0;
@@ -513,7 +768,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
         if (p < g.P) {
 #pragma unroll
           for (int r = 0; r < 16; r++)
-            T[mfma32_row(r, lane_f) * g.P + p] = X6 ? acc[r] : acc[r] + bsv[r];
+            T[mfma32_row(r, lane_f) * g.P + p] = SPL ? acc[r] : acc[r] + bsv[r];
         }
       }
       KCNN_TMARK(2)
@@ -1503,8 +1758,13 @@ int fwd_regs_blocks_per_cu(size_t lds) {
 // the fp32 MFMA.  The rule depends on the
 // layer's shape only, so a fused and an unfused run of a layer use the same
 // arithmetic (bitwise-equal outputs).  KCNN_FWD_X6=0 keeps the fp32 MFMA.
-bool fwd_x6_ok(const ConvGeom &g, int use) {
-  return use && g.pad_h == 0 && g.pad_w == 0 && g.Kdim <= 31 && g.Gtot <= 128;
+// The f16x3 form (family value 2, the default) has the same limits except
+// Kdim <= 32 (no bias row) and half the MFMAs per item.
+// Returns the kernel's AR: 0 fp32 MFMA, 1 bf16x6, 2 f16x3.
+int fwd_arith(const ConvGeom &g, int use) {
+  if (!use || g.pad_h != 0 || g.pad_w != 0 || g.Gtot > 128) return 0;
+  if (use == 2) return g.Kdim <= 32 ? 2 : 0;
+  return g.Kdim <= 31 ? 1 : 0;
 }
 
 unsigned frame_grid(const ConvGeom &g, int blocks_per_cu) {
@@ -1543,23 +1803,25 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
   static const int variant = KCNN_KNOB("KCNN_FWD_VARIANT", 2);
   if (variant == 2 && g.Kdim <= 32 && g.G <= 128 && g.P <= 4 * 32 * 3 &&
       g.C * g.HW <= 256 * 8) {
-    const size_t lds = (size_t)((32 * g.P + 3) & ~3) * 4 + 128 * 4 + 32 * 8 +
+    const size_t lds = (size_t)((32 * g.P + 3) & ~3) * 4 + 160 * 4 + 32 * 8 +
                        (size_t)g.C * g.HW * 4;
     if (lds <= (size_t)kFrameLdsMax) {
       const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0);
       const int ksn = (g.Kdim + 1) / 2;
       static const int bpc_env = KCNN_KNOB("KCNN_FWD_BPC", 0);
-      const bool x6 = fwd_x6_ok(g, family(kFamFwdX6));
+      const int ar = fwd_arith(g, family(kFamFwdX6));
       const unsigned grid = frame_grid(
-          g, bpc_env > 0 ? bpc_env : x6 ? 2 : fwd_regs_blocks_per_cu(lds));
-#define KCNN_FWD_REGS_T(KS_, X6_)                                                       \
-  hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, 0, X6_>), dim3(grid), dim3(256), lds, \
+          g, bpc_env > 0 ? bpc_env : ar ? 2 : fwd_regs_blocks_per_cu(lds));
+#define KCNN_FWD_REGS_T(KS_, AR_)                                                       \
+  hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, 0, AR_>), dim3(grid), dim3(256), lds, \
                      st, g, X, xs, K, ks, bias, out, os, vec_ok, dbg, nullptr, 0, nullptr, \
                      0, PoolWin{})
-#define KCNN_FWD_REGS(KS_) KCNN_FWD_REGS_T(KS_, false)
+#define KCNN_FWD_REGS(KS_) KCNN_FWD_REGS_T(KS_, 0)
       static const int dbg = KCNN_KNOB("KCNN_FWD_DEBUG", 0);
-      if (x6 && g.Kdim < 16) KCNN_FWD_REGS_T(1, true);
-      else if (x6) KCNN_FWD_REGS_T(2, true);
+      if (ar == 2 && g.Kdim <= 16) KCNN_FWD_REGS_T(1, 2);
+      else if (ar == 2) KCNN_FWD_REGS_T(2, 2);
+      else if (ar == 1 && g.Kdim < 16) KCNN_FWD_REGS_T(1, 1);
+      else if (ar == 1) KCNN_FWD_REGS_T(2, 1);
       else if (ksn <= 4) KCNN_FWD_REGS(4);
       else if (ksn <= 8) KCNN_FWD_REGS(8);
       else if (ksn <= 12) KCNN_FWD_REGS(12);
@@ -1642,24 +1904,38 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
   if (g.Kdim > 32 || g.G > 128 || g.P < 16 || g.P > 4 * 32 * 3 ||
       g.C * g.HW > 256 * 8)
     return -1;
-  const size_t lds = (size_t)((32 * g.P + 3) & ~3) * 4 + 128 * 4 + 32 * 8 +
+  const size_t lds = (size_t)((32 * g.P + 3) & ~3) * 4 + 160 * 4 + 32 * 8 +
                      (size_t)g.C * g.HW * 4;
   if (lds > (size_t)kFrameLdsMax) return -1;
   const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0) ? 1 | y_nt() : 0;
   const int ksn = (g.Kdim + 1) / 2;
   static const int grid_env = KCNN_KNOB("KCNN_FWD_GRID", 0);
-  const bool x6 = fwd_x6_ok(g, family(kFamFwdX6));
+  const int ar = fwd_arith(g, family(kFamFwdX6));
   const unsigned grid = grid_env > 0 ? (unsigned)std::min<int64_t>(grid_env, g.R)
-                                     : frame_grid(g, x6 ? 2 : fwd_regs_blocks_per_cu(lds));
+                                     : frame_grid(g, ar ? 2 : fwd_regs_blocks_per_cu(lds));
   static const int dbg = KCNN_KNOB("KCNN_FWD_DEBUG", 0);
-#define KCNN_FWD_POOL_T(KS_, PC_, X6_)                                                      \
-  hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_, X6_>), dim3(grid), dim3(256), lds, \
-                     st, g, X, xs, K, ks, bias, out, os, vec_ok, dbg, pool, ps, mask, ms, pw3)
-#define KCNN_FWD_POOL(KS_, PC_) KCNN_FWD_POOL_T(KS_, PC_, false)
+  // the register-pooled-only form: pooled output only, pc 2 / 4, G = 128
+  // and 12 position tiles (each of the 4 waves has 3)
+  const int ntile = (g.P + 31) / 32;
+  const bool rp = out == nullptr && (pc == 2 || pc == 4) && !win3 && g.G == 128 &&
+                  ntile > 4 * 2 && ntile <= 4 * 3;
+#define KCNN_FWD_POOL_T(KS_, PC_, AR_)                                                      \
+  do {                                                                                       \
+    if (rp && (PC_ == 2 || PC_ == 4) && AR_ != 0)                                            \
+      hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_, AR_, (PC_ == 2 || PC_ == 4) && AR_ != 0>), \
+                         dim3(grid), dim3(256), lds, st, g, X, xs, K, ks, bias, out, os,     \
+                         vec_ok, dbg, pool, ps, mask, ms, pw3);                              \
+    else                                                                                     \
+      hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_, AR_>), dim3(grid), dim3(256), lds, \
+                         st, g, X, xs, K, ks, bias, out, os, vec_ok, dbg, pool, ps, mask, ms, pw3); \
+  } while (0)
+#define KCNN_FWD_POOL(KS_, PC_) KCNN_FWD_POOL_T(KS_, PC_, 0)
 #define KCNN_FWD_POOL_KS(PC_)                     \
   do {                                            \
-    if (x6 && g.Kdim < 16) KCNN_FWD_POOL_T(1, PC_, true); \
-    else if (x6) KCNN_FWD_POOL_T(2, PC_, true);   \
+    if (ar == 2 && g.Kdim <= 16) KCNN_FWD_POOL_T(1, PC_, 2); \
+    else if (ar == 2) KCNN_FWD_POOL_T(2, PC_, 2); \
+    else if (ar == 1 && g.Kdim < 16) KCNN_FWD_POOL_T(1, PC_, 1); \
+    else if (ar == 1) KCNN_FWD_POOL_T(2, PC_, 1); \
     else if (ksn <= 4) KCNN_FWD_POOL(4, PC_);     \
     else if (ksn <= 8) KCNN_FWD_POOL(8, PC_);     \
     else if (ksn <= 12) KCNN_FWD_POOL(12, PC_);   \

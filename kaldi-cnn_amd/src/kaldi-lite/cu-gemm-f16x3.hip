@@ -49,15 +49,19 @@
 
 #include <algorithm>
 
+#include "cnslmat/f16-split.h"
 #include "cnslmat/hip-util.h"
 #include "kaldi-lite/cu-kernels-lite.h"
 
 namespace {
 
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+using kcnn::f16x3::f16x8;
+using kcnn::f16x3::f32x16;
+using kcnn::f16x3::NONFINITE;
+using kcnn::f16x3::SKIP;
+using kcnn::f16x3::scale_exp;
+using kcnn::f16x3::split2h;
+using kcnn::f16x3::mfma;
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -68,8 +72,6 @@ constexpr int A_PLANE = BM * ROWB;            // 16 KB
 constexpr int B_PLANE = BN * ROWB;            // 8 KB
 constexpr int BUF = 2 * (A_PLANE + B_PLANE);  // 48 KB
 constexpr int LDS_BYTES = 2 * BUF + (BM + BN) * 4;
-constexpr uint32_t NONFINITE = 0x7f800000u;   // |x| bits >= this: Inf or NaN
-constexpr int SKIP = 0x40000000;              // scale of an Inf / NaN row or column
 
 struct GemmF16Args {
   const float *A, *B;
@@ -90,38 +92,6 @@ __device__ __forceinline__ int swz(int r, int c) {
 template <int R>
 __device__ __forceinline__ int tswz(int k, int col) {
   return k * (R * 2) + ((((col >> 3) ^ ((k & 3) << 2))) << 4) + ((col & 7) << 1);
-}
-
-// the scale exponent s for a row whose largest |x| has the bit pattern mb:
-// max |x| * 2^s in [2^14, 2^15)
-__device__ __forceinline__ int scale_exp(uint32_t mb) {
-  if (mb >= NONFINITE) return SKIP;
-  if (mb == 0) return 0;
-  const int e = mb >= 0x00800000u ? (int)(mb >> 23) - 127
-                                  : (31 - (int)__builtin_clz(mb)) - 149;  // subnormal
-  return 14 - e;
-}
-
-// a - (float)f16 half of h, in one v_fma_mix_f32 (a * 1.0 - h, exact here:
-// h is a's f16 rounding, so the difference is an fp32 number)
-__device__ __forceinline__ float sub_h0(float a, uint32_t h) {
-  float r;
-  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(r) : "v"(a), "v"(h));
-  return r;
-}
-__device__ __forceinline__ float sub_h1(float a, uint32_t h) {
-  float r;
-  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r)
-      : "v"(a), "v"(h));
-  return r;
-}
-// (x0 * 2^e0, x1 * 2^e1) -> packed f16 pairs hi, lo: 6 VALU
-__device__ __forceinline__ void split2h(float x0, float x1, int e0, int e1, uint32_t &h,
-                                        uint32_t &l) {
-  const float a = __builtin_amdgcn_ldexpf(x0, e0), b = __builtin_amdgcn_ldexpf(x1, e1);
-  h = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, f16x2));
-  l = __builtin_bit_cast(uint32_t,
-                         __builtin_convertvector((f32x2){sub_h0(a, h), sub_h1(b, h)}, f16x2));
 }
 
 // Operand tile loaders (R rows of C's side x BK per K step), loads two steps
@@ -334,9 +304,6 @@ struct Loader {
   }
 };
 
-__device__ __forceinline__ f32x16 mfma(const f16x8 &a, const f16x8 &b, const f32x16 &c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-}
 
 // The scale exponents of the tile's rows and columns into sexp; true (for
 // the whole block) when one of them is an Inf / NaN row or column

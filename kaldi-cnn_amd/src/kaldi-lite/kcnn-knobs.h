@@ -1,14 +1,14 @@
 // kaldi-lite/kcnn-knobs.h -- run-time switches of libkcnn.so.
 //
-// Kernel-family selectors are product settings: each picks between two
-// implementations of the same math (bf16x6 on the bf16 matrix cores, or the
-// fp32-input MFMA kernels), is documented in DESIGN.md §3 and is covered by
+// Kernel-family selectors are product settings: each picks between
+// implementations of the same math (f16x3 / bf16x6 on the f16 / bf16 matrix
+// cores, or the fp32-input MFMA kernels), is documented in DESIGN.md §3 and is covered by
 // tests/test_gpu_families.py.  They are set through the C-ABI
 // (kcnn_set_kernel_family) or, once when the library loads, by the
 // environment variable named in the table below.
 //
 //   family     env              values
-//   fwd_x6     KCNN_FWD_X6      1 bf16x6 frame-resident forward, 0 fp32 MFMA
+//   fwd_x6     KCNN_FWD_X6      2 f16x3 frame-resident forward, 1 bf16x6, 0 fp32 MFMA
 //   bwd_x6     KCNN_BWD_X6      1 bf16x6 fused backward, 0 fp32 MFMA
 //   igemm_x6   KCNN_IGEMM_X6    1 bf16x6 implicit GEMM, 0 fp32 MFMA
 //   wgrad_x6   KCNN_WGRAD_X6    2 wide bf16x6, 1 128-wide bf16x6, 0 fp32 MFMA

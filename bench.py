@@ -653,19 +653,23 @@ def main():
                              "hbm_frac": round(byts / ms / 1e6 / PEAK_HBM_GBS, 4),
                              "TFLOP/s": round(flop / ms / 1e9, 2) if flop else None,
                              "mfma_frac": round(flop / ms / 1e9 / PEAK_FP32_MFMA_TFLOPS, 4) if flop else None}
-    gemm_x6 = os.environ.get("KCNN_GEMM", "1") != "0"
+    gemm_mode = kcnn.get_kernel_family("gemm")
     if k_fc[1]:
-        # FullyConnectedComponent's three GEMMs (CuMatrixBase::AddMatMat):
-        # the in-house bf16x6 kernel (kaldi-lite/cu-gemm-x6.hip) by default,
-        # rocBLAS sgemm with KCNN_GEMM=0
+        # FullyConnectedComponent's three GEMMs (CuMatrixBase::AddMatMat): the
+        # in-house f16x3 kernel (kaldi-lite/cu-gemm-f16x3.hip, 3 f16 products
+        # per fp32 product) by default, bf16x6 (cu-gemm-x6.hip, 6 bf16
+        # products) with KCNN_GEMM=1, rocBLAS sgemm with KCNN_GEMM=0
         fc_tf = FC_FLOP * B / (k_fc[0] / args.steps) / 1e9
+        nprod = {2: 3, 1: 6}.get(gemm_mode)
         kernels["fc_gemms"] = {
-            "engine": "bf16x6 (cu-gemm-x6.hip)" if gemm_x6 else "rocBLAS sgemm",
+            "engine": {2: "f16x3 (cu-gemm-f16x3.hip)", 1: "bf16x6 (cu-gemm-x6.hip)"}.get(
+                gemm_mode, "rocBLAS sgemm"),
             "ms_per_step": round(k_fc[0] / args.steps, 4),
             "TFLOP/s": round(fc_tf, 2),
             "mfma_frac": round(fc_tf / PEAK_FP32_MFMA_TFLOPS, 4),
-            # six bf16 products per fp32 product: the share of the bf16 engine
-            "frac_of_bf16_peak": round(6 * fc_tf / PEAK_BF16_MFMA_TFLOPS, 4) if gemm_x6
+            # split products per fp32 product: the share of the f16 / bf16
+            # engine (same dense peak) they occupy
+            "frac_of_bf16_peak": round(nprod * fc_tf / PEAK_BF16_MFMA_TFLOPS, 4) if nprod
             else None}
 
     # Dominant hand-written hot-path kernel by time.

@@ -58,9 +58,17 @@ struct kcnn_nnet {
   // below consumes the pool's out_deriv and mask directly; materialised by
   // kcnn_nnet_input_deriv on request, or when that conv's pass declines
   std::vector<char> deriv_deferred;
+  // fwd[i]'s max |value| per row and per column from the fused forward that
+  // wrote it (pool-stats.h; fstat_valid[i]), offered to the next component's
+  // GEMMs (CuGemmStatsHint) for the minibatch of the last Propagate
+  std::vector<uint32_t *> fstat;
+  std::vector<size_t> fstat_words;
+  std::vector<char> fstat_valid;
   ~kcnn_nnet() {
     for (auto *m : mask)
       if (m) CuDevice::Instantiate().Free(m);
+    for (auto *f : fstat)
+      if (f) CuDevice::Instantiate().Free(f);
     for (auto *c : comps) delete c;
   }
 };
@@ -644,6 +652,9 @@ kcnn_nnet *kcnn_nnet_new(const char *config) {
     n->mask_bytes.assign(n->comps.size(), 0);
     n->mask_valid.assign(n->comps.size(), 0);
     n->out_stale.assign(n->comps.size() + 1, 0);
+    n->fstat.assign(n->comps.size() + 1, nullptr);
+    n->fstat_words.assign(n->comps.size() + 1, 0);
+    n->fstat_valid.assign(n->comps.size() + 1, 0);
     n->deriv_deferred.assign(n->comps.size(), 0);
   });
   return rc ? nullptr : n.release();
@@ -668,6 +679,15 @@ static void size_output(CuMatrix<BaseFloat> *m, int rows, int cols) {
   if (m->NumRows() != rows || m->NumCols() != cols) m->Resize(rows, cols);
 }
 
+// The statistics of component i's input (fwd[i]) while its Propagate /
+// Backprop runs, when the fused forward that wrote it gave them.
+static std::unique_ptr<CuGemmStatsHint> input_stats(const kcnn_nnet *n, size_t i) {
+  if (i >= n->fstat_valid.size() || !n->fstat_valid[i]) return nullptr;
+  const CuMatrix<BaseFloat> &x = n->fwd[i];
+  return std::unique_ptr<CuGemmStatsHint>(new CuGemmStatsHint(
+      x.Data(), x.NumRows(), x.NumCols(), x.Stride(), n->fstat[i], n->fstat[i] + x.NumRows()));
+}
+
 // Component i (Conv) and i+1 (channel-only Maxpool) in one fused pass;
 // false when the pair does not qualify.
 static bool propagate_pair(kcnn_nnet *n, size_t i) {
@@ -689,9 +709,32 @@ static bool propagate_pair(kcnn_nnet *n, size_t i) {
   size_output(&n->fwd[i + 1], rows, conv->OutputDim());
   size_output(&n->fwd[i + 2], rows, pool->OutputDim());
   const bool store = g_fusion == 2;
+  // room for the pooled output's statistics (rows + columns, kept) and the
+  // kernel's column partials (this call only)
+  PoolStatsOut ps;
+  const size_t pw = mask_bytes == 1 && conv->In_pad_height() == 0 && conv->In_pad_width() == 0
+                        ? kcnn_conv2d_maxpool_stats_words(
+                              rows, conv->In_height(), conv->In_width(), conv->In_channels(),
+                              conv->Kernel_height(), conv->Kernel_width(), conv->Group(),
+                              pool->FusableChannelPool())
+                        : 0;
+  CuScratch part(pw * 4);
+  if (pw) {
+    const size_t need = (size_t)rows + pool->OutputDim();
+    if (n->fstat_words[i + 2] < need) {
+      if (n->fstat[i + 2]) CuDevice::Instantiate().Free(n->fstat[i + 2]);
+      n->fstat[i + 2] = static_cast<uint32_t *>(CuDevice::Instantiate().Malloc(need * 4));
+      n->fstat_words[i + 2] = need;
+    }
+    ps.rowmax = n->fstat[i + 2];
+    ps.colmax = n->fstat[i + 2] + rows;
+    ps.partials = static_cast<uint32_t *>(part.p);
+    ps.partial_words = pw;
+  }
   if (!conv->PropagateMaxpool(n->fwd[i], &n->fwd[i + 1], *pool, &n->fwd[i + 2],
-                              n->mask[i + 1], pool->OutputDim(), store))
+                              n->mask[i + 1], pool->OutputDim(), store, pw ? &ps : nullptr))
     return false;
+  n->fstat_valid[i + 2] = ps.produced;
   n->mask_valid[i + 1] = 1;
   n->out_stale[i + 1] = !store;
   return true;
@@ -725,9 +768,11 @@ int kcnn_nnet_propagate(kcnn_nnet *n, const float *in, MatrixDim in_dim) {
     std::fill(n->mask_valid.begin(), n->mask_valid.end(), 0);
     std::fill(n->out_stale.begin(), n->out_stale.end(), 0);
     std::fill(n->deriv_deferred.begin(), n->deriv_deferred.end(), 0);
+    std::fill(n->fstat_valid.begin(), n->fstat_valid.end(), 0);
     for (size_t i = 0; i < n->comps.size(); i++) {
       if (propagate_pair(n, i) || propagate_relu_pair(n, i)) { i++; continue; }
       ChunkInfo ii = nnet_in_info(n, i), oi = nnet_out_info(n, i);
+      auto hint = input_stats(n, i);
       n->comps[i]->Propagate(ii, oi, n->fwd[i], &n->fwd[i + 1]);
     }
   });
@@ -783,6 +828,7 @@ int kcnn_nnet_backprop_component(kcnn_nnet *n, int i, const float *out_deriv,
     const int nc = (int)n->comps.size();
     KALDI_ASSERT(i >= 0 && i < nc);
     Component *c = n->comps[i];
+    auto hint = input_stats(n, i);
     if (n->out_stale[i + 1]) n->out_stale[i + 1] = 2;
     auto *u = dynamic_cast<UpdatableComponent *>(c);
     CuMatrix<BaseFloat> *dx = &n->deriv[i];

@@ -304,6 +304,29 @@ __device__ __forceinline__ unsigned tie_mask4(float v0, float v1, float v2, floa
   return m;
 }
 
+// The frame's max |pooled| bits: the wave's maximum into prow by atomic max
+// (prow zeroed by the host; four waves per frame)
+__device__ __forceinline__ void frame_row_max(uint32_t *prow, uint32_t v, int lane) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  if (lane == 0) atomicMax(prow, v);
+}
+
+// Column maxima of the pooled output from the forward's per-workgroup
+// partials [nblk][npool]: colmax[c] = max over workgroups (colmax zeroed;
+// blockIdx.y takes a chunk of 32 workgroups' rows, atomic max across chunks)
+constexpr int COLMAX_ROWS = 32;
+__global__ __launch_bounds__(256) void pool_colmax_kernel(const uint32_t *__restrict__ pcol,
+                                                           int nblk, int npool,
+                                                           uint32_t *__restrict__ colmax) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= npool) return;
+  const int b0 = blockIdx.y * COLMAX_ROWS, b1 = min(nblk, b0 + COLMAX_ROWS);
+  uint32_t m = 0;
+  for (int b = b0; b < b1; b++) m = max(m, pcol[(int64_t)b * npool + c]);
+  atomicMax(colmax + c, m);
+}
+
 // RP: the register-pooled form only (out == nullptr, PC 2 or 4, G = 128 and
 // every wave with FT position tiles: c2), without the generic item loop and
 // the LDS epilogue, whose uniform conditions otherwise overflow the SGPRs.
@@ -313,7 +336,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
     const float *__restrict__ K, int ks, const float *__restrict__ bias,
     float *__restrict__ out, int os, int vec_ok, int dbg,
     float *__restrict__ pool, int ps, unsigned char *__restrict__ mask, int ms,
-    PoolWin pw3) {
+    PoolWin pw3, uint32_t *__restrict__ prow, uint32_t *__restrict__ pcol) {
   constexpr bool X6 = AR == 1, F16 = AR == 2, SPL = AR != 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float *T = reinterpret_cast<float *>(smem);                 // [32][P]
@@ -424,6 +447,15 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
 #else
 #define KCNN_TMARK(i)
 #endif
+  // RP: the pooled output's statistics for the FC GEMM that reads it
+  // (cu-gemm-f16x3.hip's operand scales): max |value| bits per frame (prow,
+  // atomic max) and per pooled column over this workgroup's frames, kept in
+  // the LDS slab T (unused by this form; npool = 32 * P words) by ds_max and
+  // stored to the workgroup's row of the partials pcol at the end
+  uint32_t *Tcol = reinterpret_cast<uint32_t *>(T);
+  if constexpr (RP) {
+    for (int e = tid; e < g.G / PC * g.P; e += 256) Tcol[e] = 0;
+  }
   // the next frame's map is prefetched into registers while this one runs
   constexpr int XV = 8;  // CHW <= 2048 (host check)
   float xv[XV];
@@ -565,6 +597,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
         // the pooling of one item's accumulators (F16: y = acc * 2^-(sa +
         // sb(p)) + b first, in one rounding; fp32 items: acc * 1 + -0, i.e.
         // acc itself)
+        uint32_t rowrun = 0;  // RP: max |pooled| bits of this lane in the frame
         auto pool_item = [&](floatx16 &acc, int gb, int t, bool sl) {
           const int p = (wave_q + 4 * t) * 32 + l_f;
           // accumulator r = 4k + i of lane (l, h) is filter 8k + 4h + i at
@@ -628,6 +661,22 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
               }
             }
           }
+          if constexpr (RP) {
+            // lanes past P hold position P - 1's values: their max lands there
+            const int pc = min(p, g.P - 1) + h_f * (4 / PC) * Pq;
+#pragma unroll
+            for (int j = 0; j < NGP; j++) {
+              const uint32_t a = __float_as_uint(mx[j]) & 0x7fffffffu;  // never NaN
+              const int r0 = j * PC;
+              const int U = (gb * 32 + (r0 & 3) + 8 * (r0 >> 2)) / PC;
+              __hip_atomic_fetch_max(Tcol + U * Pq + pc, a, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+              rowrun = max(rowrun, a);
+            }
+            // (pinned per item: left free, the scheduler spreads the items'
+            // statistics and holds 34 more VGPRs)
+            asm volatile("" : "+v"(rowrun));
+          }
 #pragma unroll
           for (int j = 0; j < NGP; j++) {
             if constexpr (PC == 4) {
@@ -661,11 +710,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
           if (slow) {  // uniform: the frame's items in fp32 (rare: Inf, range)
 #pragma unroll 1
             for (int i = 0; i < NI; i++) {
-              if (!valid(i)) continue;
+              if (!RP && !valid(i)) continue;
               const int gb = i / FT, t = i % FT;
               floatx16 a = fwd_item_fp32(g, K, ks, bias, Xs, koff, gb, wave_q + 4 * t, lane_f);
               pool_item(a, gb, t, true);
             }
+            if constexpr (RP) frame_row_max(prow + n, rowrun, lane_f);
             KCNN_TMARK(2)
             continue;  // next frame
           }
@@ -700,6 +750,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
             pool_item(a, i / FT, i % FT, false);
           }
         }
+        if constexpr (RP) frame_row_max(prow + n, rowrun, lane_f);
         KCNN_TMARK(2)
         continue;  // next frame
       }
@@ -869,6 +920,15 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
       KCNN_TMARK(4)
       __syncthreads();
       KCNN_TMARK(5)
+    }
+  }
+  if constexpr (RP) {
+    // this workgroup's row of the column partials
+    __syncthreads();
+    if (pcol) {
+      const int npool = g.G / PC * g.P;
+      uint32_t *dst = pcol + (int64_t)blockIdx.x * npool;
+      for (int e = tid; e < npool; e += 256) dst[e] = Tcol[e];
     }
   }
 #ifdef KCNN_PHASE_TIMING
@@ -1815,7 +1875,7 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
 #define KCNN_FWD_REGS_T(KS_, AR_)                                                       \
   hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, 0, AR_>), dim3(grid), dim3(256), lds, \
                      st, g, X, xs, K, ks, bias, out, os, vec_ok, dbg, nullptr, 0, nullptr, \
-                     0, PoolWin{})
+                     0, PoolWin{}, nullptr, nullptr)
 #define KCNN_FWD_REGS(KS_) KCNN_FWD_REGS_T(KS_, 0)
       static const int dbg = KCNN_KNOB("KCNN_FWD_DEBUG", 0);
       if (ar == 2 && g.Kdim <= 16) KCNN_FWD_REGS_T(1, 2);
@@ -1867,7 +1927,8 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
                              const float *K, int ks, const float *bias,
                              float *out, int os, float *pool, int ps,
                              unsigned char *mask, int ms, int pc,
-                             hipStream_t st, int ph, int pw) {
+                             hipStream_t st, int ph, int pw, PoolStatsOut *stats) {
+  if (stats) stats->produced = 0;
   const bool win3 = ph > 1 || pw > 1;  // 16-bit mask; ms in mask elements
   if (win3) {
     if (pc < 1 || 32 % pc != 0 || ph * pw * pc > 16 || g.oh % ph != 0 || g.ow % pw != 0)
@@ -1888,7 +1949,7 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
       const int rc = kcnn_conv_fwd_frame_pool(gc, X, xs, K + g0, ks, bias ? bias + g0 : nullptr,
                                               out ? out + (int64_t)g0 * g.P : nullptr, os,
                                               pool + pofs, ps,
-                                              mc, ms, pc, st, ph, pw);
+                                              mc, ms, pc, st, ph, pw, nullptr);
       if (rc) return g0 == 0 ? rc : (rc < 0 ? (int)hipErrorLaunchFailure : rc);
     }
     return 0;
@@ -1917,17 +1978,29 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
   // the register-pooled-only form: pooled output only, pc 2 / 4, G = 128
   // and 12 position tiles (each of the 4 waves has 3)
   const int ntile = (g.P + 31) / 32;
-  const bool rp = out == nullptr && (pc == 2 || pc == 4) && !win3 && g.G == 128 &&
-                  ntile > 4 * 2 && ntile <= 4 * 3;
+  const bool rp = out == nullptr && pc == 4 && !win3 && g.G == 128 && ntile > 4 * 2 &&
+                  ntile <= 4 * 3 && ar == 2;
+  // the register-pooled kernel also gives the pooled output's max |value|
+  // bits per frame and per column (stats, when the caller passes room)
+  uint32_t *prow = nullptr, *pcol = nullptr;
+  if (rp && stats && stats->partials &&
+      stats->partial_words >= (size_t)grid * (g.G / pc) * g.P) {
+    prow = stats->rowmax;
+    pcol = stats->partials;
+    hipError_t e = hipMemsetAsync(prow, 0, (size_t)g.R * 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(stats->colmax, 0, (size_t)(g.G / pc) * g.P * 4, st);
+    if (e != hipSuccess) return (int)e;
+  }
 #define KCNN_FWD_POOL_T(KS_, PC_, AR_)                                                      \
   do {                                                                                       \
-    if (rp && (PC_ == 2 || PC_ == 4) && AR_ != 0)                                            \
-      hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_, AR_, (PC_ == 2 || PC_ == 4) && AR_ != 0>), \
+    if (rp && PC_ == 4 && AR_ == 2)                                                          \
+      hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_, AR_, PC_ == 4 && AR_ == 2>),     \
                          dim3(grid), dim3(256), lds, st, g, X, xs, K, ks, bias, out, os,     \
-                         vec_ok, dbg, pool, ps, mask, ms, pw3);                              \
+                         vec_ok, dbg, pool, ps, mask, ms, pw3, prow, pcol);                  \
     else                                                                                     \
       hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_, AR_>), dim3(grid), dim3(256), lds, \
-                         st, g, X, xs, K, ks, bias, out, os, vec_ok, dbg, pool, ps, mask, ms, pw3); \
+                         st, g, X, xs, K, ks, bias, out, os, vec_ok, dbg, pool, ps, mask, ms, pw3, \
+                         nullptr, nullptr);                                                  \
   } while (0)
 #define KCNN_FWD_POOL(KS_, PC_) KCNN_FWD_POOL_T(KS_, PC_, 0)
 #define KCNN_FWD_POOL_KS(PC_)                     \
@@ -1950,7 +2023,19 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
 #undef KCNN_FWD_POOL_KS
 #undef KCNN_FWD_POOL
 #undef KCNN_FWD_POOL_T
+  if (pcol) {
+    const int npool = g.G / pc * g.P;
+    hipLaunchKernelGGL(pool_colmax_kernel,
+                       dim3((npool + 255) / 256, (grid + COLMAX_ROWS - 1) / COLMAX_ROWS),
+                       dim3(256), 0, st, pcol, (int)grid, npool, stats->colmax);
+    stats->produced = 1;
+  }
   return (int)hipGetLastError();
+}
+
+size_t kcnn_pool_stats_partial_words(const ConvGeom &g, int pc) {
+  // frame_grid(g, 2) workgroups (the x6 / f16x3 register kernel) x pooled columns
+  return pc > 0 ? (size_t)frame_grid(g, 2) * (g.G / pc) * g.P : 0;
 }
 
 int kcnn_conv_dgrad_frame(const ConvGeom &g, const float *dY, int dys,

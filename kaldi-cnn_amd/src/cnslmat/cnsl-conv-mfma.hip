@@ -1010,6 +1010,34 @@ int hipF_conv2d_maxpool(const float *in, MatrixDim in_dim, int in_height,
                         float *pool, MatrixDim pool_dim, unsigned char *mask,
                         int mask_stride, int pool_channel_dim,
                         kcnn_stream_t stream) {
+  return kcnn_conv2d_maxpool_stats(in, in_dim, in_height, in_width, in_channel, pad_h, pad_w,
+                                   kernel, kernel_dim, kernel_height, kernel_width, group,
+                                   bias, out, out_dim, pool, pool_dim, mask, mask_stride,
+                                   pool_channel_dim, stream, nullptr);
+}
+
+// The scratch words for the pooled output's statistics (pool-stats.h) of
+// hipF_conv2d_maxpool's geometry; 0 when the layer takes no frame kernel.
+size_t kcnn_conv2d_maxpool_stats_words(int rows, int in_height, int in_width,
+                                       int in_channel, int kernel_height, int kernel_width,
+                                       int group, int pool_channel_dim) {
+  ConvGeom g = make_geom(rows, in_height, in_width, in_channel, 0, 0, kernel_height,
+                         kernel_width, group);
+  if (g.oh <= 0 || g.ow <= 0 || pool_channel_dim <= 0) return 0;
+  return kcnn_pool_stats_partial_words(g, pool_channel_dim);
+}
+
+// hipF_conv2d_maxpool plus the pooled output's statistics when its kernel
+// gives them (stats nullable; stats->produced tells)
+int kcnn_conv2d_maxpool_stats(const float *in, MatrixDim in_dim, int in_height,
+                              int in_width, int in_channel, int pad_h, int pad_w,
+                              const float *kernel, MatrixDim kernel_dim,
+                              int kernel_height, int kernel_width, int group,
+                              const float *bias, float *out, MatrixDim out_dim,
+                              float *pool, MatrixDim pool_dim, unsigned char *mask,
+                              int mask_stride, int pool_channel_dim,
+                              kcnn_stream_t stream, PoolStatsOut *stats) {
+  if (stats) stats->produced = 0;
   ConvGeom g = make_geom(in_dim.rows, in_height, in_width, in_channel, pad_h,
                          pad_w, kernel_height, kernel_width, group);
   if (g.oh <= 0 || g.ow <= 0 || in_dim.cols != g.HW * in_channel ||
@@ -1024,7 +1052,7 @@ int hipF_conv2d_maxpool(const float *in, MatrixDim in_dim, int in_height,
   return kcnn_conv_fwd_frame_pool(g, in, in_dim.stride, kernel, kernel_dim.stride,
                                   bias, out, out_dim.stride, pool, pool_dim.stride,
                                   mask, mask_stride, pool_channel_dim,
-                                  kcnn::as_stream(stream)) == 0 ? 0 : -1;
+                                  kcnn::as_stream(stream), 1, 1, stats) == 0 ? 0 : -1;
 }
 
 int hipF_conv2d_maxpool3d(const float *in, MatrixDim in_dim, int in_height,

@@ -3,6 +3,7 @@
 #define KCNN_CNSLMAT_CONV_GEOM_H_
 
 #include "hip-util.h"
+#include "pool-stats.h"
 
 namespace kcnn {
 
@@ -51,11 +52,14 @@ __device__ __forceinline__ int mfma32_row(int r, int lane) {
 int kcnn_conv_fwd_frame(const kcnn::ConvGeom &g, const float *X, int xs,
                         const float *K, int ks, const float *bias, float *out,
                         int os, hipStream_t st);
+// the pooled output's statistics: pool-stats.h
+size_t kcnn_pool_stats_partial_words(const kcnn::ConvGeom &g, int pc);
 int kcnn_conv_fwd_frame_pool(const kcnn::ConvGeom &g, const float *X, int xs,
                              const float *K, int ks, const float *bias,
                              float *out, int os, float *pool, int ps,
                              unsigned char *mask, int ms, int pc,
-                             hipStream_t st, int ph = 1, int pw = 1);
+                             hipStream_t st, int ph = 1, int pw = 1,
+                             PoolStatsOut *stats = nullptr);
 int kcnn_conv_dgrad_frame(const kcnn::ConvGeom &g, const float *dY, int dys,
                           const float *K, int ks, float *dX, int dxs,
                           hipStream_t st);

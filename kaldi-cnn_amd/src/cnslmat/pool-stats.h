@@ -1,0 +1,42 @@
+// cnslmat/pool-stats.h -- the pooled output's operand statistics from the
+// fused conv + pool forward.
+//
+// The register-pooled frame forward (cnsl-conv-frame.hip) writes, besides the
+// pooled output and its routing mask, the max |value| bit patterns of the
+// pooled output per frame (rowmax[R]) and per pooled column (colmax[npool],
+// through partial_words of scratch: kcnn_pool_stats_partial_words).  The FC
+// GEMMs that read the pooled output take them as its f16x3 operand scales
+// (kaldi-lite/cu-gemm-f16x3.hip via CuGemmStatsHint) instead of reading it
+// once more.  produced = 1 when the launch wrote them.
+#ifndef KCNN_CNSLMAT_POOL_STATS_H_
+#define KCNN_CNSLMAT_POOL_STATS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "cnsl-hip-kernels.h"  // MatrixDim, kcnn_stream_t
+
+struct PoolStatsOut {
+  uint32_t *rowmax = nullptr, *colmax = nullptr, *partials = nullptr;
+  size_t partial_words = 0;
+  int produced = 0;
+};
+
+// hipF_conv2d_maxpool (include/cnsl-hip-kernels.h) plus the statistics when
+// its kernel gives them (stats nullable), and the scratch words they need
+// (0: the layer has no frame kernel)
+extern "C" {
+int kcnn_conv2d_maxpool_stats(const float *in, MatrixDim in_dim, int in_height,
+                              int in_width, int in_channel, int pad_h, int pad_w,
+                              const float *kernel, MatrixDim kernel_dim,
+                              int kernel_height, int kernel_width, int group,
+                              const float *bias, float *out, MatrixDim out_dim,
+                              float *pool, MatrixDim pool_dim, unsigned char *mask,
+                              int mask_stride, int pool_channel_dim,
+                              kcnn_stream_t stream, PoolStatsOut *stats);
+size_t kcnn_conv2d_maxpool_stats_words(int rows, int in_height, int in_width,
+                                       int in_channel, int kernel_height, int kernel_width,
+                                       int group, int pool_channel_dim);
+}
+
+#endif  // KCNN_CNSLMAT_POOL_STATS_H_

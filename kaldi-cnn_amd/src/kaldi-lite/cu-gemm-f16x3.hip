@@ -1046,6 +1046,16 @@ extern "C" int kl_gemm_f16x3(int transA, int transB, int M, int N, int K, float 
                              const float *A, int lda, const float *B, int ldb, float beta,
                              float *C, int ldc, void *ws, size_t ws_bytes,
                              kcnn_stream_t stream) {
+  return kl_gemm_f16x3_given(transA, transB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc,
+                             nullptr, nullptr, ws, ws_bytes, stream);
+}
+// ... with either operand's statistics supplied by its producer (nullable):
+// only the missing ones are computed (one read of that operand)
+extern "C" int kl_gemm_f16x3_given(int transA, int transB, int M, int N, int K, float alpha,
+                                   const float *A, int lda, const float *B, int ldb, float beta,
+                                   float *C, int ldc, const uint32_t *amax_given,
+                                   const uint32_t *bmax_given, void *ws, size_t ws_bytes,
+                                   kcnn_stream_t stream) {
   if (M < 0 || N < 0 || K < 0) return (int)hipErrorInvalidValue;
   if (M == 0 || N == 0 || K == 0) return (int)hipErrorNotSupported;
   const size_t pb = partial_bytes(M, N, K);
@@ -1055,12 +1065,18 @@ extern "C" int kl_gemm_f16x3(int transA, int transB, int M, int N, int K, float 
   uint32_t *bmax = amax + M;
   uint32_t *parta = bmax + N + 4;
   uint32_t *partb = parta + (transA ? stat_part_words(K, M, 1) : 0);
-  const StatOp sa = transA ? stat_op(A, K, M, lda, 1, amax, parta)
-                           : stat_op(A, M, K, lda, 0, amax, nullptr);
-  const StatOp sb = transB ? stat_op(B, N, K, ldb, 0, bmax, nullptr)
-                           : stat_op(B, K, N, ldb, 1, bmax, partb);
-  const int rc = stats_launch(sa, sb, kcnn::as_stream(stream));
-  if (rc) return rc;
-  return kl_gemm_f16x3_st(transA, transB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, amax,
-                          bmax, pb ? ws : nullptr, pb, stream);
+  const StatOp sa = amax_given ? StatOp{}
+                    : transA   ? stat_op(A, K, M, lda, 1, amax, parta)
+                               : stat_op(A, M, K, lda, 0, amax, nullptr);
+  const StatOp sb = bmax_given ? StatOp{}
+                    : transB   ? stat_op(B, N, K, ldb, 0, bmax, nullptr)
+                               : stat_op(B, K, N, ldb, 1, bmax, partb);
+  if (!amax_given || !bmax_given) {
+    const int rc = amax_given ? stats_launch(sb, StatOp{}, kcnn::as_stream(stream))
+                              : stats_launch(sa, sb, kcnn::as_stream(stream));
+    if (rc) return rc;
+  }
+  return kl_gemm_f16x3_st(transA, transB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc,
+                          amax_given ? amax_given : amax, bmax_given ? bmax_given : bmax,
+                          pb ? ws : nullptr, pb, stream);
 }

@@ -49,6 +49,12 @@ size_t kl_gemm_f16x3_full_workspace_bytes(int M, int N, int K);
 int kl_gemm_f16x3(int transA, int transB, int M, int N, int K, float alpha,
                   const float *A, int lda, const float *B, int ldb, float beta, float *C,
                   int ldc, void *ws, size_t ws_bytes, kcnn_stream_t st);
+/* kl_gemm_f16x3 with op(A)'s row and/or op(B)'s column statistics supplied
+   (nullable; e.g. from the fused conv + pool forward that wrote the operand) */
+int kl_gemm_f16x3_given(int transA, int transB, int M, int N, int K, float alpha,
+                        const float *A, int lda, const float *B, int ldb, float beta, float *C,
+                        int ldc, const uint32_t *amax, const uint32_t *bmax, void *ws,
+                        size_t ws_bytes, kcnn_stream_t st);
 /* the same product from operands already split into bf16 planes h, m, l
    (plane p of X at X + p * ps elements); kl_split_planes makes them */
 int kl_split_planes(const float *src, int rows, int cols, int ld, uint16_t *dst, int ldp,

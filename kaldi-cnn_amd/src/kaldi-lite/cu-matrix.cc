@@ -254,6 +254,24 @@ void CuMatrixBase<Real>::AddMat(Real alpha, const CuMatrixBase<Real> &A,
                             data_, Dim(), S()));
 }
 
+static thread_local const CuGemmStatsHint *g_stats_hints = nullptr;
+
+CuGemmStatsHint::CuGemmStatsHint(const float *data, MatrixIndexT rows, MatrixIndexT cols,
+                                 MatrixIndexT stride, const uint32_t *rmax,
+                                 const uint32_t *cmax)
+    : rowmax(rmax), colmax(cmax), data_(data), rows_(rows), cols_(cols), stride_(stride),
+      prev_(g_stats_hints) {
+  g_stats_hints = this;
+}
+CuGemmStatsHint::~CuGemmStatsHint() { g_stats_hints = prev_; }
+const CuGemmStatsHint *CuGemmStatsHint::Find(const float *data, MatrixIndexT rows,
+                                             MatrixIndexT cols, MatrixIndexT stride) {
+  for (const CuGemmStatsHint *h = g_stats_hints; h; h = h->prev_)
+    if (h->data_ == data && h->rows_ == rows && h->cols_ == cols && h->stride_ == stride)
+      return h;
+  return nullptr;
+}
+
 template <typename Real>
 void CuMatrixBase<Real>::AddMatMat(Real alpha, const CuMatrixBase<Real> &A,
                                    MatrixTransposeType transA,
@@ -284,11 +302,19 @@ void CuMatrixBase<Real>::AddMatMat(Real alpha, const CuMatrixBase<Real> &A,
     if (transA == kNoTrans && !aligned(A)) { Acopy = A; Ap = &Acopy; }
     if (transB == kTrans && !aligned(B)) { Bcopy = B; Bp = &Bcopy; }
     if (mode == 2) {
+      // op(A)'s row / op(B)'s column statistics from their producer, if any
+      // (CuGemmStatsHint: e.g. the fused conv + pool forward's pooled output)
+      const CuGemmStatsHint *ha = CuGemmStatsHint::Find(A.Data(), A.NumRows(), A.NumCols(),
+                                                        A.Stride());
+      const CuGemmStatsHint *hb = CuGemmStatsHint::Find(B.Data(), B.NumRows(), B.NumCols(),
+                                                        B.Stride());
+      const uint32_t *ag = ha ? (transA == kNoTrans ? ha->rowmax : ha->colmax) : nullptr;
+      const uint32_t *bg = hb ? (transB == kNoTrans ? hb->colmax : hb->rowmax) : nullptr;
       const size_t wsf = kl_gemm_f16x3_full_workspace_bytes(m, n, k);
       void *wf = dev0.Malloc(wsf);
-      const int rc = kl_gemm_f16x3(transA == kTrans, transB == kTrans, m, n, k, alpha,
-                                   Ap->Data(), Ap->Stride(), Bp->Data(), Bp->Stride(), beta,
-                                   data_, stride_, wf, wsf, S());
+      const int rc = kl_gemm_f16x3_given(transA == kTrans, transB == kTrans, m, n, k, alpha,
+                                         Ap->Data(), Ap->Stride(), Bp->Data(), Bp->Stride(),
+                                         beta, data_, stride_, ag, bg, wf, wsf, S());
       dev0.Free(wf);
       // past the f16x3 kernel's 32-bit addressing the bf16x6 kernel (same
       // error bound) takes the product

@@ -294,6 +294,30 @@ Real TraceMatMat(const CuMatrixBase<Real> &A, const CuMatrixBase<Real> &B,
 template <typename Real>
 Real VecVec(const CuVectorBase<Real> &a, const CuVectorBase<Real> &b);
 
+/// Statistics a producer computed for a matrix's contents -- max |x| bit
+/// patterns per row and per column (device arrays, either nullable) -- offered
+/// to AddMatMat while the object is in scope on this thread.  AddMatMat's
+/// f16x3 engine scales each operand row / column by them
+/// (kaldi-lite/cu-gemm-f16x3.hip) and would otherwise read the operand once
+/// more to compute them.  The owner keeps the matrix unmodified in scope.
+class CuGemmStatsHint {
+ public:
+  CuGemmStatsHint(const float *data, MatrixIndexT rows, MatrixIndexT cols, MatrixIndexT stride,
+                  const uint32_t *rowmax, const uint32_t *colmax);
+  ~CuGemmStatsHint();
+  CuGemmStatsHint(const CuGemmStatsHint &) = delete;
+  CuGemmStatsHint &operator=(const CuGemmStatsHint &) = delete;
+  /// the innermost hint for exactly this matrix, or NULL
+  static const CuGemmStatsHint *Find(const float *data, MatrixIndexT rows, MatrixIndexT cols,
+                                     MatrixIndexT stride);
+  const uint32_t *rowmax, *colmax;
+
+ private:
+  const float *data_;
+  MatrixIndexT rows_, cols_, stride_;
+  const CuGemmStatsHint *prev_;
+};
+
 /// Host N(0,1) generator shared by SetRandn (splitmix64 -> Box-Muller).
 void RandnFill(float *dst, size_t n);
 void SetRandnSeed(uint64_t seed);

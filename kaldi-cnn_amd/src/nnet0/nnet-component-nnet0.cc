@@ -218,7 +218,8 @@ bool ConvolutionComponent::PropagateMaxpool(const CuMatrixBase<BaseFloat> &in,
                                             const MaxpoolComponent &pool,
                                             CuMatrixBase<BaseFloat> *pool_out,
                                             unsigned char *mask,
-                                            int32 mask_stride, bool store_out) const {
+                                            int32 mask_stride, bool store_out,
+                                            PoolStatsOut *pool_stats) const {
   const int32 pc = pool.FusableChannelPool();
   int32 ph = 1, pw = 1, pc3 = 0;
   const bool win3 = pc == 0 && pool.FusableWindow3D(&ph, &pw, &pc3);
@@ -238,11 +239,12 @@ bool ConvolutionComponent::PropagateMaxpool(const CuMatrixBase<BaseFloat> &in,
                  kernel_width_, group_, bias_params_.Data(), store_out ? out->Data() : NULL,
                  out->Dim(), pool_out->Data(), pool_out->Dim(), reinterpret_cast<unsigned short *>(mask),
                  mask_stride, ph, pw, pc3, S())
-           : hipF_conv2d_maxpool(
+           : kcnn_conv2d_maxpool_stats(
                  in.Data(), in.Dim(), in_height_, in_width_, in_channel_, in_pad_height_,
                  in_pad_width_, linear_params_.Data(), linear_params_.Dim(), kernel_height_,
                  kernel_width_, group_, bias_params_.Data(), store_out ? out->Data() : NULL,
-                 out->Dim(), pool_out->Data(), pool_out->Dim(), mask, mask_stride, pc, S());
+                 out->Dim(), pool_out->Data(), pool_out->Dim(), mask, mask_stride, pc, S(),
+                 pool_stats);
   if (rc < 0) {
     prof.Cancel();  // declined: nothing launched
     return false;

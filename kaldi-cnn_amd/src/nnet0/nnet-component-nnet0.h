@@ -19,6 +19,7 @@
 #include <iostream>
 #include <string>
 
+#include "../cnslmat/pool-stats.h"
 #include "../kaldi-lite/cu-matrix.h"
 #include "../nnet2/nnet-component.h"
 
@@ -60,6 +61,8 @@ class ConvolutionComponent : public nnet2::UpdatableComponent {
   inline int32 Out_height() const { return out_height_; }
   inline int32 Out_width() const { return out_width_; }
   inline int32 Group() const { return group_; }
+  inline int32 In_pad_height() const { return in_pad_height_; }
+  inline int32 In_pad_width() const { return in_pad_width_; }
   inline int32 KernelDim() const { return kernel_height_ * kernel_width_ * in_channel_; }
   inline int32 Kernel_height() const { return kernel_height_; }
   inline int32 Kernel_width() const { return kernel_width_; }
@@ -128,11 +131,15 @@ class ConvolutionComponent : public nnet2::UpdatableComponent {
   // store_out = false leaves `out` unwritten (sized, contents stale): the
   // pool's backprop from the mask and this component's Backprop never read
   // it, so a training step does not need it in HBM.
+  // pool_stats (nullable, channel-only pools): room for the pooled output's
+  // max |value| per frame and per column (cnslmat/pool-stats.h), filled
+  // (pool_stats->produced) when the kernel gives them.
   bool PropagateMaxpool(const CuMatrixBase<BaseFloat> &in,
                         CuMatrixBase<BaseFloat> *out,
                         const MaxpoolComponent &pool,
                         CuMatrixBase<BaseFloat> *pool_out, unsigned char *mask,
-                        int32 mask_stride, bool store_out = true) const;
+                        int32 mask_stride, bool store_out = true,
+                        PoolStatsOut *pool_stats = NULL) const;
 
   // Propagate and the Propagate of a RectifiedLinearComponent that consumes
   // `out`, in one pass (hipF_conv2d_relu): relu_out = max(out, 0), `out`

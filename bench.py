@@ -152,6 +152,8 @@ KERNEL_SOURCES = {
     "maxpool_direct_prop_kernel": "kaldi-cnn_amd/src/cnslmat/cnsl-hip-kernels.hip",
     "maxpool_direct_backprop_kernel": "kaldi-cnn_amd/src/cnslmat/cnsl-hip-kernels.hip",
     "gemm_f16x3_kernel": "kaldi-cnn_amd/src/kaldi-lite/cu-gemm-f16x3.hip",
+    "gemm_f16x3_fast_kernel": "kaldi-cnn_amd/src/kaldi-lite/cu-gemm-f16x3.hip",
+    "pool_colmax_kernel": "kaldi-cnn_amd/src/cnslmat/cnsl-conv-frame.hip",
 }
 
 

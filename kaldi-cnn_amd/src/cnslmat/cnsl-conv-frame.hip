@@ -313,18 +313,22 @@ __device__ __forceinline__ void frame_row_max(uint32_t *prow, uint32_t v, int la
 }
 
 // Column maxima of the pooled output from the forward's per-workgroup
-// partials [nblk][npool]: colmax[c] = max over workgroups (colmax zeroed;
-// blockIdx.y takes a chunk of 32 workgroups' rows, atomic max across chunks)
+// partials [nblk][npool], one exponent byte each (the |x| bits >> 23: the
+// GEMM's scale needs only the binade).  colmax[c] = the largest partial's
+// binade with every mantissa bit set, an upper bound in the max's binade (so
+// the same scale; 0x7f... for Inf; an all-zero column gets the subnormal
+// bound, harmless).  colmax zeroed; blockIdx.y takes 32 workgroups' rows,
+// atomic max across those chunks.
 constexpr int COLMAX_ROWS = 32;
-__global__ __launch_bounds__(256) void pool_colmax_kernel(const uint32_t *__restrict__ pcol,
+__global__ __launch_bounds__(256) void pool_colmax_kernel(const uint8_t *__restrict__ pcol,
                                                            int nblk, int npool,
                                                            uint32_t *__restrict__ colmax) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= npool) return;
   const int b0 = blockIdx.y * COLMAX_ROWS, b1 = min(nblk, b0 + COLMAX_ROWS);
   uint32_t m = 0;
-  for (int b = b0; b < b1; b++) m = max(m, pcol[(int64_t)b * npool + c]);
-  atomicMax(colmax + c, m);
+  for (int b = b0; b < b1; b++) m = max(m, (uint32_t)pcol[(int64_t)b * npool + c]);
+  atomicMax(colmax + c, (m << 23) | 0x7fffffu);
 }
 
 // RP: the register-pooled form only (out == nullptr, PC 2 or 4, G = 128 and
@@ -925,10 +929,17 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
   if constexpr (RP) {
     // this workgroup's row of the column partials
     __syncthreads();
-    if (pcol) {
+    if (pcol) {  // exponent bytes (pool_colmax_kernel), four per dword store
       const int npool = g.G / PC * g.P;
-      uint32_t *dst = pcol + (int64_t)blockIdx.x * npool;
-      for (int e = tid; e < npool; e += 256) dst[e] = Tcol[e];
+      uint8_t *dst = reinterpret_cast<uint8_t *>(pcol) + (int64_t)blockIdx.x * npool;
+      if (npool % 4 == 0) {
+        for (int e = 4 * tid; e < npool; e += 1024)
+          *reinterpret_cast<uint32_t *>(dst + e) =
+              (Tcol[e] >> 23) | (Tcol[e + 1] >> 23) << 8 | (Tcol[e + 2] >> 23) << 16 |
+              (Tcol[e + 3] >> 23) << 24;
+      } else {
+        for (int e = tid; e < npool; e += 256) dst[e] = (uint8_t)(Tcol[e] >> 23);
+      }
     }
   }
 #ifdef KCNN_PHASE_TIMING
@@ -1984,7 +1995,7 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
   // bits per frame and per column (stats, when the caller passes room)
   uint32_t *prow = nullptr, *pcol = nullptr;
   if (rp && stats && stats->partials &&
-      stats->partial_words >= (size_t)grid * (g.G / pc) * g.P) {
+      stats->partial_words * 4 >= (size_t)grid * (g.G / pc) * g.P) {
     prow = stats->rowmax;
     pcol = stats->partials;
     hipError_t e = hipMemsetAsync(prow, 0, (size_t)g.R * 4, st);
@@ -2027,15 +2038,17 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
     const int npool = g.G / pc * g.P;
     hipLaunchKernelGGL(pool_colmax_kernel,
                        dim3((npool + 255) / 256, (grid + COLMAX_ROWS - 1) / COLMAX_ROWS),
-                       dim3(256), 0, st, pcol, (int)grid, npool, stats->colmax);
+                       dim3(256), 0, st, reinterpret_cast<const uint8_t *>(pcol), (int)grid,
+                       npool, stats->colmax);
     stats->produced = 1;
   }
   return (int)hipGetLastError();
 }
 
 size_t kcnn_pool_stats_partial_words(const ConvGeom &g, int pc) {
-  // frame_grid(g, 2) workgroups (the x6 / f16x3 register kernel) x pooled columns
-  return pc > 0 ? (size_t)frame_grid(g, 2) * (g.G / pc) * g.P : 0;
+  // frame_grid(g, 2) workgroups (the f16x3 register kernel) x pooled columns
+  // exponent bytes
+  return pc > 0 ? ((size_t)frame_grid(g, 2) * (g.G / pc) * g.P + 3) / 4 : 0;
 }
 
 int kcnn_conv_dgrad_frame(const ConvGeom &g, const float *dY, int dys,

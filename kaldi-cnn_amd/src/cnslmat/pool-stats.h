@@ -3,8 +3,10 @@
 //
 // The register-pooled frame forward (cnsl-conv-frame.hip) writes, besides the
 // pooled output and its routing mask, the max |value| bit patterns of the
-// pooled output per frame (rowmax[R]) and per pooled column (colmax[npool],
-// through partial_words of scratch: kcnn_pool_stats_partial_words).  The FC
+// pooled output per frame (rowmax[R], exact) and per pooled column
+// (colmax[npool]: the max's binade with every mantissa bit set, which is all
+// the GEMM's power-of-two scale reads; through partial_words of scratch:
+// kcnn_pool_stats_partial_words).  The FC
 // GEMMs that read the pooled output take them as its f16x3 operand scales
 // (kaldi-lite/cu-gemm-f16x3.hip via CuGemmStatsHint) instead of reading it
 // once more.  produced = 1 when the launch wrote them.

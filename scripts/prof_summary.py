@@ -32,7 +32,7 @@ HOT = [
     (r"conv_bwd_dma_kernel<\d+, \w+, \w+, [48]>", "conv_bwd_pooled"),
     (r"conv_bwd_dma_kernel", "conv_bwd_fused"),
     (r"conv_bwd_frame_kernel", "conv_bwd_fused"),
-    (r"conv_fwd_regs_kernel<\d+, \d+, [248](, \w+)?>", "conv_fwd_maxpool"),
+    (r"conv_fwd_regs_kernel<\d+, \d+, [248](, \w+)*>", "conv_fwd_maxpool"),
     (r"conv_fwd_regs_kernel", "conv_fwd"),
     (r"conv_fwd_slab_kernel", "conv_fwd"),
     (r"conv_fwd_frame_kernel", "conv_fwd"),

@@ -435,6 +435,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--frames-per-gpu", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="one GPU: capture the step once as a HIP graph and replay it "
+                         "(measured slower than host-issued steps at c2: 2.75-2.80 M vs "
+                         "2.86 M frames/s; c5 1.6 % faster)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--no-fusion", action="store_true",
                     help="run Conv and Maxpool as separate components")
@@ -515,6 +519,28 @@ def main():
     for _ in range(args.warmup):
         step()
 
+    # --graph, one GPU: the step captured once as a HIP graph and replayed
+    # (the same kernels with the same arguments; the caching allocator's
+    # blocks are warm, so the capture allocates nothing).  Data-parallel steps
+    # (RCCL inside) and a failed capture run the step eagerly.
+    graph = None
+    if not dist and args.graph:
+        try:
+            gs = torch.cuda.Stream()
+            gs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(gs):
+                kcnn.sync_stream()
+                step()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=gs, capture_error_mode="relaxed"):
+                step()
+            g.replay()
+            torch.cuda.synchronize()
+            graph = g
+        except Exception as e:  # noqa: BLE001 -- reported, eager fallback
+            print(f"bench: HIP graph capture failed ({e!r}); eager steps", file=sys.stderr)
+        kcnn.sync_stream()  # back to the current stream
+
     def timed(profiled):
         """K steps between barriers + device syncs; max over ranks."""
         kcnn.set_profiling(profiled)
@@ -525,7 +551,10 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            step()
+            if graph is not None and not profiled:
+                graph.replay()
+            else:
+                step()
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
@@ -574,6 +603,7 @@ def main():
                 "scaling": "weak", "vs_baseline": None, "dtype": "f32",
                 "data": "synthetic N(0,1) frames",
                 "profiled_ms_per_step": round(elapsed_prof / args.steps * 1e3, 4),
+                "hip_graph": graph is not None,
                 "config": {"workload": workload, "frames_per_gpu": B,
                            "parallelism": f"dp{world}"},
                 "conv": {"ms_per_step": round(conv_ms, 4),
@@ -727,6 +757,7 @@ def main():
             # the second pass of K steps with hipEvents around each scope
             # (kernel times below come from it)
             "profiled_ms_per_step": round(elapsed_prof / args.steps * 1e3, 4),
+            "hip_graph": graph is not None,
             "config": {"workload": "c2: Conv(40x11x3, 8x1, 128) -> Maxpool(1x1x4) -> "
                                    "FC(11616->1024), fwd+bwd+update",
                        "baseline_config": baseline_config(B, world),

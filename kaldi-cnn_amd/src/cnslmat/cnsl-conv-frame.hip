@@ -304,12 +304,19 @@ __device__ __forceinline__ unsigned tie_mask4(float v0, float v1, float v2, floa
   return m;
 }
 
-// The frame's max |pooled| bits: the wave's maximum into prow by atomic max
-// (prow zeroed by the host; four waves per frame)
-__device__ __forceinline__ void frame_row_max(uint32_t *prow, uint32_t v, int lane) {
+// The register-pooled forward's statistics outputs (pool-stats.h): rowmax
+// per frame, the per-workgroup column partials (exponent bytes) and the
+// column maxima that pool_colmax_kernel fills (zeroed here first)
+struct RpStats {
+  uint32_t *rowmax = nullptr, *partials = nullptr, *colmax = nullptr;
+};
+
+// The wave's max |pooled| bits of the frame into its slot of rslot (LDS; the
+// frame's four slots are combined after the next barrier)
+__device__ __forceinline__ void frame_row_max(uint32_t *rslot, uint32_t v, int lane) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
-  if (lane == 0) atomicMax(prow, v);
+  if (lane == 0) *rslot = v;
 }
 
 // Column maxima of the pooled output from the forward's per-workgroup
@@ -340,7 +347,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
     const float *__restrict__ K, int ks, const float *__restrict__ bias,
     float *__restrict__ out, int os, int vec_ok, int dbg,
     float *__restrict__ pool, int ps, unsigned char *__restrict__ mask, int ms,
-    PoolWin pw3, uint32_t *__restrict__ prow, uint32_t *__restrict__ pcol) {
+    PoolWin pw3, RpStats rps) {
   constexpr bool X6 = AR == 1, F16 = AR == 2, SPL = AR != 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float *T = reinterpret_cast<float *>(smem);                 // [32][P]
@@ -349,6 +356,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
   int2 *koff = reinterpret_cast<int2 *>(Bs + 160);             // [2*KS] taps
   constexpr int NKT = SPL ? 16 * KS : 2 * KS;                   // tap entries (<= 32)
   float *Xs = reinterpret_cast<float *>(koff + NKT);            // [C*HW]
+  uint32_t *rslot = reinterpret_cast<uint32_t *>(Xs + g.C * g.HW);  // [2][4] RP row maxima
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = lane & 31, h = lane >> 5;
@@ -457,8 +465,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
   // the LDS slab T (unused by this form; npool = 32 * P words) by ds_max and
   // stored to the workgroup's row of the partials pcol at the end
   uint32_t *Tcol = reinterpret_cast<uint32_t *>(T);
+  uint32_t *const prow = rps.rowmax, *const pcol = rps.partials;
   if constexpr (RP) {
     for (int e = tid; e < g.G / PC * g.P; e += 256) Tcol[e] = 0;
+    // pool_colmax_kernel's atomic maxima start from 0 (it runs after this grid)
+    const int c = blockIdx.x * 256 + tid;
+    if (rps.colmax && c < g.G / PC * g.P) rps.colmax[c] = 0;
   }
   // the next frame's map is prefetched into registers while this one runs
   constexpr int XV = 8;  // CHW <= 2048 (host check)
@@ -467,7 +479,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
   for (int i = 0; i < XV; i++)
     if (blockIdx.x < (unsigned)g.R && tid + 256 * i < CHW)
       xv[i] = X[(int64_t)blockIdx.x * xs + tid + 256 * i];
-  for (int n = blockIdx.x; n < g.R; n += gridDim.x) {
+  int it = 0;  // this workgroup's frame count
+  for (int n = blockIdx.x; n < g.R; n += gridDim.x, ++it) {
     // lane ids made opaque per frame: the frame-invariant LDS / global
     // addresses are recomputed instead of hoisted out of the loop (hoisted,
     // they overflow the register file)
@@ -477,6 +490,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
     asm volatile("" : "+s"(wave_q));  // constants overflow the SGPRs)
     const int lane_f = tid_f & 63, l_f = lane_f & 31, h_f = lane_f >> 5;
     __syncthreads();  // previous frame's Xs / T reads done
+    if constexpr (RP) {  // the previous frame's row maximum from its four wave slots
+      if (it > 0 && tid_f == 0 && prow) {
+        const uint32_t *q = rslot + ((it - 1) & 1) * 4;
+        prow[n - (int)gridDim.x] = max(max(q[0], q[1]), max(q[2], q[3]));
+      }
+    }
     KCNN_TMARK(5)
 #pragma unroll
     for (int i = 0; i < XV; i++)
@@ -719,7 +738,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
               floatx16 a = fwd_item_fp32(g, K, ks, bias, Xs, koff, gb, wave_q + 4 * t, lane_f);
               pool_item(a, gb, t, true);
             }
-            if constexpr (RP) frame_row_max(prow + n, rowrun, lane_f);
+            if constexpr (RP) frame_row_max(rslot + (it & 1) * 4 + wave_q, rowrun, lane_f);
             KCNN_TMARK(2)
             continue;  // next frame
           }
@@ -754,7 +773,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
             pool_item(a, i / FT, i % FT, false);
           }
         }
-        if constexpr (RP) frame_row_max(prow + n, rowrun, lane_f);
+        if constexpr (RP) frame_row_max(rslot + (it & 1) * 4 + wave_q, rowrun, lane_f);
         KCNN_TMARK(2)
         continue;  // next frame
       }
@@ -927,8 +946,13 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
     }
   }
   if constexpr (RP) {
-    // this workgroup's row of the column partials
+    // this workgroup's row of the column partials, and its last frame's row
+    // maximum
     __syncthreads();
+    if (it > 0 && tid == 0 && prow) {
+      const uint32_t *q = rslot + ((it - 1) & 1) * 4;
+      prow[blockIdx.x + (it - 1) * (int)gridDim.x] = max(max(q[0], q[1]), max(q[2], q[3]));
+    }
     if (pcol) {  // exponent bytes (pool_colmax_kernel), four per dword store
       const int npool = g.G / PC * g.P;
       uint8_t *dst = reinterpret_cast<uint8_t *>(pcol) + (int64_t)blockIdx.x * npool;
@@ -1875,7 +1899,7 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
   if (variant == 2 && g.Kdim <= 32 && g.G <= 128 && g.P <= 4 * 32 * 3 &&
       g.C * g.HW <= 256 * 8) {
     const size_t lds = (size_t)((32 * g.P + 3) & ~3) * 4 + 160 * 4 + 32 * 8 +
-                       (size_t)g.C * g.HW * 4;
+                       (size_t)g.C * g.HW * 4 + 8 * 4;
     if (lds <= (size_t)kFrameLdsMax) {
       const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0);
       const int ksn = (g.Kdim + 1) / 2;
@@ -1886,7 +1910,7 @@ int kcnn_conv_fwd_frame(const ConvGeom &g, const float *X, int xs,
 #define KCNN_FWD_REGS_T(KS_, AR_)                                                       \
   hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, 0, AR_>), dim3(grid), dim3(256), lds, \
                      st, g, X, xs, K, ks, bias, out, os, vec_ok, dbg, nullptr, 0, nullptr, \
-                     0, PoolWin{}, nullptr, nullptr)
+                     0, PoolWin{}, RpStats{})
 #define KCNN_FWD_REGS(KS_) KCNN_FWD_REGS_T(KS_, 0)
       static const int dbg = KCNN_KNOB("KCNN_FWD_DEBUG", 0);
       if (ar == 2 && g.Kdim <= 16) KCNN_FWD_REGS_T(1, 2);
@@ -1977,7 +2001,7 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
       g.C * g.HW > 256 * 8)
     return -1;
   const size_t lds = (size_t)((32 * g.P + 3) & ~3) * 4 + 160 * 4 + 32 * 8 +
-                     (size_t)g.C * g.HW * 4;
+                     (size_t)g.C * g.HW * 4 + 8 * 4;
   if (lds > (size_t)kFrameLdsMax) return -1;
   const int vec_ok = ((uintptr_t)out % 16 == 0) && (os % 4 == 0) ? 1 | y_nt() : 0;
   const int ksn = (g.Kdim + 1) / 2;
@@ -1993,25 +2017,25 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
                   ntile <= 4 * 3 && ar == 2;
   // the register-pooled kernel also gives the pooled output's max |value|
   // bits per frame and per column (stats, when the caller passes room)
-  uint32_t *prow = nullptr, *pcol = nullptr;
+  RpStats rps;
   if (rp && stats && stats->partials &&
-      stats->partial_words * 4 >= (size_t)grid * (g.G / pc) * g.P) {
-    prow = stats->rowmax;
-    pcol = stats->partials;
-    hipError_t e = hipMemsetAsync(prow, 0, (size_t)g.R * 4, st);
-    if (e == hipSuccess) e = hipMemsetAsync(stats->colmax, 0, (size_t)(g.G / pc) * g.P * 4, st);
-    if (e != hipSuccess) return (int)e;
+      stats->partial_words * 4 >= (size_t)grid * (g.G / pc) * g.P &&
+      (size_t)grid * 256 >= (size_t)(g.G / pc) * g.P) {
+    rps.rowmax = stats->rowmax;
+    rps.partials = stats->partials;
+    rps.colmax = stats->colmax;
   }
+  uint32_t *pcol = rps.partials;
 #define KCNN_FWD_POOL_T(KS_, PC_, AR_)                                                      \
   do {                                                                                       \
     if (rp && PC_ == 4 && AR_ == 2)                                                          \
       hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_, AR_, PC_ == 4 && AR_ == 2>),     \
                          dim3(grid), dim3(256), lds, st, g, X, xs, K, ks, bias, out, os,     \
-                         vec_ok, dbg, pool, ps, mask, ms, pw3, prow, pcol);                  \
+                         vec_ok, dbg, pool, ps, mask, ms, pw3, rps);                         \
     else                                                                                     \
       hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_, AR_>), dim3(grid), dim3(256), lds, \
                          st, g, X, xs, K, ks, bias, out, os, vec_ok, dbg, pool, ps, mask, ms, pw3, \
-                         nullptr, nullptr);                                                  \
+                         RpStats{});                                                         \
   } while (0)
 #define KCNN_FWD_POOL(KS_, PC_) KCNN_FWD_POOL_T(KS_, PC_, 0)
 #define KCNN_FWD_POOL_KS(PC_)                     \

@@ -343,8 +343,9 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
   const int lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
   const int half2 = lane >> 5;
   const bool partial = p.ksplit > 1;
-  float *slab = partial ? p.part + (int64_t)split * p.M * p.N : p.C;
-  const int ldo = partial ? p.N : p.ldc;
+  const int np4 = (p.N + 3) & ~3;  // partial slab pitch (16-B rows)
+  float *slab = partial ? p.part + (int64_t)split * p.M * np4 : p.C;
+  const int ldo = partial ? np4 : p.ldc;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -412,9 +413,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
   const float *baseB = B_KC ? p.B + (int64_t)col0 * p.ldb : p.B + (int64_t)kbeg * p.ldb + col0;
   const int vra = p.M - row0, vrb = p.N - col0;
   const int64_t endA = A_KC ? ((int64_t)(vra - 1) * p.lda + p.K) * 4
-                            : ((int64_t)(p.K - 1 - kbeg) * p.lda + vra) * 4;
+                            : ((int64_t)(p.K - 1 - kbeg) * p.lda + ((vra + 3) & ~3)) * 4;
   const int64_t endB = B_KC ? ((int64_t)(vrb - 1) * p.ldb + p.K) * 4
-                            : ((int64_t)(p.K - 1 - kbeg) * p.ldb + vrb) * 4;
+                            : ((int64_t)(p.K - 1 - kbeg) * p.ldb + ((vrb + 3) & ~3)) * 4;
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
       (void *)baseA, (short)0, (int)(endA < 0x7fffffff ? endA : 0x7fffffff), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
@@ -553,9 +554,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
   const float *baseB = B_KC ? p.B + (int64_t)col0 * p.ldb : p.B + (int64_t)kbeg * p.ldb + col0;
   const int vra = p.M - row0, vrb = p.N - col0;
   const int64_t endA = A_KC ? ((int64_t)(vra - 1) * p.lda + p.K) * 4
-                            : ((int64_t)(p.K - 1 - kbeg) * p.lda + vra) * 4;
+                            : ((int64_t)(p.K - 1 - kbeg) * p.lda + ((vra + 3) & ~3)) * 4;
   const int64_t endB = B_KC ? ((int64_t)(vrb - 1) * p.ldb + p.K) * 4
-                            : ((int64_t)(p.K - 1 - kbeg) * p.ldb + vrb) * 4;
+                            : ((int64_t)(p.K - 1 - kbeg) * p.ldb + ((vrb + 3) & ~3)) * 4;
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
       (void *)baseA, (short)0, (int)(endA < 0x7fffffff ? endA : 0x7fffffff), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
@@ -841,41 +842,33 @@ int stats_launch(const StatOp &a, const StatOp &b, hipStream_t st) {
   return kcnn::launch_status();
 }
 
-// C = alpha * sum_s part[s] + beta * C, the splits added in increasing s;
-// elements of an Inf / NaN row or column are the epilogue's (split 0)
-template <bool VEC>
+// C = alpha * sum_s part[s] + beta * C, the splits added in increasing s
+// (slab rows padded to np4 = N rounded up to 4: 16-B reads; a quad's columns
+// past N are not stored); elements of an Inf / NaN row or column are the
+// epilogue's (split 0)
 __global__ void gemm_f16x3_reduce_kernel(const float *__restrict__ part, int S, int M, int N,
                                          float alpha, float beta, float *C, int ldc,
                                          const uint32_t *__restrict__ amax,
                                          const uint32_t *__restrict__ bmax) {
-  constexpr int W = VEC ? 4 : 1;
-  const int64_t nw = N / W;
-  const int64_t total = (int64_t)M * nw;
-  const int64_t plane = (int64_t)M * N;
+  const int np4 = (N + 3) & ~3, nq = np4 >> 2;
+  const int64_t total = (int64_t)M * nq;
+  const int64_t plane = (int64_t)M * np4;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = e / nw, c = (e - r * nw) * W;
-    float s[W];
-    if constexpr (VEC) {
-      const float4 v = *reinterpret_cast<const float4 *>(part + r * N + c);
-      s[0] = v.x; s[1] = v.y; s[2] = v.z; s[3] = v.w;
-    } else {
-      s[0] = part[r * N + c];
-    }
+    const int r = (int)(e / nq), c = (int)(e - (int64_t)r * nq) * 4;
+    const float *q = part + (int64_t)r * np4 + c;
+    float4 v = *reinterpret_cast<const float4 *>(q);
     for (int k = 1; k < S; ++k) {
-      if constexpr (VEC) {
-        const float4 v = *reinterpret_cast<const float4 *>(part + k * plane + r * N + c);
-        s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
-      } else {
-        s[0] += part[k * plane + r * N + c];
-      }
+      const float4 w = *reinterpret_cast<const float4 *>(q + k * plane);
+      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
     }
     if (amax[r] >= NONFINITE) continue;
-    float *o = C + r * ldc + c;
+    const float sv[4] = {v.x, v.y, v.z, v.w};
+    float *o = C + (int64_t)r * ldc + c;
 #pragma unroll
-    for (int i = 0; i < W; ++i) {
-      if (bmax[c + i] >= NONFINITE) continue;
-      o[i] = beta == 0.0f ? alpha * s[i] : alpha * s[i] + beta * o[i];
+    for (int i = 0; i < 4; ++i) {
+      if (c + i >= N || bmax[c + i] >= NONFINITE) continue;
+      o[i] = beta == 0.0f ? alpha * sv[i] : alpha * sv[i] + beta * o[i];
     }
   }
 }
@@ -943,7 +936,7 @@ size_t align16(size_t b) { return (b + 15) & ~(size_t)15; }
 size_t partial_bytes(int M, int N, int K) {
   const int64_t tiles = (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const int s = choose_ksplit(tiles, K);
-  return s > 1 ? align16(sizeof(float) * (size_t)s * M * N) : 0;
+  return s > 1 ? align16(sizeof(float) * (size_t)s * M * ((N + 3) & ~3)) : 0;
 }
 
 }  // namespace
@@ -993,7 +986,7 @@ extern "C" int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, flo
   a.tiles_n = (N + BN - 1) / BN;
   const int64_t tiles = (int64_t)a.tiles_m * a.tiles_n;
   int s = choose_ksplit(tiles, K);
-  const size_t need = s > 1 ? sizeof(float) * (size_t)s * M * N : 0;
+  const size_t need = s > 1 ? sizeof(float) * (size_t)s * M * ((N + 3) & ~3) : 0;
   if (need > ws_bytes || !ws) s = 1;
   if (s > 1) a.part = static_cast<float *>(ws);
   a.ksplit = s;
@@ -1007,21 +1000,20 @@ extern "C" int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, flo
   };
   if (!fits(a_kc, lda, BM) || !fits(b_kc, ldb, BN)) return (int)hipErrorNotSupported;
   // a row-contiguous operand takes 16-B loads along its rows when they are
-  // aligned and its row count (M or N) is a multiple of 4
-  auto mode = [](bool kc, const float *ptr, int ld, int rows) {
+  // aligned (pitch % 4 == 0: a quad that starts inside the row count M or N
+  // ends inside the pitch; its values past the count feed only C rows or
+  // columns that are not stored, and the descriptors above end at the last
+  // row's padded quad)
+  auto mode = [](bool kc, const float *ptr, int ld) {
     if (kc) return (int)LK;
     static const int tr = KCNN_KNOB("KCNN_F16X3_TR", 1);
-    return tr && ld % 4 == 0 && (uintptr_t)ptr % 16 == 0 && rows % 4 == 0 ? (int)LT : (int)LR;
+    return tr && ld % 4 == 0 && (uintptr_t)ptr % 16 == 0 ? (int)LT : (int)LR;
   };
-  launch(mode(a_kc, A, lda, M), mode(b_kc, B, ldb, N), a, (unsigned)nb, st);
+  launch(mode(a_kc, A, lda), mode(b_kc, B, ldb), a, (unsigned)nb, st);
   int rc = kcnn::launch_status();
   if (rc || s == 1) return rc;
-  if (N % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0)
-    hipLaunchKernelGGL(gemm_f16x3_reduce_kernel<true>, dim3(kcnn::grid_for((int64_t)M * (N / 4))),
-                       dim3(256), 0, st, a.part, s, M, N, alpha, beta, C, ldc, amax, bmax);
-  else
-    hipLaunchKernelGGL(gemm_f16x3_reduce_kernel<false>, dim3(kcnn::grid_for((int64_t)M * N)),
-                       dim3(256), 0, st, a.part, s, M, N, alpha, beta, C, ldc, amax, bmax);
+  hipLaunchKernelGGL(gemm_f16x3_reduce_kernel, dim3(kcnn::grid_for((int64_t)M * ((N + 3) / 4))),
+                     dim3(256), 0, st, a.part, s, M, N, alpha, beta, C, ldc, amax, bmax);
   return kcnn::launch_status();
 }
 

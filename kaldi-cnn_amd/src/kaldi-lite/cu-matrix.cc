@@ -293,14 +293,17 @@ void CuMatrixBase<Real>::AddMatMat(Real alpha, const CuMatrixBase<Real> &A,
     // need the K-contiguous operands (A untransposed, B transposed)
     // row-aligned; one that is not (a caller's matrix with an odd pitch,
     // e.g. an output derivative of 3454 columns) is copied once into a
-    // padded-pitch CuMatrix, which costs far less than the GEMM.
+    // padded-pitch CuMatrix, which costs far less than the GEMM.  So is a
+    // row-contiguous one under f16x3, whose 16-B transposed loads (LT) take
+    // 450 -> ~260 us on nnet.config's last FC weight gradient (the one-column
+    // loads' kernel otherwise).
     auto aligned = [](const CuMatrixBase<Real> &X) {
       return X.Stride() % 4 == 0 && reinterpret_cast<uintptr_t>(X.Data()) % 16 == 0;
     };
     CuMatrix<Real> Acopy, Bcopy;
     const CuMatrixBase<Real> *Ap = &A, *Bp = &B;
-    if (transA == kNoTrans && !aligned(A)) { Acopy = A; Ap = &Acopy; }
-    if (transB == kTrans && !aligned(B)) { Bcopy = B; Bp = &Bcopy; }
+    if ((transA == kNoTrans || mode == 2) && !aligned(A)) { Acopy = A; Ap = &Acopy; }
+    if ((transB == kTrans || mode == 2) && !aligned(B)) { Bcopy = B; Bp = &Bcopy; }
     if (mode == 2) {
       // op(A)'s row / op(B)'s column statistics from their producer, if any
       // (CuGemmStatsHint: e.g. the fused conv + pool forward's pooled output)

@@ -25,6 +25,22 @@ __global__ __launch_bounds__(256) void relu_prop_kernel(const float *__restrict_
   }
 }
 
+// The same four columns to a lane (16-B accesses; see kn_relu_prop)
+__global__ __launch_bounds__(256) void relu_prop4_kernel(const float *__restrict__ in,
+                                                         int64_t is, float *__restrict__ out,
+                                                         int64_t os, int rows, int cols) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= cols) return;
+  for (int r = blockIdx.y; r < rows; r += gridDim.y) {
+    float4 v = *reinterpret_cast<const float4 *>(in + (int64_t)r * is + c);
+    if (v.x < 0.0f) v.x = 0.0f;
+    if (v.y < 0.0f) v.y = 0.0f;
+    if (v.z < 0.0f) v.z = 0.0f;
+    if (v.w < 0.0f) v.w = 0.0f;
+    *reinterpret_cast<float4 *>(out + (int64_t)r * os + c) = v;
+  }
+}
+
 constexpr int kReluRowsPerPart = 64;
 
 // Block: 256 consecutive columns x one chunk of kReluRowsPerPart rows.
@@ -48,6 +64,50 @@ __global__ __launch_bounds__(256) void relu_backprop_kernel(
     part_v[(int64_t)blockIdx.y * cols + c] = sv;
     part_h[(int64_t)blockIdx.y * cols + c] = sh;
   }
+}
+
+// The same map four columns to a lane (16-B accesses; cols, strides and
+// pointers multiples of 4 floats): a block is 256 columns x one 64-row part,
+// wave w taking rows w, w + 4, ...; the part's column sums are the four
+// waves' sums added in wave order.
+__global__ __launch_bounds__(256) void relu_backprop4_kernel(
+    const float *__restrict__ ov, int64_t ovs, const float *__restrict__ od, int64_t ods,
+    float *__restrict__ id, int64_t ids, int rows, int cols, float *__restrict__ part_v,
+    float *__restrict__ part_h) {
+  __shared__ float4 red[2][3][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + lane) * 4;
+  const int r0 = blockIdx.y * kReluRowsPerPart;
+  const int r1 = min(rows, r0 + kReluRowsPerPart);
+  float4 sv = make_float4(0.0f, 0.0f, 0.0f, 0.0f), sh = sv;
+  if (c < cols) {
+#pragma unroll 4
+    for (int r = r0 + w; r < r1; r += 4) {
+      const float4 o = *reinterpret_cast<const float4 *>(ov + (int64_t)r * ovs + c);
+      const float4 d = *reinterpret_cast<const float4 *>(od + (int64_t)r * ods + c);
+      const float4 h = make_float4(o.x > 0.0f ? 1.0f : 0.0f, o.y > 0.0f ? 1.0f : 0.0f,
+                                   o.z > 0.0f ? 1.0f : 0.0f, o.w > 0.0f ? 1.0f : 0.0f);
+      *reinterpret_cast<float4 *>(id + (int64_t)r * ids + c) =
+          make_float4(h.x * d.x, h.y * d.y, h.z * d.z, h.w * d.w);
+      sv.x += o.x; sv.y += o.y; sv.z += o.z; sv.w += o.w;
+      sh.x += h.x; sh.y += h.y; sh.z += h.z; sh.w += h.w;
+    }
+  }
+  if (part_v == nullptr) return;
+  if (w > 0) {
+    red[0][w - 1][lane] = sv;
+    red[1][w - 1][lane] = sh;
+  }
+  __syncthreads();
+  if (w > 0 || c >= cols) return;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float4 a = red[0][k][lane], b = red[1][k][lane];
+    sv.x += a.x; sv.y += a.y; sv.z += a.z; sv.w += a.w;
+    sh.x += b.x; sh.y += b.y; sh.z += b.z; sh.w += b.w;
+  }
+  *reinterpret_cast<float4 *>(part_v + (int64_t)blockIdx.y * cols + c) = sv;
+  *reinterpret_cast<float4 *>(part_h + (int64_t)blockIdx.y * cols + c) = sh;
 }
 
 __global__ __launch_bounds__(256) void relu_stats_final_kernel(
@@ -153,14 +213,22 @@ int kn_relu_prop(const float *in, MatrixDim in_dim, float *out, MatrixDim out_di
   if (in_dim.rows != out_dim.rows || in_dim.cols != out_dim.cols)
     return (int)hipErrorInvalidValue;
   if (in_dim.rows == 0 || in_dim.cols == 0) return 0;
-  const unsigned cb = (unsigned)((in_dim.cols + 255) / 256);
+  const bool vec4 = in_dim.cols % 4 == 0 && in_dim.stride % 4 == 0 && out_dim.stride % 4 == 0 &&
+                    (uintptr_t)in % 16 == 0 && (uintptr_t)out % 16 == 0;
+  const int cpb = vec4 ? 1024 : 256;  // columns per block
+  const unsigned cb = (unsigned)((in_dim.cols + cpb - 1) / cpb);
   unsigned rb = (unsigned)in_dim.rows;
   const unsigned cap = 8192u / cb + 1u;  // ~8k blocks, rows grid-strided
   if (rb > cap) rb = cap;
   if (rb > 65535u) rb = 65535u;
-  hipLaunchKernelGGL(relu_prop_kernel, dim3(cb, rb), dim3(256), 0, kcnn::as_stream(st), in,
-                     (int64_t)in_dim.stride, out, (int64_t)out_dim.stride, in_dim.rows,
-                     in_dim.cols);
+  if (vec4)
+    hipLaunchKernelGGL(relu_prop4_kernel, dim3(cb, rb), dim3(256), 0, kcnn::as_stream(st), in,
+                       (int64_t)in_dim.stride, out, (int64_t)out_dim.stride, in_dim.rows,
+                       in_dim.cols);
+  else
+    hipLaunchKernelGGL(relu_prop_kernel, dim3(cb, rb), dim3(256), 0, kcnn::as_stream(st), in,
+                       (int64_t)in_dim.stride, out, (int64_t)out_dim.stride, in_dim.rows,
+                       in_dim.cols);
   return kcnn::launch_status();
 }
 
@@ -182,10 +250,20 @@ int kn_relu_backprop(const float *out_value, MatrixDim ov_dim, const float *out_
   float *pv = stats ? static_cast<float *>(ws) : nullptr;
   float *ph = stats ? pv + (size_t)nparts * od_dim.cols : nullptr;
   hipStream_t s = kcnn::as_stream(st);
-  hipLaunchKernelGGL(relu_backprop_kernel, dim3((od_dim.cols + 255) / 256, nparts),
-                     dim3(256), 0, s, out_value, (int64_t)ov_dim.stride, out_deriv,
-                     (int64_t)od_dim.stride, in_deriv, (int64_t)id_dim.stride, od_dim.rows,
-                     od_dim.cols, pv, ph);
+  const bool vec4 = od_dim.cols % 4 == 0 && ov_dim.stride % 4 == 0 &&
+                    od_dim.stride % 4 == 0 && id_dim.stride % 4 == 0 &&
+                    (uintptr_t)out_value % 16 == 0 && (uintptr_t)out_deriv % 16 == 0 &&
+                    (uintptr_t)in_deriv % 16 == 0 && (uintptr_t)pv % 16 == 0;
+  if (vec4)
+    hipLaunchKernelGGL(relu_backprop4_kernel, dim3((od_dim.cols + 255) / 256, nparts),
+                       dim3(256), 0, s, out_value, (int64_t)ov_dim.stride, out_deriv,
+                       (int64_t)od_dim.stride, in_deriv, (int64_t)id_dim.stride, od_dim.rows,
+                       od_dim.cols, pv, ph);
+  else
+    hipLaunchKernelGGL(relu_backprop_kernel, dim3((od_dim.cols + 255) / 256, nparts),
+                       dim3(256), 0, s, out_value, (int64_t)ov_dim.stride, out_deriv,
+                       (int64_t)od_dim.stride, in_deriv, (int64_t)id_dim.stride, od_dim.rows,
+                       od_dim.cols, pv, ph);
   int rc = kcnn::launch_status();
   if (rc || !stats) return rc;
   hipLaunchKernelGGL(relu_stats_final_kernel, dim3((od_dim.cols + 255) / 256), dim3(256),

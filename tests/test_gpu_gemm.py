@@ -244,3 +244,25 @@ def test_gemm_planes(kc, ta, tb, shape):
     m, n, k = shape
     _check_planes(torch, kc, m, n, k, ta, tb)
     _check_planes(torch, kc, m, n, k, ta, tb, alpha=0.5, beta=1.0)
+
+
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("shape,pitch", [((258, 130, 300), 2), ((258, 130, 4500), 2),
+                                         ((3454, 64, 1024), 2), ((130, 70, 200), 12)])
+def test_gemm_f16x3_ragged_rows(kc, ta, tb, shape, pitch):
+    """M and N not multiples of 4: a row-contiguous operand with a 16-B pitch
+    takes the 16-B transposed loads, whose last quad runs into the pitch's
+    padding (those rows / columns of C are not stored); an odd pitch is
+    copied to a padded one first; split K sums slabs of a padded pitch."""
+    import torch
+    m, n, k = shape
+    for alpha, beta in ((1.0, 0.0), (0.5, 1.0)):
+        a, b, c0 = _mats(torch, m, n, k, ta, tb, 9, pitch=pitch)
+        for x in (a, b):  # NaN in the pitch's padding: never reaches a stored C
+            torch.as_strided(x, (x.shape[0], pitch), (x.stride(0), 1), x.shape[1]).fill_(
+                float("nan"))
+        c = c0.clone()
+        _gemm_mode(kc, 2, lambda: kc.gemm(a, b, c, ta, tb, alpha, beta))
+        torch.cuda.synchronize()
+        _bound(torch, a, b, c0, c, ta, tb, alpha, beta)

@@ -16,9 +16,10 @@ from _util import assert_same, dev, host, randn, rng
 pytestmark = pytest.mark.gpu
 
 
-def test_relu_component(kc):
+@pytest.mark.parametrize("dim", [2304, 2303])  # 16-B lanes; the one-column kernels
+def test_relu_component(kc, dim):
     r = rng(1)
-    dim, N = 2304, 37
+    N = 70  # two 64-row stats parts, the second ragged
     comp = kc.Component.NewFromString(f"RectifiedLinearComponent dim={dim}")
     assert comp.Type() == "RectifiedLinearComponent" and comp.InputDim() == dim
     assert not comp.BackpropNeedsInput() and comp.BackpropNeedsOutput()

@@ -494,7 +494,11 @@ def main():
     gen = torch.Generator(device="cuda")
     gen.manual_seed(20261015 + rank)  # each rank its own shard of frames
     x = torch.randn((in_rows, in_cols), generator=gen, device="cuda")
-    dy = torch.randn((B, out_cols), generator=gen, device="cuda") * 1e-2
+    # the output derivative in a pitched buffer (rows padded to 16 floats), as
+    # a CuMatrix holds it (the reference's CuMatrix: cudaMallocPitch); an
+    # unpadded 3454-column nnet.config derivative costs the FC GEMMs a copy
+    pitch = (out_cols + 15) // 16 * 16
+    dy = torch.randn((B, pitch), generator=gen, device="cuda").mul_(1e-2)[:, :out_cols]
 
     grads = kcnn_dp.gradient_buffers(
         net, lambda n: torch.empty(n, device="cuda"))

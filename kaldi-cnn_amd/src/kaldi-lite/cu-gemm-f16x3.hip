@@ -249,7 +249,10 @@ struct Loader {
       const int unit = tid;
       const int rq = unit % (R / 4), kq = unit / (R / 4);
       float x0 = v[0][4 * j + 2 * hf], x1 = v[0][4 * j + 2 * hf + 1];
-      if (RAG && kv < BK && kq * KPT + j >= kv) x0 = x1 = 0.0f;
+      if (RAG && kv < BK) {
+        asm volatile("");  // a branch: not per-element selects in every K step
+        if (kq * KPT + j >= kv) x0 = x1 = 0.0f;
+      }
       split2h(x0, x1, e[2 * hf], e[2 * hf + 1], ph[hf], pl[hf]);
       if (hf == 1) {
         const int o = tswz<R>(kq * KPT + j, 4 * rq);
@@ -272,6 +275,7 @@ struct Loader {
       }
       float x0 = v[u][2 * q], x1 = v[u][2 * q + 1];
       if (RAG && kv < BK) {
+        asm volatile("");  // a branch: not per-element selects in every K step
         if (kb + 2 * q >= kv) x0 = 0.0f;
         if (kb + 2 * q + 1 >= kv) x1 = 0.0f;
       }

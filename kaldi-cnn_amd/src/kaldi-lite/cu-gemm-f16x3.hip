@@ -78,6 +78,7 @@ struct GemmF16Args {
   float *C;                      // the output
   float *part;                   // ksplit > 1: the partial slabs [ksplit][M][N]
   const uint32_t *amax, *bmax;   // max |x| bits per row of op(A), per column of op(B)
+  const float *bias;             // nullable: C += bias[col] on every row (after alpha, beta)
   int M, N, K, lda, ldb, ldc;
   int kps, ksplit, tiles_m, tiles_n;
   float alpha, beta;
@@ -366,8 +367,13 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
         if (row >= p.M || er == SKIP) continue;
         const float v = __builtin_amdgcn_ldexpf(acc[i][j][g], -(er + ec));
         float *o = slab + (int64_t)row * ldo + col;
-        if (partial) *o = v;
-        else *o = p.beta == 0.0f ? p.alpha * v : p.alpha * v + p.beta * *o;
+        if (partial) {
+          *o = v;
+        } else {
+          float r = p.beta == 0.0f ? p.alpha * v : p.alpha * v + p.beta * *o;
+          if (p.bias) r += p.bias[col];
+          *o = r;
+        }
       }
     }
   if (skip && split == 0) {
@@ -383,7 +389,9 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
         sum = fmaf(a, b, sum);
       }
       float *o = p.C + (int64_t)row * p.ldc + col;
-      *o = p.beta == 0.0f ? p.alpha * sum : p.alpha * sum + p.beta * *o;
+      float r = p.beta == 0.0f ? p.alpha * sum : p.alpha * sum + p.beta * *o;
+      if (p.bias) r += p.bias[col];
+      *o = r;
     }
   }
 }
@@ -853,7 +861,8 @@ int stats_launch(const StatOp &a, const StatOp &b, hipStream_t st) {
 __global__ void gemm_f16x3_reduce_kernel(const float *__restrict__ part, int S, int M, int N,
                                          float alpha, float beta, float *C, int ldc,
                                          const uint32_t *__restrict__ amax,
-                                         const uint32_t *__restrict__ bmax) {
+                                         const uint32_t *__restrict__ bmax,
+                                         const float *__restrict__ bias) {
   const int np4 = (N + 3) & ~3, nq = np4 >> 2;
   const int64_t total = (int64_t)M * nq;
   const int64_t plane = (int64_t)M * np4;
@@ -872,7 +881,9 @@ __global__ void gemm_f16x3_reduce_kernel(const float *__restrict__ part, int S, 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if (c + i >= N || bmax[c + i] >= NONFINITE) continue;
-      o[i] = beta == 0.0f ? alpha * sv[i] : alpha * sv[i] + beta * o[i];
+      float r = beta == 0.0f ? alpha * sv[i] : alpha * sv[i] + beta * o[i];
+      if (bias) r += bias[c + i];
+      o[i] = r;
     }
   }
 }
@@ -972,10 +983,10 @@ extern "C" int kl_absmax_cols(const float *X, int rows, int cols, int ld, uint32
 extern "C" size_t kl_gemm_f16x3_workspace_bytes(int M, int N, int K) {
   return partial_bytes(M, N, K);
 }
-extern "C" int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alpha,
-                                const float *A, int lda, const float *B, int ldb, float beta,
-                                float *C, int ldc, const uint32_t *amax, const uint32_t *bmax,
-                                void *ws, size_t ws_bytes, kcnn_stream_t stream) {
+static int gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alpha,
+                         const float *A, int lda, const float *B, int ldb, float beta, float *C,
+                         int ldc, const uint32_t *amax, const uint32_t *bmax, const float *bias,
+                         void *ws, size_t ws_bytes, kcnn_stream_t stream) {
   if (M < 0 || N < 0 || K < 0) return (int)hipErrorInvalidValue;
   if (M == 0 || N == 0 || K == 0) return (int)hipErrorNotSupported;
   const bool a_kc = !transA, b_kc = transB != 0;
@@ -983,7 +994,7 @@ extern "C" int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, flo
     return (int)hipErrorNotSupported;
   hipStream_t st = kcnn::as_stream(stream);
   GemmF16Args a{};
-  a.A = A; a.B = B; a.C = C; a.amax = amax; a.bmax = bmax;
+  a.A = A; a.B = B; a.C = C; a.amax = amax; a.bmax = bmax; a.bias = bias;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.alpha = alpha; a.beta = beta;
   a.tiles_m = (M + BM - 1) / BM;
@@ -1017,8 +1028,15 @@ extern "C" int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, flo
   int rc = kcnn::launch_status();
   if (rc || s == 1) return rc;
   hipLaunchKernelGGL(gemm_f16x3_reduce_kernel, dim3(kcnn::grid_for((int64_t)M * ((N + 3) / 4))),
-                     dim3(256), 0, st, a.part, s, M, N, alpha, beta, C, ldc, amax, bmax);
+                     dim3(256), 0, st, a.part, s, M, N, alpha, beta, C, ldc, amax, bmax, bias);
   return kcnn::launch_status();
+}
+extern "C" int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alpha,
+                                const float *A, int lda, const float *B, int ldb, float beta,
+                                float *C, int ldc, const uint32_t *amax, const uint32_t *bmax,
+                                void *ws, size_t ws_bytes, kcnn_stream_t stream) {
+  return gemm_f16x3_st(transA, transB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, amax, bmax,
+                       nullptr, ws, ws_bytes, stream);
 }
 
 // The same with the operand statistics computed here (op(A)'s rows: A's rows,
@@ -1052,6 +1070,16 @@ extern "C" int kl_gemm_f16x3_given(int transA, int transB, int M, int N, int K, 
                                    float *C, int ldc, const uint32_t *amax_given,
                                    const uint32_t *bmax_given, void *ws, size_t ws_bytes,
                                    kcnn_stream_t stream) {
+  return kl_gemm_f16x3_bias(transA, transB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc,
+                            amax_given, bmax_given, nullptr, ws, ws_bytes, stream);
+}
+// ... and C += bias[col] on every row (bias nullable), in the same store: the
+// FC forward's out = bias; out += in W^T without the bias copy or C's re-read
+extern "C" int kl_gemm_f16x3_bias(int transA, int transB, int M, int N, int K, float alpha,
+                                  const float *A, int lda, const float *B, int ldb, float beta,
+                                  float *C, int ldc, const uint32_t *amax_given,
+                                  const uint32_t *bmax_given, const float *bias, void *ws,
+                                  size_t ws_bytes, kcnn_stream_t stream) {
   if (M < 0 || N < 0 || K < 0) return (int)hipErrorInvalidValue;
   if (M == 0 || N == 0 || K == 0) return (int)hipErrorNotSupported;
   const size_t pb = partial_bytes(M, N, K);
@@ -1072,7 +1100,7 @@ extern "C" int kl_gemm_f16x3_given(int transA, int transB, int M, int N, int K, 
                               : stats_launch(sa, sb, kcnn::as_stream(stream));
     if (rc) return rc;
   }
-  return kl_gemm_f16x3_st(transA, transB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc,
-                          amax_given ? amax_given : amax, bmax_given ? bmax_given : bmax,
-                          pb ? ws : nullptr, pb, stream);
+  return gemm_f16x3_st(transA, transB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc,
+                       amax_given ? amax_given : amax, bmax_given ? bmax_given : bmax, bias,
+                       pb ? ws : nullptr, pb, stream);
 }

@@ -55,6 +55,12 @@ int kl_gemm_f16x3_given(int transA, int transB, int M, int N, int K, float alpha
                         const float *A, int lda, const float *B, int ldb, float beta, float *C,
                         int ldc, const uint32_t *amax, const uint32_t *bmax, void *ws,
                         size_t ws_bytes, kcnn_stream_t st);
+/* kl_gemm_f16x3_given with C += bias[j] on every row (bias nullable; after
+   alpha and beta), in the kernel's own store. */
+int kl_gemm_f16x3_bias(int transA, int transB, int M, int N, int K, float alpha,
+                       const float *A, int lda, const float *B, int ldb, float beta, float *C,
+                       int ldc, const uint32_t *amax_given, const uint32_t *bmax_given,
+                       const float *bias, void *ws, size_t ws_bytes, kcnn_stream_t stream);
 /* the same product from operands already split into bf16 planes h, m, l
    (plane p of X at X + p * ps elements); kl_split_planes makes them */
 int kl_split_planes(const float *src, int rows, int cols, int ld, uint16_t *dst, int ldp,

@@ -272,6 +272,61 @@ const CuGemmStatsHint *CuGemmStatsHint::Find(const float *data, MatrixIndexT row
   return nullptr;
 }
 
+// The f16x3 product (mode 2) of aligned operands Ap, Bp (A, B themselves, or
+// their padded copies; A and B name the operands for the statistics hints),
+// plus bias[j] on every row when bias != NULL.  False when the kernel
+// declines (past its 32-bit addressing): C is untouched then, and the bf16x6
+// kernel (same error bound) takes the product.
+template <typename Real>
+bool CuMatrixBase<Real>::GemmF16x3(Real alpha, const CuMatrixBase<Real> &A,
+                                   const CuMatrixBase<Real> &Ap, MatrixTransposeType transA,
+                                   const CuMatrixBase<Real> &B, const CuMatrixBase<Real> &Bp,
+                                   MatrixTransposeType transB, Real beta, const Real *bias) {
+  const MatrixIndexT m = num_rows_, n = num_cols_;
+  const MatrixIndexT k = transA == kNoTrans ? A.NumCols() : A.NumRows();
+  CuDevice &dev0 = CuDevice::Instantiate();
+  // op(A)'s row / op(B)'s column statistics from their producer, if any
+  // (CuGemmStatsHint: e.g. the fused conv + pool forward's pooled output)
+  const CuGemmStatsHint *ha = CuGemmStatsHint::Find(A.Data(), A.NumRows(), A.NumCols(),
+                                                    A.Stride());
+  const CuGemmStatsHint *hb = CuGemmStatsHint::Find(B.Data(), B.NumRows(), B.NumCols(),
+                                                    B.Stride());
+  const uint32_t *ag = ha ? (transA == kNoTrans ? ha->rowmax : ha->colmax) : nullptr;
+  const uint32_t *bg = hb ? (transB == kNoTrans ? hb->colmax : hb->rowmax) : nullptr;
+  const size_t wsf = kl_gemm_f16x3_full_workspace_bytes(m, n, k);
+  void *wf = dev0.Malloc(wsf);
+  const int rc = kl_gemm_f16x3_bias(transA == kTrans, transB == kTrans, m, n, k, alpha,
+                                    Ap.Data(), Ap.Stride(), Bp.Data(), Bp.Stride(), beta, data_,
+                                    stride_, ag, bg, bias, wf, wsf, S());
+  dev0.Free(wf);
+  if (rc == (int)hipErrorNotSupported) return false;
+  CNSL_SAFE_CALL(rc);
+  return true;
+}
+
+template <typename Real>
+void CuMatrixBase<Real>::AddMatMatBias(Real alpha, const CuMatrixBase<Real> &A,
+                                       MatrixTransposeType transA, const CuMatrixBase<Real> &B,
+                                       MatrixTransposeType transB,
+                                       const CuVectorBase<Real> &bias) {
+  const MatrixIndexT k = transA == kNoTrans ? A.NumCols() : A.NumRows();
+  KALDI_ASSERT(bias.Dim() == num_cols_);
+  CuDevice &dev0 = CuDevice::Instantiate();
+  auto aligned = [](const CuMatrixBase<Real> &X) {
+    return X.Stride() % 4 == 0 && reinterpret_cast<uintptr_t>(X.Data()) % 16 == 0;
+  };
+  if (dev0.GemmMode() == 2 && num_rows_ > 0 && num_cols_ > 0 && k > 0 && aligned(A) &&
+      aligned(B)) {
+    KALDI_ASSERT((transA == kNoTrans ? A.NumRows() : A.NumCols()) == num_rows_ &&
+                 (transB == kNoTrans ? B.NumCols() : B.NumRows()) == num_cols_ &&
+                 (transB == kNoTrans ? B.NumRows() : B.NumCols()) == k);
+    CuProfileScope prof("AddMatMat");
+    if (GemmF16x3(alpha, A, A, transA, B, B, transB, 0.0f, bias.Data())) return;
+  }
+  CopyRowsFromVec(bias);
+  AddMatMat(alpha, A, transA, B, transB, 1.0f);
+}
+
 template <typename Real>
 void CuMatrixBase<Real>::AddMatMat(Real alpha, const CuMatrixBase<Real> &A,
                                    MatrixTransposeType transA,
@@ -304,28 +359,7 @@ void CuMatrixBase<Real>::AddMatMat(Real alpha, const CuMatrixBase<Real> &A,
     const CuMatrixBase<Real> *Ap = &A, *Bp = &B;
     if ((transA == kNoTrans || mode == 2) && !aligned(A)) { Acopy = A; Ap = &Acopy; }
     if ((transB == kTrans || mode == 2) && !aligned(B)) { Bcopy = B; Bp = &Bcopy; }
-    if (mode == 2) {
-      // op(A)'s row / op(B)'s column statistics from their producer, if any
-      // (CuGemmStatsHint: e.g. the fused conv + pool forward's pooled output)
-      const CuGemmStatsHint *ha = CuGemmStatsHint::Find(A.Data(), A.NumRows(), A.NumCols(),
-                                                        A.Stride());
-      const CuGemmStatsHint *hb = CuGemmStatsHint::Find(B.Data(), B.NumRows(), B.NumCols(),
-                                                        B.Stride());
-      const uint32_t *ag = ha ? (transA == kNoTrans ? ha->rowmax : ha->colmax) : nullptr;
-      const uint32_t *bg = hb ? (transB == kNoTrans ? hb->colmax : hb->rowmax) : nullptr;
-      const size_t wsf = kl_gemm_f16x3_full_workspace_bytes(m, n, k);
-      void *wf = dev0.Malloc(wsf);
-      const int rc = kl_gemm_f16x3_given(transA == kTrans, transB == kTrans, m, n, k, alpha,
-                                         Ap->Data(), Ap->Stride(), Bp->Data(), Bp->Stride(),
-                                         beta, data_, stride_, ag, bg, wf, wsf, S());
-      dev0.Free(wf);
-      // past the f16x3 kernel's 32-bit addressing the bf16x6 kernel (same
-      // error bound) takes the product
-      if (rc != (int)hipErrorNotSupported) {
-        CNSL_SAFE_CALL(rc);
-        return;
-      }
-    }
+    if (mode == 2 && GemmF16x3(alpha, A, *Ap, transA, B, *Bp, transB, beta, nullptr)) return;
     const size_t wsb = kl_gemm_x6_workspace_bytes(m, n, k);
     void *ws = wsb ? dev0.Malloc(wsb) : nullptr;
     const int rc = kl_gemm_x6(transA == kTrans, transB == kTrans, m, n, k, alpha,

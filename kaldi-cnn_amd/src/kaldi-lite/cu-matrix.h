@@ -114,6 +114,12 @@ class CuMatrixBase {
   void AddMatMat(Real alpha, const CuMatrixBase<Real> &A,
                  MatrixTransposeType transA, const CuMatrixBase<Real> &B,
                  MatrixTransposeType transB, Real beta);
+  /// *this = alpha * op(A) op(B) + bias on every row (an FC forward's
+  /// CopyRowsFromVec(bias); AddMatMat(alpha, A, tA, B, tB, 1.0) in one pass
+  /// under the f16x3 engine; those two calls otherwise)
+  void AddMatMatBias(Real alpha, const CuMatrixBase<Real> &A, MatrixTransposeType transA,
+                     const CuMatrixBase<Real> &B, MatrixTransposeType transB,
+                     const CuVectorBase<Real> &bias);
   /// every row = v
   void CopyRowsFromVec(const CuVectorBase<Real> &v);
   void CopyRowsFromVec(const VectorBase<Real> &v);  // host vector
@@ -165,6 +171,10 @@ class CuMatrixBase {
                          bool fromCompToContainer);
 
  protected:
+  bool GemmF16x3(Real alpha, const CuMatrixBase<Real> &A, const CuMatrixBase<Real> &Ap,
+                 MatrixTransposeType transA, const CuMatrixBase<Real> &B,
+                 const CuMatrixBase<Real> &Bp, MatrixTransposeType transB, Real beta,
+                 const Real *bias);
   CuMatrixBase() : data_(nullptr), num_cols_(0), num_rows_(0), stride_(0) {}
   CuMatrixBase(Real *data, MatrixIndexT num_rows, MatrixIndexT num_cols,
                MatrixIndexT stride)

@@ -253,8 +253,9 @@ void AffineComponent::Propagate(const ChunkInfo &in_info,
   in_info.CheckSize(in);
   out_info.CheckSize(*out);
   KALDI_ASSERT(in_info.NumChunks() == out_info.NumChunks());
-  out->CopyRowsFromVec(bias_params_);
-  out->AddMatMat(1.0, in, kNoTrans, linear_params_, kTrans, 1.0);
+  // CopyRowsFromVec(bias); AddMatMat(1.0, in, kNoTrans, W, kTrans, 1.0), the
+  // bias added in the GEMM's store under the f16x3 engine
+  out->AddMatMatBias(1.0, in, kNoTrans, linear_params_, kTrans, bias_params_);
 }
 
 void AffineComponent::Scale(BaseFloat scale) {

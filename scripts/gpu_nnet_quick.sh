@@ -5,7 +5,7 @@ set -o pipefail
 O=${1:-gpurun_out/nnetq}
 rm -rf $O; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 700 python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_nnet2.py tests/test_gpu_nnet.py "tests/test_gpu_fullsize.py::test_c2_bench_step" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest_rc=$?" >> $O/pytest.log; tail -40 $O/pytest.log; exit 3; }
+timeout -k 10 700 python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_components.py tests/test_gpu_nnet2.py tests/test_gpu_nnet.py "tests/test_gpu_fullsize.py::test_c2_bench_step" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest_rc=$?" >> $O/pytest.log; tail -40 $O/pytest.log; exit 3; }
 tail -1 $O/pytest.log
 timeout -k 10 300 python bench.py --config nnet --no-cpu-baseline --json-out $O/bench_nnet.json > $O/bench_nnet.log 2>&1 || exit 6
 python -c "import json;d=json.load(open('$O/bench_nnet.json'));print('nnet', d['value'], d['ms_per_step'])"

@@ -284,6 +284,28 @@ def test_fc_component(kc, path, I, Od, N):
     assert_bound(host(comp.BiasParams()), of.b, np.abs(b0) + lr * gb_s, what="FC b'")
 
 
+@pytest.mark.parametrize("I,Od,N", [(300, 70, 33), (8192, 64, 40), (2048, 1024, 300)])
+def test_fc_bias_in_gemm_store(kc, I, Od, N):
+    """FC Propagate adds the bias in the f16x3 GEMM's own store (one split or
+    the split-K sum): the bits of the reference's two calls, out =
+    CopyRowsFromVec(bias) then AddMatMat(1, in, W^T, beta = 1)."""
+    import torch
+    comp = kc.Component.NewFromString(
+        f"FullyConnectedComponent input-dim={I} output-dim={Od} learning-rate=0.02 "
+        f"param-stddev=0.01 bias-stddev=1")
+    r = rng(I + Od)
+    W = randn(r, (Od, I), 0.05)
+    b = randn(r, (Od,), 0.5)
+    comp.SetParam(0, dev(W))
+    comp.SetParam(1, dev(b))
+    x = randn(r, (N, I))
+    y = host(comp.Propagate(dev(x)))
+    c = dev(np.broadcast_to(b, (N, Od)).copy())
+    kc.gemm(dev(x), dev(W), c, False, True, 1.0, 1.0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(y, host(c))
+
+
 @pytest.mark.parametrize("I,Od,N", [(512, 256, 2048), (300, 70, 33), (1000, 130, 4100)])
 def test_fc_update_equals_gradient_then_apply(kc, I, Od, N):
     """The update inside Backprop (UpdateSimple, nnet-component-nnet0.cc:1133-1150)

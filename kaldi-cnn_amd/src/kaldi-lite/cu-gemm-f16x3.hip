@@ -878,6 +878,21 @@ __global__ void gemm_f16x3_reduce_kernel(const float *__restrict__ part, int S, 
     if (amax[r] >= NONFINITE) continue;
     const float sv[4] = {v.x, v.y, v.z, v.w};
     float *o = C + (int64_t)r * ldc + c;
+    const bool fin = c + 4 <= N && max(max(bmax[c], bmax[c + 1]), max(bmax[c + 2], bmax[c + 3])) <
+                                       NONFINITE;
+    if (fin && ((ldc & 3) | ((uintptr_t)C & 15)) == 0) {  // one 16-B store (same values)
+      float4 ov = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (beta != 0.0f) ov = *reinterpret_cast<const float4 *>(o);
+      const float oi[4] = {ov.x, ov.y, ov.z, ov.w};
+      float w[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        w[i] = beta == 0.0f ? alpha * sv[i] : alpha * sv[i] + beta * oi[i];
+        if (bias) w[i] += bias[c + i];
+      }
+      *reinterpret_cast<float4 *>(o) = make_float4(w[0], w[1], w[2], w[3]);
+      continue;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if (c + i >= N || bmax[c + i] >= NONFINITE) continue;

@@ -6,7 +6,9 @@ host beside it.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-gpu B]
 
-N > 1 runs under torch.distributed.run, one process per GPU: the minibatch is
+N > 1 runs under torch.distributed.run, one process per GPU (started by
+bench.py itself as a child `python -m torch.distributed.run` when no launcher
+set WORLD_SIZE, so `python bench.py --gpus N` runs N ranks): the minibatch is
 row-sharded (weak scaling, B frames per GPU), gradients are computed per
 component and all-reduced over RCCL (sum, fp32) while the lower layers
 backpropagate, then every replica applies the same update with
@@ -428,6 +430,30 @@ def dp_report(dist, grads, marks, steps, reps=5):
                     "back to back with nothing else running"}
 
 
+def launch_ranks(n):
+    """Run this script under `python -m torch.distributed.run` with n ranks
+    on this node (rendezvous on 127.0.0.1, a free port) as a child process;
+    returns its exit status (nonzero when the launch itself fails)."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL
+    try:
+        rc = subprocess.run(cmd, env=env).returncode
+    except OSError as e:
+        print(f"bench: cannot start {n} ranks: {e}", file=sys.stderr)
+        return 2
+    if rc != 0:
+        print(f"bench: the {n}-rank run exited with status {rc}", file=sys.stderr)
+    return rc if rc > 0 else (1 if rc else 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -450,6 +476,13 @@ def main():
                     help="c2 (default, BASELINE's metric), the c5 deep stack, or the "
                          "reference's egs/exp/nnet/nnet.config model")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` without a launcher: start the N ranks
+        # (one process per GPU) as a child torch.distributed.run, before this
+        # process touches the GPU, relay its output (rank 0's JSON line) and
+        # exit with its status; never a one-GPU line for an N-GPU request
+        raise SystemExit(launch_ranks(args.gpus))
 
     import torch
     import kcnn

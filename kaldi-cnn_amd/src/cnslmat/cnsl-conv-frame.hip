@@ -281,6 +281,25 @@ __device__ __forceinline__ floatx16 fwd_item_fp32(
   return y;
 }
 
+// The F16 forward's check of an item touching a spread group (f16-split.h):
+// with |W'|, |x'| <= 2^15 the elements the split holds only to 2^-25
+// (scaled) add at most 2^-9 Kdim to a scaled sum, fct times that to y; an
+// output with |y| >= 2^10 Kdim fct therefore carries at most 2^-19 |y| <=
+// 2^-19 S of it.  Any output below that bound sends the whole item to
+// fwd_item_fp32 (every lane: a wave-uniform decision, the same in the fused
+// and the unfused epilogue).
+__device__ __forceinline__ void spread_check(floatx16 &y, float fct, const ConvGeom &g,
+                                             const float *__restrict__ K, int ks,
+                                             const float *__restrict__ bias, const float *Xs,
+                                             const int2 *koff, int gb, int tile, int lane) {
+  const float thr = fct * (1024.0f * (float)g.Kdim * (1.0f + 1.0f / 1024.0f));
+  float mn = fabsf(y[0]);
+#pragma unroll
+  for (int r = 1; r < 16; r++) mn = fminf(mn, fabsf(y[r]));
+  if (__builtin_amdgcn_ballot_w64(!(mn >= thr)) != 0)
+    y = fwd_item_fp32(g, K, ks, bias, Xs, koff, gb, tile, lane);
+}
+
 // The routing mask of a 4-way pool group, bit c = (v_c == mx): the four
 // compares first, then the four selects, so each select reads a compare
 // result three VALU later and needs no wait states (hipcc's order, compare /
@@ -304,19 +323,29 @@ __device__ __forceinline__ unsigned tie_mask4(float v0, float v1, float v2, floa
   return m;
 }
 
-// The register-pooled forward's statistics outputs (pool-stats.h): rowmax
-// per frame, the per-workgroup column partials (exponent bytes) and the
-// column maxima that pool_colmax_kernel fills (zeroed here first)
+// The register-pooled forward's statistics outputs (pool-stats.h): the
+// per-frame block rowmax [max[R], min[R]], the per-workgroup column partials
+// (exponent bytes: [nblk][npool] of the maxima, then of the minima) and the
+// column block colmax [max[npool], min[npool]] that pool_colmax_kernel fills
+// (initialised here first)
 struct RpStats {
   uint32_t *rowmax = nullptr, *partials = nullptr, *colmax = nullptr;
 };
 
-// The wave's max |pooled| bits of the frame into its slot of rslot (LDS; the
-// frame's four slots are combined after the next barrier)
-__device__ __forceinline__ void frame_row_max(uint32_t *rslot, uint32_t v, int lane) {
+// The wave's max |pooled| bits of the frame and its min (|pooled| - 1,
+// wrapping: a zero never wins; f16-split.h's spread groups) into its slots of
+// rslot (LDS: [2][4] maxima, then [2][4] minima; the frame's four slots are
+// combined after the next barrier)
+__device__ __forceinline__ void frame_row_max(uint32_t *rslot, uint32_t v, uint32_t u, int lane) {
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
-  if (lane == 0) *rslot = v;
+  for (int o = 32; o >= 1; o >>= 1) {
+    v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    u = min(u, (uint32_t)__shfl_xor((int)u, o));
+  }
+  if (lane == 0) {
+    rslot[0] = v;
+    rslot[8] = u;
+  }
 }
 
 // Column maxima of the pooled output from the forward's per-workgroup
@@ -324,8 +353,14 @@ __device__ __forceinline__ void frame_row_max(uint32_t *rslot, uint32_t v, int l
 // GEMM's scale needs only the binade).  colmax[c] = the largest partial's
 // binade with every mantissa bit set, an upper bound in the max's binade (so
 // the same scale; 0x7f... for Inf; an all-zero column gets the subnormal
-// bound, harmless).  colmax zeroed; blockIdx.y takes 32 workgroups' rows,
-// atomic max across those chunks.
+// bound, harmless).  The minima the same way from the partials after them
+// ((|x| - 1) >> 23 per byte, 0xff: no nonzero value): colmax[npool + c] =
+// the smallest partial's binade with no mantissa bit (1 for the subnormal
+// binade; 0xffffffff when the column has no nonzero value, which the spread
+// test of f16-split.h reads as "none"), a lower bound in the min's binade
+// (the test reads only binades; one binade low where |x| is a power of two:
+// conservative).  colmax zeroed, the minima set to 0xffffffff; blockIdx.y
+// takes 32 workgroups' rows, atomic max / min across those chunks.
 constexpr int COLMAX_ROWS = 32;
 __global__ __launch_bounds__(256) void pool_colmax_kernel(const uint8_t *__restrict__ pcol,
                                                            int nblk, int npool,
@@ -333,9 +368,14 @@ __global__ __launch_bounds__(256) void pool_colmax_kernel(const uint8_t *__restr
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= npool) return;
   const int b0 = blockIdx.y * COLMAX_ROWS, b1 = min(nblk, b0 + COLMAX_ROWS);
-  uint32_t m = 0;
-  for (int b = b0; b < b1; b++) m = max(m, (uint32_t)pcol[(int64_t)b * npool + c]);
+  const uint8_t *pmin = pcol + (int64_t)nblk * npool;
+  uint32_t m = 0, n = 0xff;
+  for (int b = b0; b < b1; b++) {
+    m = max(m, (uint32_t)pcol[(int64_t)b * npool + c]);
+    n = min(n, (uint32_t)pmin[(int64_t)b * npool + c]);
+  }
   atomicMax(colmax + c, (m << 23) | 0x7fffffu);
+  atomicMin(colmax + npool + c, n == 0xff ? 0xffffffffu : max(n << 23, 1u));
 }
 
 // RP: the register-pooled form only (out == nullptr, PC 2 or 4, G = 128 and
@@ -356,7 +396,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
   int2 *koff = reinterpret_cast<int2 *>(Bs + 160);             // [2*KS] taps
   constexpr int NKT = SPL ? 16 * KS : 2 * KS;                   // tap entries (<= 32)
   float *Xs = reinterpret_cast<float *>(koff + NKT);            // [C*HW]
-  uint32_t *rslot = reinterpret_cast<uint32_t *>(Xs + g.C * g.HW);  // [2][4] RP row maxima
+  uint32_t *rslot = reinterpret_cast<uint32_t *>(Xs + g.C * g.HW);  // [2][2][4] RP row max / min
+  uint8_t *Tmn = reinterpret_cast<uint8_t *>(rslot + 16);  // [npool] RP column min bytes
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = lane & 31, h = lane >> 5;
@@ -371,9 +412,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
   f16x3::f16x8 wh[F16 ? 4 : 1][F16 ? KS : 1], wl[F16 ? 4 : 1][F16 ? KS : 1];
   int sa = 0;
   bool wslow = false;  // Inf in W: every item in fp32
+  bool wspread = false;  // W is a spread group (f16-split.h): every item checked
+  const float m1 = F16 ? f16x3::opaque_m1() : 0.0f;  // the split's -1 (f16-split.h)
   if constexpr (F16) {
     float wv[4][KS][8];
     float m = 0.0f;
+    uint32_t mn = 0xffffffffu;  // min 2|w| - 2 (wrapping: a zero never wins)
 #pragma unroll
     for (int gb = 0; gb < 4; gb++)
 #pragma unroll
@@ -383,16 +427,22 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
           const int k = 16 * s + 8 * h + e, gg = gb * 32 + l;
           wv[gb][s][e] = gg < g.G && k < g.Kdim ? K[(int64_t)k * ks + gg] : 0.0f;
           m = fmaxf(m, fabsf(wv[gb][s][e]));  // NaN ignored: it propagates by itself
+          mn = min(mn, (__float_as_uint(wv[gb][s][e]) << 1) - 2u);
         }
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    const int s0 = f16x3::scale_exp(__builtin_amdgcn_readfirstlane(__float_as_uint(m)));
+    for (int o = 32; o >= 1; o >>= 1) {
+      m = fmaxf(m, __shfl_xor(m, o));
+      mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+    }
+    const uint32_t mwb = __builtin_amdgcn_readfirstlane(__float_as_uint(m));
+    wspread = f16x3::spread(mwb, (__builtin_amdgcn_readfirstlane(mn) >> 1) + 1u);
+    const int s0 = f16x3::scale_exp(mwb);
     wslow = s0 == f16x3::SKIP;
     sa = wslow ? 0 : s0;
 #pragma unroll
     for (int gb = 0; gb < 4; gb++)
 #pragma unroll
-      for (int s = 0; s < KS; s++) f16x3::split8h(wv[gb][s], sa, wh[gb][s], wl[gb][s]);
+      for (int s = 0; s < KS; s++) f16x3::split8h(wv[gb][s], sa, wh[gb][s], wl[gb][s], m1);
   }
   if constexpr (X6) {
 #pragma unroll
@@ -467,10 +517,17 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
   uint32_t *Tcol = reinterpret_cast<uint32_t *>(T);
   uint32_t *const prow = rps.rowmax, *const pcol = rps.partials;
   if constexpr (RP) {
-    for (int e = tid; e < g.G / PC * g.P; e += 256) Tcol[e] = 0;
-    // pool_colmax_kernel's atomic maxima start from 0 (it runs after this grid)
+    for (int e = tid; e < g.G / PC * g.P; e += 256) {
+      Tcol[e] = 0;
+      Tmn[e] = 0xff;
+    }
+    // pool_colmax_kernel's atomic maxima start from 0, its minima from
+    // 0xffffffff (it runs after this grid)
     const int c = blockIdx.x * 256 + tid;
-    if (rps.colmax && c < g.G / PC * g.P) rps.colmax[c] = 0;
+    if (rps.colmax && c < g.G / PC * g.P) {
+      rps.colmax[c] = 0;
+      rps.colmax[g.G / PC * g.P + c] = 0xffffffffu;
+    }
   }
   // the next frame's map is prefetched into registers while this one runs
   constexpr int XV = 8;  // CHW <= 2048 (host check)
@@ -494,6 +551,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
       if (it > 0 && tid_f == 0 && prow) {
         const uint32_t *q = rslot + ((it - 1) & 1) * 4;
         prow[n - (int)gridDim.x] = max(max(q[0], q[1]), max(q[2], q[3]));
+        prow[g.R + n - (int)gridDim.x] = min(min(q[8], q[9]), min(q[10], q[11])) + 1u;
       }
     }
     KCNN_TMARK(5)
@@ -513,6 +571,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
     f16x3::f16x8 bxh[F16 ? FT : 1][F16 ? KS : 1], bxl[F16 ? FT : 1][F16 ? KS : 1];
     float ft[F16 ? FT : 1];  // F16: the unscale factor 2^-(sa + sb(p)) of tile t
     bool slow = false;       // F16: this wave_q's items of the frame in fp32
+    int tsp = 0;             // F16: bit t, tile t has a spread position column
 #pragma unroll
     for (int t = 0; t < FT; t++) {
       if constexpr (F16) {
@@ -524,6 +583,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
         const int pb = (int)px * g.H + (int)py;
         float v[KS][8];
         float m = 0.0f;
+        uint32_t mn = 0xffffffffu;  // min 2|x| - 2 (wrapping: a zero never wins)
 #pragma unroll
         for (int s = 0; s < KS; s++) {
           const int k0 = 16 * s + 8 * h_f;
@@ -539,14 +599,32 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
           for (int e = 0; e < 8; e++) {
             v[s][e] = k0 + e < g.Kdim ? v[s][e] : 0.0f;
             m = fmaxf(m, fabsf(v[s][e]));
+            mn = min(mn, (__float_as_uint(v[s][e]) << 1) - 2u);
           }
         }
         // the column's other half: lane l ^ 32, through ds_bpermute.  (With
         // v_permlane32_swap here, one accumulator register of 16 lanes of a
         // wave's last item came out wrong in about one call in four of a
         // 601-frame forward, G = 96, Kdim 12; experiments/diag_det2.py.)
+#ifdef KCNN_FWD_PERMLANE  // experiment: the swap variant of the hazard study
+        {
+          auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m),
+                                                     false, false);
+#ifdef KCNN_FWD_PERMLANE_NOP  // two wait states between the swap and its readers
+          uint32_t s0 = sw[0], s1 = sw[1];
+          asm volatile("s_nop 1" : "+v"(s0), "+v"(s1));
+          sw[0] = s0;
+          sw[1] = s1;
+#endif
+          m = fmaxf(m, __uint_as_float(h_f ? sw[1] : sw[0]));
+        }
+#else
         m = fmaxf(m, __shfl_xor(m, 32));
+#endif
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, 32));
         const uint32_t mb = __float_as_uint(m);
+        // a spread position column (f16-split.h): the tile's items are checked
+        if (__builtin_amdgcn_ballot_w64(f16x3::spread(mb, (mn >> 1) + 1u)) != 0) tsp |= 1 << t;
         int sb = mb == 0 ? -sa : f16x3::scale_exp(mb);
         const int E = -(sa + sb);
         const bool bad = sb == f16x3::SKIP || E < -149 || E > 127;
@@ -554,7 +632,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
         ft[t] = __builtin_amdgcn_ldexpf(1.0f, bad ? 0 : E);
         if (__builtin_amdgcn_ballot_w64(bad) != 0) slow = true;
 #pragma unroll
-        for (int s = 0; s < KS; s++) f16x3::split8h(v[s], sb, bxh[t][s], bxl[t][s]);
+        for (int s = 0; s < KS; s++) f16x3::split8h(v[s], sb, bxh[t][s], bxl[t][s], m1);
         continue;
       }
       if constexpr (X6) {
@@ -621,6 +699,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
         // sb(p)) + b first, in one rounding; fp32 items: acc * 1 + -0, i.e.
         // acc itself)
         uint32_t rowrun = 0;  // RP: max |pooled| bits of this lane in the frame
+        uint32_t rowmn = 0xffffffffu;  // RP: min (|pooled| - 1) of this lane in the frame
         auto pool_item = [&](floatx16 &acc, int gb, int t, bool sl) {
           const int p = (wave_q + 4 * t) * 32 + l_f;
           // accumulator r = 4k + i of lane (l, h) is filter 8k + 4h + i at
@@ -654,6 +733,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
               acc[4 * k + 2] = fmaf(acc[4 * k + 2], fct, b4.z);
               acc[4 * k + 3] = fmaf(acc[4 * k + 3], fct, b4.w);
             }
+            if (!sl && (wspread || (tsp >> t) & 1))  // uniform, rare
+              spread_check(acc, fct, g, K, ks, bias, Xs, koff, gb, wave_q + 4 * t, lane_f);
           }
           // The pool value by IEEE max (v_max3: NaN skipped like the
           // reference's `val < x` test, ties between equal nonzero values
@@ -687,6 +768,16 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
           if constexpr (RP) {
             // lanes past P hold position P - 1's values: their max lands there
             const int pc = min(p, g.P - 1) + h_f * (4 / PC) * Pq;
+            // the column min bytes: each pooled column has one owner lane
+            // (two for column P - 1, holding the same value), so a plain
+            // read-modify-write (the reads first, one wait for the four)
+            uint32_t old[NGP];
+#pragma unroll
+            for (int j = 0; j < NGP; j++) {
+              const int r0 = j * PC;
+              const int U = (gb * 32 + (r0 & 3) + 8 * (r0 >> 2)) / PC;
+              old[j] = Tmn[U * Pq + pc];
+            }
 #pragma unroll
             for (int j = 0; j < NGP; j++) {
               const uint32_t a = __float_as_uint(mx[j]) & 0x7fffffffu;  // never NaN
@@ -695,10 +786,13 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
               __hip_atomic_fetch_max(Tcol + U * Pq + pc, a, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_WORKGROUP);
               rowrun = max(rowrun, a);
+              const uint32_t u = a - 1u;  // wraps for 0: never the min
+              rowmn = min(rowmn, u);
+              Tmn[U * Pq + pc] = (uint8_t)min(old[j], u >> 23);
             }
             // (pinned per item: left free, the scheduler spreads the items'
             // statistics and holds 34 more VGPRs)
-            asm volatile("" : "+v"(rowrun));
+            asm volatile("" : "+v"(rowrun), "+v"(rowmn));
           }
 #pragma unroll
           for (int j = 0; j < NGP; j++) {
@@ -738,7 +832,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
               floatx16 a = fwd_item_fp32(g, K, ks, bias, Xs, koff, gb, wave_q + 4 * t, lane_f);
               pool_item(a, gb, t, true);
             }
-            if constexpr (RP) frame_row_max(rslot + (it & 1) * 4 + wave_q, rowrun, lane_f);
+            if constexpr (RP) frame_row_max(rslot + (it & 1) * 4 + wave_q, rowrun, rowmn, lane_f);
             KCNN_TMARK(2)
             continue;  // next frame
           }
@@ -773,7 +867,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
             pool_item(a, i / FT, i % FT, false);
           }
         }
-        if constexpr (RP) frame_row_max(rslot + (it & 1) * 4 + wave_q, rowrun, lane_f);
+        if constexpr (RP) frame_row_max(rslot + (it & 1) * 4 + wave_q, rowrun, rowmn, lane_f);
         KCNN_TMARK(2)
         continue;  // next frame
       }
@@ -799,6 +893,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
               acc = f16x3::mfma3(wh[gb][s], wl[gb][s], bxh[t][s], bxl[t][s], acc);
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[r] = fmaf(acc[r], ft[t], bsv[r]);
+            if (wspread || (tsp >> t) & 1)  // uniform, rare
+              spread_check(acc, ft[t], g, K, ks, bias, Xs, koff, gb, pt, lane_f);
           }
         } else if constexpr (X6) {
 #pragma unroll
@@ -951,7 +1047,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
     __syncthreads();
     if (it > 0 && tid == 0 && prow) {
       const uint32_t *q = rslot + ((it - 1) & 1) * 4;
-      prow[blockIdx.x + (it - 1) * (int)gridDim.x] = max(max(q[0], q[1]), max(q[2], q[3]));
+      const int fr = blockIdx.x + (it - 1) * (int)gridDim.x;
+      prow[fr] = max(max(q[0], q[1]), max(q[2], q[3]));
+      prow[g.R + fr] = min(min(q[8], q[9]), min(q[10], q[11])) + 1u;
     }
     if (pcol) {  // exponent bytes (pool_colmax_kernel), four per dword store
       const int npool = g.G / PC * g.P;
@@ -964,6 +1062,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
       } else {
         for (int e = tid; e < npool; e += 256) dst[e] = (uint8_t)(Tcol[e] >> 23);
       }
+      // the minima's bytes after every workgroup's maxima
+      uint8_t *dsn = reinterpret_cast<uint8_t *>(pcol) + ((int64_t)gridDim.x + blockIdx.x) * npool;
+      for (int e = tid; e < npool; e += 256) dsn[e] = Tmn[e];
     }
   }
 #ifdef KCNN_PHASE_TIMING
@@ -2010,16 +2111,20 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
   const unsigned grid = grid_env > 0 ? (unsigned)std::min<int64_t>(grid_env, g.R)
                                      : frame_grid(g, ar ? 2 : fwd_regs_blocks_per_cu(lds));
   static const int dbg = KCNN_KNOB("KCNN_FWD_DEBUG", 0);
-  // the register-pooled-only form: pooled output only, pc 2 / 4, G = 128
-  // and 12 position tiles (each of the 4 waves has 3)
+  // the register-pooled-only form: pooled output only, pc 4, G = 128 and
+  // exactly 12 position tiles, so each of the 4 waves has all 3 (the form
+  // runs every item unfiltered: with 9-11 tiles a wave's third tile would
+  // pool and take statistics from registers no gather wrote)
   const int ntile = (g.P + 31) / 32;
-  const bool rp = out == nullptr && pc == 4 && !win3 && g.G == 128 && ntile > 4 * 2 &&
-                  ntile <= 4 * 3 && ar == 2;
+  // (its LDS: 16 more words of row slots and a min byte per pooled column)
+  const size_t lds_rp = lds + 8 * 4 + ((((size_t)g.G / 4) * g.P + 15) & ~(size_t)15);
+  const bool rp = out == nullptr && pc == 4 && !win3 && g.G == 128 && ntile == 4 * 3 &&
+                  ar == 2 && lds_rp <= (size_t)kFrameLdsMax;
   // the register-pooled kernel also gives the pooled output's max |value|
   // bits per frame and per column (stats, when the caller passes room)
   RpStats rps;
   if (rp && stats && stats->partials &&
-      stats->partial_words * 4 >= (size_t)grid * (g.G / pc) * g.P &&
+      stats->partial_words * 4 >= 2 * (size_t)grid * (g.G / pc) * g.P &&
       (size_t)grid * 256 >= (size_t)(g.G / pc) * g.P) {
     rps.rowmax = stats->rowmax;
     rps.partials = stats->partials;
@@ -2030,7 +2135,7 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
   do {                                                                                       \
     if (rp && PC_ == 4 && AR_ == 2)                                                          \
       hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_, AR_, PC_ == 4 && AR_ == 2>),     \
-                         dim3(grid), dim3(256), lds, st, g, X, xs, K, ks, bias, out, os,     \
+                         dim3(grid), dim3(256), lds_rp, st, g, X, xs, K, ks, bias, out, os,  \
                          vec_ok, dbg, pool, ps, mask, ms, pw3, rps);                         \
     else                                                                                     \
       hipLaunchKernelGGL((conv_fwd_regs_kernel<KS_, 3, PC_, AR_>), dim3(grid), dim3(256), lds, \
@@ -2071,8 +2176,8 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
 
 size_t kcnn_pool_stats_partial_words(const ConvGeom &g, int pc) {
   // frame_grid(g, 2) workgroups (the f16x3 register kernel) x pooled columns
-  // exponent bytes
-  return pc > 0 ? ((size_t)frame_grid(g, 2) * (g.G / pc) * g.P + 3) / 4 : 0;
+  // exponent bytes, for the maxima and the minima
+  return pc > 0 ? (2 * (size_t)frame_grid(g, 2) * (g.G / pc) * g.P + 3) / 4 : 0;
 }
 
 int kcnn_conv_dgrad_frame(const ConvGeom &g, const float *dY, int dys,

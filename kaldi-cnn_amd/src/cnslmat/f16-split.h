@@ -49,41 +49,72 @@ __device__ __forceinline__ int scale_exp(uint32_t mb) {
   return 14 - e;
 }
 
-// a - (float)f16 half of h, in one v_fma_mix_f32 (a * 1.0 - h, exact here:
-// h is a's f16 rounding, so the difference is an fp32 number)
-#ifdef KCNN_F16_NOASM  // experiment: the same differences in plain C
-__device__ __forceinline__ float sub_h0(float a, uint32_t h) {
-  return a - (float)__builtin_bit_cast(f16x2, h)[0];
+// exponent of a finite nonzero |x| bit pattern (subnormals by their leading
+// bit)
+__device__ __forceinline__ int ebits(uint32_t b) {
+  return b >= 0x00800000u ? (int)(b >> 23) - 127 : (31 - (int)__builtin_clz(b)) - 149;
 }
-__device__ __forceinline__ float sub_h1(float a, uint32_t h) {
-  return a - (float)__builtin_bit_cast(f16x2, h)[1];
+// A group is "spread" when its smallest nonzero |x| (bit pattern mn; 0: the
+// group has none) lies below 2^-6 after the group's scale, i.e. more than 20
+// binades under the group's max (mx).  In a group that is not spread every
+// element is held to within 2^-19 of itself (the 2^-25 absolute floor of the
+// lo part over an element of at least 2^-6); a spread group's small
+// elements are held only to 2^-25 absolute (their lo part is an f16
+// subnormal, their hi part too below 2^-14), which a dot product can show
+// when they carry its sum (a large element meeting zeros in the other
+// operand).  The kernels check products that touch a spread group (the GEMM's
+// store, the conv forward's epilogue) and recompute the ones the check
+// cannot clear in fp32.
+__device__ __forceinline__ bool spread(uint32_t mx, uint32_t mn) {
+  return mn != 0 && mx < NONFINITE && ebits(mn) < ebits(mx) - 20;
 }
-#else
-__device__ __forceinline__ float sub_h0(float a, uint32_t h) {
+
+// a - (float)f16 half of h, in one v_fma_mix_f32: fma(h, m1, a) with m1 = -1
+// (exact here: h is a's f16 rounding, so the difference is an fp32 number).
+// m1 comes from opaque_m1(), a -1.0f the compiler cannot fold: folded, the fma
+// becomes a - h, i.e. a v_cvt_f32_f16 and a v_sub_f32 (one VALU more per
+// value); opaque, the fma of an extended f16 is selected as v_fma_mix_f32 with
+// the half picked by op_sel.  The instruction is then the compiler's own, so
+// its hazard recognizer sees it (r04 wrote it as inline asm, which it cannot
+// see through: DESIGN 3, "the f16x3 split and the hazard recognizer").
+__device__ __forceinline__ float opaque_m1() {
+  float v = -1.0f;
+  asm volatile("" : "+s"(v));
+  return v;
+}
+#ifdef KCNN_F16_ASM  // experiment build: r04's inline asm form, for the hazard study
+__device__ __forceinline__ float sub_h0(float a, uint32_t h, float) {
   float r;
   asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(r) : "v"(a), "v"(h));
   return r;
 }
-__device__ __forceinline__ float sub_h1(float a, uint32_t h) {
+__device__ __forceinline__ float sub_h1(float a, uint32_t h, float) {
   float r;
   asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r)
       : "v"(a), "v"(h));
   return r;
 }
+#else
+__device__ __forceinline__ float sub_h0(float a, uint32_t h, float m1) {
+  return __builtin_fmaf((float)__builtin_bit_cast(f16x2, h)[0], m1, a);
+}
+__device__ __forceinline__ float sub_h1(float a, uint32_t h, float m1) {
+  return __builtin_fmaf((float)__builtin_bit_cast(f16x2, h)[1], m1, a);
+}
 #endif
 // (x0 * 2^e0, x1 * 2^e1) -> packed f16 pairs hi, lo: 6 VALU
 __device__ __forceinline__ void split2h(float x0, float x1, int e0, int e1, uint32_t &h,
-                                        uint32_t &l) {
+                                        uint32_t &l, float m1) {
   const float a = __builtin_amdgcn_ldexpf(x0, e0), b = __builtin_amdgcn_ldexpf(x1, e1);
   h = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, f16x2));
-  l = __builtin_bit_cast(uint32_t,
-                         __builtin_convertvector((f32x2){sub_h0(a, h), sub_h1(b, h)}, f16x2));
+  l = __builtin_bit_cast(uint32_t, __builtin_convertvector(
+                                       (f32x2){sub_h0(a, h, m1), sub_h1(b, h, m1)}, f16x2));
 }
 // eight values under one scale -> the hi and lo f16x8 fragments
-__device__ __forceinline__ void split8h(const float *v, int e, f16x8 &h, f16x8 &l) {
+__device__ __forceinline__ void split8h(const float *v, int e, f16x8 &h, f16x8 &l, float m1) {
   uint32_t hh[4], ll[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) split2h(v[2 * i], v[2 * i + 1], e, e, hh[i], ll[i]);
+  for (int i = 0; i < 4; ++i) split2h(v[2 * i], v[2 * i + 1], e, e, hh[i], ll[i], m1);
   h = __builtin_bit_cast(f16x8, make_uint4(hh[0], hh[1], hh[2], hh[3]));
   l = __builtin_bit_cast(f16x8, make_uint4(ll[0], ll[1], ll[2], ll[3]));
 }

@@ -71,13 +71,15 @@ constexpr int ROWB = BK * 2;                  // bytes per LDS row of one plane
 constexpr int A_PLANE = BM * ROWB;            // 16 KB
 constexpr int B_PLANE = BN * ROWB;            // 8 KB
 constexpr int BUF = 2 * (A_PLANE + B_PLANE);  // 48 KB
-constexpr int LDS_BYTES = 2 * BUF + (BM + BN) * 4;
+constexpr int LDS_BYTES = 2 * BUF + (BM + BN) * 8;  // + sexp, sw
 
 struct GemmF16Args {
   const float *A, *B;
   float *C;                      // the output
   float *part;                   // ksplit > 1: the partial slabs [ksplit][M][N]
   const uint32_t *amax, *bmax;   // max |x| bits per row of op(A), per column of op(B)
+  const uint32_t *amin, *bmin;   // min nonzero |x| bits (0: none), the same groups
+  float wspread;                 // a spread group's weight in the store's check (tile_epilogue)
   const float *bias;             // nullable: C += bias[col] on every row (after alpha, beta)
   int M, N, K, lda, ldb, ldc;
   int kps, ksplit, tiles_m, tiles_n;
@@ -182,7 +184,7 @@ struct Loader {
   // partial; without it no masking code is emitted -- the compiler turns
   // the uniform kv test into per-element selects)
   template <int PL, bool RAG>
-  __device__ __forceinline__ void store(char *lds, int tid, int kv) const {
+  __device__ __forceinline__ void store(char *lds, int tid, int kv, float m1) const {
 #pragma unroll
     for (int u = 0; u < UPT; ++u) {
       const int unit = tid + u * NT;
@@ -201,8 +203,8 @@ struct Loader {
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
           uint32_t h0, l0, h1, l1;
-          split2h(x[4 * j], x[4 * j + 1], e[0], e[1], h0, l0);
-          split2h(x[4 * j + 2], x[4 * j + 3], e[2], e[3], h1, l1);
+          split2h(x[4 * j], x[4 * j + 1], e[0], e[1], h0, l0, m1);
+          split2h(x[4 * j + 2], x[4 * j + 3], e[2], e[3], h1, l1, m1);
           const int o = tswz<R>(kq * KPT + j, 4 * rq);
           *reinterpret_cast<uint2 *>(lds + o) = make_uint2(h0, h1);
           *reinterpret_cast<uint2 *>(lds + PL + o) = make_uint2(l0, l1);
@@ -228,7 +230,7 @@ struct Loader {
           uint32_t h[4], l[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            split2h(x[cc * 8 + 2 * i], x[cc * 8 + 2 * i + 1], e[u], e[u], h[i], l[i]);
+            split2h(x[cc * 8 + 2 * i], x[cc * 8 + 2 * i + 1], e[u], e[u], h[i], l[i], m1);
           const int off = swz(r, c0 + cc);
           *reinterpret_cast<uint4 *>(lds + off) = make_uint4(h[0], h[1], h[2], h[3]);
           *reinterpret_cast<uint4 *>(lds + PL + off) = make_uint4(l[0], l[1], l[2], l[3]);
@@ -244,7 +246,7 @@ struct Loader {
   static constexpr int NPIECE = MODE == LT ? 2 * KPT : UPT * (KPT / 2);
   template <int PL, bool RAG>
   __device__ __forceinline__ void piece(char *lds, int tid, int pc, int kv, uint32_t (&ph)[4],
-                                        uint32_t (&pl)[4]) const {
+                                        uint32_t (&pl)[4], float m1) const {
     if constexpr (MODE == LT) {
       const int j = pc >> 1, hf = pc & 1;
       const int unit = tid;
@@ -254,7 +256,7 @@ struct Loader {
         asm volatile("");  // a branch: not per-element selects in every K step
         if (kq * KPT + j >= kv) x0 = x1 = 0.0f;
       }
-      split2h(x0, x1, e[2 * hf], e[2 * hf + 1], ph[hf], pl[hf]);
+      split2h(x0, x1, e[2 * hf], e[2 * hf + 1], ph[hf], pl[hf], m1);
       if (hf == 1) {
         const int o = tswz<R>(kq * KPT + j, 4 * rq);
         *reinterpret_cast<uint2 *>(lds + o) = make_uint2(ph[0], ph[1]);
@@ -280,7 +282,7 @@ struct Loader {
         if (kb + 2 * q >= kv) x0 = 0.0f;
         if (kb + 2 * q + 1 >= kv) x1 = 0.0f;
       }
-      split2h(x0, x1, e[u], e[u], ph[q & 3], pl[q & 3]);
+      split2h(x0, x1, e[u], e[u], ph[q & 3], pl[q & 3], m1);
       if ((q & 3) == 3) {
         const int off = swz(r, c0 + (q >> 2));
         *reinterpret_cast<uint4 *>(lds + off) = make_uint4(ph[0], ph[1], ph[2], ph[3]);
@@ -310,22 +312,78 @@ struct Loader {
 };
 
 
-// The scale exponents of the tile's rows and columns into sexp; true (for
-// the whole block) when one of them is an Inf / NaN row or column
-__device__ __forceinline__ bool tile_scales(const GemmF16Args &p, int *sexp, int row0, int col0,
-                                            int tid) {
-  int skip = 0;
+// The scale exponents of the tile's rows and columns into sexp, and each
+// one's spread weight into sw (wspread for a spread group, f16-split.h
+// spread(), else 0).  Returns bit 0: one of them is an Inf / NaN row or
+// column; bit 1: one of them is spread (both for the whole block).
+__device__ __forceinline__ int tile_scales(const GemmF16Args &p, int *sexp, float *sw, int row0,
+                                           int col0, int tid) {
+  int skip = 0, spr = 0;
   for (int i = tid; i < BM + BN; i += NT) {
     int s = 0;
+    float w = 0.0f;
     if (i < BM) {
-      if (row0 + i < p.M) s = scale_exp(p.amax[row0 + i]);
+      if (row0 + i < p.M) {
+        s = scale_exp(p.amax[row0 + i]);
+        if (kcnn::f16x3::spread(p.amax[row0 + i], p.amin[row0 + i])) w = p.wspread;
+      }
     } else if (col0 + i - BM < p.N) {
       s = scale_exp(p.bmax[col0 + i - BM]);
+      if (kcnn::f16x3::spread(p.bmax[col0 + i - BM], p.bmin[col0 + i - BM])) w = p.wspread;
     }
     sexp[i] = s;
+    sw[i] = w;
     skip |= s == SKIP;
+    spr |= w != 0.0f;
   }
-  return __syncthreads_or(skip) != 0;
+  const int any_skip = __syncthreads_or(skip) != 0;
+  return any_skip | (__syncthreads_or(spr) != 0 ? 2 : 0);
+}
+
+// One C element by a whole wave, for the store's check (called with the same
+// row and column in every lane): fp32 products of op(A) row i and op(B)
+// column j, lane l summing k = l, l + 64, ... in order, then a butterfly over
+// the lanes (every lane ends with the same bits: deterministic)
+__device__ __forceinline__ float wave_dot(const GemmF16Args &p, bool a_kc, bool b_kc, int row,
+                                          int col, int lane) {
+  float s = 0.0f;
+  for (int k = lane; k < p.K; k += 64) {
+    const float a = a_kc ? p.A[(int64_t)row * p.lda + k] : p.A[(int64_t)k * p.lda + row];
+    const float b = b_kc ? p.B[(int64_t)col * p.ldb + k] : p.B[(int64_t)k * p.ldb + col];
+    s = fmaf(a, b, s);
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+  return s;
+}
+__device__ __forceinline__ float store_value(const GemmF16Args &p, float v, float *o, int col) {
+  float r = p.beta == 0.0f ? p.alpha * v : p.alpha * v + p.beta * *o;
+  if (p.bias) r += p.bias[col];
+  return r;
+}
+// The elements a lane's check rejected (bit n of `mine` its n-th candidate,
+// decode(lane, n) -> (row, col)), each recomputed by the whole wave
+// (wave_dot) and stored: a wave-uniform loop over the wave's rejections
+template <typename Decode>
+__device__ __forceinline__ void fix_rejected(const GemmF16Args &p, bool a_kc, bool b_kc,
+                                             uint64_t mine, int lane, Decode decode) {
+  for (;;) {
+    const uint64_t who = __ballot(mine != 0);
+    if (who == 0) break;
+    const int l = __builtin_ctzll(who);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)mine, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(mine >> 32), l);
+    const uint64_t bits = ((uint64_t)hi << 32) | lo;
+    const int n = __builtin_ctzll(bits);
+    int row, col;
+    decode(l, n, row, col);
+    const float v = wave_dot(p, a_kc, b_kc, row, col, lane);
+    if (lane == 0) {
+      float *o = p.C + (int64_t)row * p.ldc + col;
+      *o = store_value(p, v, o, col);
+    }
+    if (lane == l) mine &= mine - 1;
+  }
 }
 
 // The tile's results.  C/D map of 32x32x16: register g of lane l holds row
@@ -343,14 +401,21 @@ __device__ __forceinline__ bool tile_scales(const GemmF16Args &p, int *sexp, int
 //    (IEEE Inf / NaN, the reference sgemm's pattern).
 template <bool A_KC, bool B_KC>
 __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *sexp,
-                                              const f32x16 (&acc)[2][2], int split, int row0,
-                                              int col0, bool skip, int tid) {
+                                              const float *sw, const f32x16 (&acc)[2][2],
+                                              int split, int row0, int col0, int flags, int tid) {
   const int lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
   const int half2 = lane >> 5;
   const bool partial = p.ksplit > 1;
+  const bool skip = flags & 1;
+  // the spread check (f16-split.h): with a spread row or column in the tile
+  // and one split, an element whose |acc| is below its threshold is
+  // recomputed in fp32 (fix_rejected) instead of stored; split K checks the
+  // summed value in gemm_f16x3_reduce_kernel
+  const bool check = (flags & 2) && !partial;
   const int np4 = (p.N + 3) & ~3;  // partial slab pitch (16-B rows)
   float *slab = partial ? p.part + (int64_t)split * p.M * np4 : p.C;
   const int ldo = partial ? np4 : p.ldc;
+  uint64_t rej = 0;  // bit (2 i + j) * 16 + g: that element is rejected
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -359,23 +424,31 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
       const int col = col0 + cl;
       const int ec = sexp[BM + cl];
       if (col >= p.N || ec == SKIP) continue;
+      const float wc = check ? sw[BM + cl] : 0.0f;
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int rl = wm * 64 + i * 32 + (g & 3) + 8 * (g >> 2) + 4 * half2;
         const int row = row0 + rl;
         const int er = sexp[rl];
         if (row >= p.M || er == SKIP) continue;
+        if (check) {
+          const float thr = wc + sw[rl];
+          if (thr != 0.0f && !(fabsf(acc[i][j][g]) >= thr)) {
+            rej |= (uint64_t)1 << ((2 * i + j) * 16 + g);
+            continue;
+          }
+        }
         const float v = __builtin_amdgcn_ldexpf(acc[i][j][g], -(er + ec));
         float *o = slab + (int64_t)row * ldo + col;
-        if (partial) {
-          *o = v;
-        } else {
-          float r = p.beta == 0.0f ? p.alpha * v : p.alpha * v + p.beta * *o;
-          if (p.bias) r += p.bias[col];
-          *o = r;
-        }
+        *o = partial ? v : store_value(p, v, o, col);
       }
     }
+  if (check)
+    fix_rejected(p, A_KC, B_KC, rej, lane, [&](int l, int n, int &row, int &col) {
+      const int i = n >> 5, j = (n >> 4) & 1, g = n & 15;
+      row = row0 + wm * 64 + i * 32 + (g & 3) + 8 * (g >> 2) + 4 * (l >> 5);
+      col = col0 + wn * 64 + j * 32 + (l & 31);
+    });
   if (skip && split == 0) {
     for (int e = tid; e < BM * BN; e += NT) {
       const int rl = e / BN, cl = e - rl * BN;
@@ -389,9 +462,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
         sum = fmaf(a, b, sum);
       }
       float *o = p.C + (int64_t)row * p.ldc + col;
-      float r = p.beta == 0.0f ? p.alpha * sum : p.alpha * sum + p.beta * *o;
-      if (p.bias) r += p.bias[col];
-      *o = r;
+      *o = store_value(p, sum, o, col);
     }
   }
 }
@@ -401,7 +472,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
   constexpr bool A_KC = AM == LK, B_KC = BMODE == LK;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int *sexp = reinterpret_cast<int *>(lds + 2 * BUF);  // [BM] rows, then [BN] columns
+  float *sw = reinterpret_cast<float *>(sexp + BM + BN);  // spread weights, the same order
   const int tid = threadIdx.x;
+  const float m1 = kcnn::f16x3::opaque_m1();
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   // XCD-aware order (gemm_x6_kernel): consecutive logical ids on one XCD
@@ -417,7 +490,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
   const int T = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   const int klast = kend - kbeg - (T - 1) * BK;  // valid k of the last tile
 
-  const bool skip = tile_scales(p, sexp, row0, col0, tid);
+  const int flags = tile_scales(p, sexp, sw, row0, col0, tid);
 
   // descriptors whose range ends at the operand's last element: a partial
   // last tile reads 0 past it (and the split zeroes the pitch's padding)
@@ -425,9 +498,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
   const float *baseB = B_KC ? p.B + (int64_t)col0 * p.ldb : p.B + (int64_t)kbeg * p.ldb + col0;
   const int vra = p.M - row0, vrb = p.N - col0;
   const int64_t endA = A_KC ? ((int64_t)(vra - 1) * p.lda + p.K) * 4
-                            : ((int64_t)(p.K - 1 - kbeg) * p.lda + ((vra + 3) & ~3)) * 4;
+                            : ((int64_t)(p.K - 1 - kbeg) * p.lda + vra) * 4;
   const int64_t endB = B_KC ? ((int64_t)(vrb - 1) * p.ldb + p.K) * 4
-                            : ((int64_t)(p.K - 1 - kbeg) * p.ldb + ((vrb + 3) & ~3)) * 4;
+                            : ((int64_t)(p.K - 1 - kbeg) * p.ldb + vrb) * 4;
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
       (void *)baseA, (short)0, (int)(endA < 0x7fffffff ? endA : 0x7fffffff), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
@@ -454,8 +527,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
   if (T > 0) {
     la[0].load(rsA, p.lda, vra, kk(0, A_KC), tid);
     lb[0].load(rsB, p.ldb, vrb, kk(0, B_KC), tid);
-    la[0].template store<A_PLANE, RAG>(lds, tid, T == 1 ? klast : BK);
-    lb[0].template store<B_PLANE, RAG>(lds + 2 * A_PLANE, tid, T == 1 ? klast : BK);
+    la[0].template store<A_PLANE, RAG>(lds, tid, T == 1 ? klast : BK, m1);
+    lb[0].template store<B_PLANE, RAG>(lds + 2 * A_PLANE, tid, T == 1 ? klast : BK, m1);
     // tiles 1, 2 into sets 1, 0 (as at every later loop entry)
     __builtin_amdgcn_sched_barrier(0);
     la[1].load(rsA, p.lda, vra, kk(1, A_KC), tid);
@@ -501,13 +574,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
         const int kv = t + 2 == T ? klast : BK;
         half_step(buf, 0);
         if (!late && t + 1 < T) {
-          lan.template store<A_PLANE, RAG>(nA, tid, kv);
-          lbn.template store<B_PLANE, RAG>(nA + 2 * A_PLANE, tid, kv);
+          lan.template store<A_PLANE, RAG>(nA, tid, kv, m1);
+          lbn.template store<B_PLANE, RAG>(nA + 2 * A_PLANE, tid, kv, m1);
         }
         half_step(buf, 1);
         if (late && t + 1 < T) {
-          lan.template store<A_PLANE, RAG>(nA, tid, kv);
-          lbn.template store<B_PLANE, RAG>(nA + 2 * A_PLANE, tid, kv);
+          lan.template store<A_PLANE, RAG>(nA, tid, kv, m1);
+          lbn.template store<B_PLANE, RAG>(nA + 2 * A_PLANE, tid, kv, m1);
         }
       }
       lan.load(rsA, p.lda, vra, kk(t + 3, A_KC), tid);
@@ -520,7 +593,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
     }
   }
 
-  tile_epilogue<A_KC, B_KC>(p, sexp, acc, split, row0, col0, skip, tid);
+  tile_epilogue<A_KC, B_KC>(p, sexp, sw, acc, split, row0, col0, flags, tid);
 }
 
 // ---------------------------------------------------------------------------
@@ -546,7 +619,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
   constexpr bool A_KC = AM == LK, B_KC = BMODE == LK;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int *sexp = reinterpret_cast<int *>(lds + 2 * BUF);
+  float *sw = reinterpret_cast<float *>(sexp + BM + BN);
   const int tid = threadIdx.x;
+  const float m1 = kcnn::f16x3::opaque_m1();
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int nb = gridDim.x, b = blockIdx.x;
@@ -561,14 +636,14 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
   const int T = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   const int klast = kend - kbeg - (T - 1) * BK;
 
-  const bool skip = tile_scales(p, sexp, row0, col0, tid);
+  const int flags = tile_scales(p, sexp, sw, row0, col0, tid);
   const float *baseA = A_KC ? p.A + (int64_t)row0 * p.lda : p.A + (int64_t)kbeg * p.lda + row0;
   const float *baseB = B_KC ? p.B + (int64_t)col0 * p.ldb : p.B + (int64_t)kbeg * p.ldb + col0;
   const int vra = p.M - row0, vrb = p.N - col0;
   const int64_t endA = A_KC ? ((int64_t)(vra - 1) * p.lda + p.K) * 4
-                            : ((int64_t)(p.K - 1 - kbeg) * p.lda + ((vra + 3) & ~3)) * 4;
+                            : ((int64_t)(p.K - 1 - kbeg) * p.lda + vra) * 4;
   const int64_t endB = B_KC ? ((int64_t)(vrb - 1) * p.ldb + p.K) * 4
-                            : ((int64_t)(p.K - 1 - kbeg) * p.ldb + ((vrb + 3) & ~3)) * 4;
+                            : ((int64_t)(p.K - 1 - kbeg) * p.ldb + vrb) * 4;
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
       (void *)baseA, (short)0, (int)(endA < 0x7fffffff ? endA : 0x7fffffff), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
@@ -613,8 +688,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
   if (T > 0) {
     la[0].load(rsA, p.lda, vra, kk(0, A_KC), tid);
     lb[0].load(rsB, p.ldb, vrb, kk(0, B_KC), tid);
-    la[0].template store<A_PLANE, RAG>(lds, tid, T == 1 ? klast : BK);
-    lb[0].template store<B_PLANE, RAG>(lds + 2 * A_PLANE, tid, T == 1 ? klast : BK);
+    la[0].template store<A_PLANE, RAG>(lds, tid, T == 1 ? klast : BK, m1);
+    lb[0].template store<B_PLANE, RAG>(lds + 2 * A_PLANE, tid, T == 1 ? klast : BK, m1);
     __builtin_amdgcn_sched_barrier(0);
     la[1].load(rsA, p.lda, vra, kk(1, A_KC), tid);
     lb[1].load(rsB, p.ldb, vrb, kk(1, B_KC), tid);
@@ -639,9 +714,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
         mfma_n(n, fa0, fb0);
         if (more) {
           if (n < LA::NPIECE)
-            lan.template piece<A_PLANE, RAG>(nbuf, tid, n, kv, ph, pl);
+            lan.template piece<A_PLANE, RAG>(nbuf, tid, n, kv, ph, pl, m1);
           else if (n - LA::NPIECE < LB::NPIECE)
-            lbn.template piece<B_PLANE, RAG>(nbuf + 2 * A_PLANE, tid, n - LA::NPIECE, kv, ph, pl);
+            lbn.template piece<B_PLANE, RAG>(nbuf + 2 * A_PLANE, tid, n - LA::NPIECE, kv, ph, pl, m1);
         }
         if (n >= 2 && n < 10) read_frag(buf, 1, n - 2, fa1, fb1);
         __builtin_amdgcn_sched_barrier(0);
@@ -665,12 +740,18 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
     if (t < T) step(t, la[1], lb[1]);
   }
 
-  tile_epilogue<A_KC, B_KC>(p, sexp, acc, split, row0, col0, skip, tid);
+  tile_epilogue<A_KC, B_KC>(p, sexp, sw, acc, split, row0, col0, flags, tid);
 }
 
-// Max |x| per row or per column of a pitched fp32 matrix, as the bit
-// patterns of |x| (unsigned order = magnitude order, Inf / NaN above every
-// finite value; max is order-independent, so the results are deterministic).
+// Max |x| and min nonzero |x| per row or per column of a pitched fp32 matrix,
+// as the bit patterns of |x| (unsigned order = magnitude order, Inf / NaN
+// above every finite value; max and min are order-independent, so the
+// results are deterministic).  A group's statistics block is [max[n], min[n]]
+// (n groups): max[i] sets the group's f16x3 scale, min[i] (0: no nonzero
+// element) says whether the group is "spread" (f16-split.h: an element far
+// enough below the max to lose low bits, which the GEMM's store then checks,
+// tile_epilogue).  The min is taken as min(|x| - 1) in wrapping unsigned
+// arithmetic, so a zero (0 - 1 = 0xffffffff) never wins, then + 1.
 // A GEMM needs op(A)'s rows and op(B)'s columns; both operands' statistics
 // go in one launch (stats_kernel: blocks [0, a.blocks) for A, then B's) and
 // one more (stats_finalize_kernel) when either is per column:
@@ -678,13 +759,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
 //    four in flight), a wave reduction and an LDS step;
 //  rows, shorter rows: a wave per row;
 //  columns: block (cb, rc) covers 1024 columns (4 per thread) of a chunk of
-//    rows (8 in flight) and stores its column maxima as partial rc; the
-//    finalize takes the maxima over the chunks (64 columns x 4 chunk groups
-//    per block, combined through LDS).
+//    rows (8 in flight) and stores its column maxima and minima as partial
+//    rc; the finalize takes the maxima / minima over the chunks (64 columns
+//    x 4 chunk groups per block, combined through LDS).
 struct StatOp {
   const float *X;
-  uint32_t *out;   // maxima per row (mode 0) or per column (mode 1)
-  uint32_t *part;  // mode 1: [rbk][cols] partials
+  uint32_t *out;   // the statistics block: maxima then minima, per row (mode 0) or column (1)
+  uint32_t *part;  // mode 1: [2][rbk][cols] partials (maxima, then minima - 1)
   int rows, cols, ld, mode, vec;
   int blocks;      // of stats_kernel
   int rpb;         // mode 0: rows per block (4: a wave each; 1: a block)
@@ -695,10 +776,17 @@ __device__ __forceinline__ const float *X_row(const StatOp &o, int r) {
   return o.X + (int64_t)r * o.ld;
 }
 
-__device__ __forceinline__ uint32_t amax4(uint32_t m, float4 q) {
-  return max(max(m, __float_as_uint(q.x) & 0x7fffffffu),
-             max(max(__float_as_uint(q.y) & 0x7fffffffu, __float_as_uint(q.z) & 0x7fffffffu),
-                 __float_as_uint(q.w) & 0x7fffffffu));
+// running max |x| (m) and min (|x| - 1) (n) over a float4
+__device__ __forceinline__ void mm4(uint32_t &m, uint32_t &n, float4 q) {
+  const uint32_t a = __float_as_uint(q.x) & 0x7fffffffu, b = __float_as_uint(q.y) & 0x7fffffffu,
+                 c = __float_as_uint(q.z) & 0x7fffffffu, d = __float_as_uint(q.w) & 0x7fffffffu;
+  m = max(max(m, a), max(max(b, c), d));
+  n = min(min(n, a - 1u), min(min(b - 1u, c - 1u), d - 1u));
+}
+__device__ __forceinline__ void mm1(uint32_t &m, uint32_t &n, float x) {
+  const uint32_t a = __float_as_uint(x) & 0x7fffffffu;
+  m = max(m, a);
+  n = min(n, a - 1u);
 }
 
 __device__ __forceinline__ void stats_rows(const StatOp &o, int blk, uint32_t *red) {
@@ -709,30 +797,42 @@ __device__ __forceinline__ void stats_rows(const StatOp &o, int blk, uint32_t *r
   const float *x = X_row(o, r);
   const int step = wide ? 1024 : 256;  // floats per sweep of the row
   int c = (wide ? threadIdx.x : lane) * 4;
-  uint32_t m = 0;
+  uint32_t m = 0, n = 0xffffffffu;
   if (o.vec) {
     for (; c + 3 * step + 4 <= o.cols; c += 4 * step) {
       float4 q[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) q[j] = *reinterpret_cast<const float4 *>(x + c + j * step);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) m = amax4(m, q[j]);
+      for (int j = 0; j < 4; ++j) mm4(m, n, q[j]);
     }
-    for (; c + 4 <= o.cols; c += step) m = amax4(m, *reinterpret_cast<const float4 *>(x + c));
+    for (; c + 4 <= o.cols; c += step) mm4(m, n, *reinterpret_cast<const float4 *>(x + c));
   }
   for (; c < o.cols; c += step)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if (c + i < o.cols) m = max(m, __float_as_uint(x[c + i]) & 0x7fffffffu);
+      if (c + i < o.cols) mm1(m, n, x[c + i]);
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
+  for (int d = 32; d >= 1; d >>= 1) {
+    m = max(m, (uint32_t)__shfl_xor((int)m, d));
+    n = min(n, (uint32_t)__shfl_xor((int)n, d));
+  }
   if (!wide) {
-    if (lane == 0) o.out[r] = m;
+    if (lane == 0) {
+      o.out[r] = m;
+      o.out[o.rows + r] = n + 1u;
+    }
     return;
   }
-  if (lane == 0) red[wave] = m;
+  if (lane == 0) {
+    red[wave] = m;
+    red[4 + wave] = n;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) o.out[r] = max(max(red[0], red[1]), max(red[2], red[3]));
+  if (threadIdx.x == 0) {
+    o.out[r] = max(max(red[0], red[1]), max(red[2], red[3]));
+    o.out[o.rows + r] = min(min(red[4], red[5]), min(red[6], red[7])) + 1u;
+  }
 }
 
 __device__ __forceinline__ void stats_cols(const StatOp &o, int blk) {
@@ -742,6 +842,7 @@ __device__ __forceinline__ void stats_cols(const StatOp &o, int blk) {
   if (c0 >= o.cols) return;
   const bool v4 = o.vec && c0 + 4 <= o.cols;
   uint32_t cm[4] = {0u, 0u, 0u, 0u};
+  uint32_t cn[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
   auto load = [&](int r) {
     const float *x = X_row(o, r) + c0;
     if (v4) return *reinterpret_cast<const float4 *>(x);
@@ -753,10 +854,10 @@ __device__ __forceinline__ void stats_cols(const StatOp &o, int blk) {
     return q;
   };
   auto take = [&](float4 q) {
-    cm[0] = max(cm[0], __float_as_uint(q.x) & 0x7fffffffu);
-    cm[1] = max(cm[1], __float_as_uint(q.y) & 0x7fffffffu);
-    cm[2] = max(cm[2], __float_as_uint(q.z) & 0x7fffffffu);
-    cm[3] = max(cm[3], __float_as_uint(q.w) & 0x7fffffffu);
+    mm1(cm[0], cn[0], q.x);
+    mm1(cm[1], cn[1], q.y);
+    mm1(cm[2], cn[2], q.z);
+    mm1(cm[3], cn[3], q.w);
   };
   int r = r0;
   for (; r + 8 <= rend; r += 8) {
@@ -768,13 +869,17 @@ __device__ __forceinline__ void stats_cols(const StatOp &o, int blk) {
   }
   for (; r < rend; ++r) take(load(r));
   uint32_t *dst = o.part + (size_t)rci * o.cols + c0;
+  uint32_t *dsn = dst + (size_t)o.rbk * o.cols;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    if (c0 + i < o.cols) dst[i] = cm[i];
+    if (c0 + i < o.cols) {
+      dst[i] = cm[i];
+      dsn[i] = cn[i];
+    }
 }
 
 __global__ __launch_bounds__(256) void stats_kernel(StatOp a, StatOp b) {
-  __shared__ uint32_t red[4];
+  __shared__ uint32_t red[8];
   const bool isa = (int)blockIdx.x < a.blocks;  // uniform
   const StatOp &o = isa ? a : b;
   const int blk = isa ? blockIdx.x : blockIdx.x - a.blocks;
@@ -783,26 +888,29 @@ __global__ __launch_bounds__(256) void stats_kernel(StatOp a, StatOp b) {
 }
 
 __global__ __launch_bounds__(256) void stats_finalize_kernel(StatOp a, StatOp b) {
-  __shared__ uint32_t red[4][64];
+  __shared__ uint32_t red[2][4][64];
   const int fa = a.mode == 1 ? a.fblocks : 0;
   const bool isa = (int)blockIdx.x < fa;
   const StatOp &o = isa ? a : b;
   const int blk = isa ? blockIdx.x : blockIdx.x - fa;
   const int c = blk * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
-  uint32_t m = 0;
+  uint32_t m = 0, n = 0xffffffffu;
   if (c < o.cols) {
-    int q = grp;
-    for (; q + 12 < o.rbk; q += 16)
-      m = max(max(m, o.part[(size_t)q * o.cols + c]),
-              max(max(o.part[(size_t)(q + 4) * o.cols + c], o.part[(size_t)(q + 8) * o.cols + c]),
-                  o.part[(size_t)(q + 12) * o.cols + c]));
-    for (; q < o.rbk; q += 4) m = max(m, o.part[(size_t)q * o.cols + c]);
+    const uint32_t *pm = o.part, *pn = o.part + (size_t)o.rbk * o.cols;
+    for (int q = grp; q < o.rbk; q += 4) {
+      m = max(m, pm[(size_t)q * o.cols + c]);
+      n = min(n, pn[(size_t)q * o.cols + c]);
+    }
   }
-  red[grp][threadIdx.x & 63] = m;
+  red[0][grp][threadIdx.x & 63] = m;
+  red[1][grp][threadIdx.x & 63] = n;
   __syncthreads();
-  if (grp == 0 && c < o.cols)
-    o.out[c] = max(max(red[0][threadIdx.x], red[1][threadIdx.x]),
-                   max(red[2][threadIdx.x], red[3][threadIdx.x]));
+  if (grp == 0 && c < o.cols) {
+    o.out[c] = max(max(red[0][0][threadIdx.x], red[0][1][threadIdx.x]),
+                   max(red[0][2][threadIdx.x], red[0][3][threadIdx.x]));
+    o.out[o.cols + c] = min(min(red[1][0][threadIdx.x], red[1][1][threadIdx.x]),
+                            min(red[1][2][threadIdx.x], red[1][3][threadIdx.x])) + 1u;
+  }
 }
 
 // a statistics pass over X (rows x cols, pitch ld): mode 0 per row, 1 per
@@ -831,14 +939,14 @@ StatOp stat_op(const float *X, int rows, int cols, int ld, int mode, uint32_t *o
 size_t stat_part_words(int rows, int cols, int mode) {
   if (mode == 0) return 0;
   const StatOp o = stat_op(nullptr, rows, cols, cols, 1, nullptr, nullptr);
-  return (size_t)o.rbk * cols;
+  return 2 * (size_t)o.rbk * cols;
 }
 int stats_launch(const StatOp &a, const StatOp &b, hipStream_t st) {
-  // empty operands: maxima 0 (no scale)
+  // empty operands: maxima 0 (no scale), minima 0 (no nonzero element)
   for (const StatOp *o : {&a, &b})
     if (o->blocks == 0 && o->out) {
       const size_t n = o->mode == 0 ? (size_t)std::max(o->rows, 0) : (size_t)std::max(o->cols, 0);
-      if (n && hipMemsetAsync(o->out, 0, n * 4, st) != hipSuccess) return (int)hipGetLastError();
+      if (n && hipMemsetAsync(o->out, 0, 2 * n * 4, st) != hipSuccess) return (int)hipGetLastError();
     }
   const int nb = a.blocks + b.blocks;
   if (nb == 0) return 0;
@@ -857,49 +965,82 @@ int stats_launch(const StatOp &a, const StatOp &b, hipStream_t st) {
 // C = alpha * sum_s part[s] + beta * C, the splits added in increasing s
 // (slab rows padded to np4 = N rounded up to 4: 16-B reads; a quad's columns
 // past N are not stored); elements of an Inf / NaN row or column are the
-// epilogue's (split 0)
-__global__ void gemm_f16x3_reduce_kernel(const float *__restrict__ part, int S, int M, int N,
-                                         float alpha, float beta, float *C, int ldc,
-                                         const uint32_t *__restrict__ amax,
-                                         const uint32_t *__restrict__ bmax,
-                                         const float *__restrict__ bias) {
+// epilogue's (split 0).  The spread check of tile_epilogue on the summed
+// value (unscaled: the threshold times 2^-(s_row + s_col)); rejected elements
+// are recomputed by their wave (fix_rejected).  The grid-stride loop runs a
+// block-uniform number of times, so every lane of a wave reaches the fix.
+__global__ void gemm_f16x3_reduce_kernel(GemmF16Args p, int a_kc, int b_kc) {
+  const int S = p.ksplit, M = p.M, N = p.N;
   const int np4 = (N + 3) & ~3, nq = np4 >> 2;
   const int64_t total = (int64_t)M * nq;
   const int64_t plane = (int64_t)M * np4;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int r = (int)(e / nq), c = (int)(e - (int64_t)r * nq) * 4;
-    const float *q = part + (int64_t)r * np4 + c;
-    float4 v = *reinterpret_cast<const float4 *>(q);
-    for (int k = 1; k < S; ++k) {
-      const float4 w = *reinterpret_cast<const float4 *>(q + k * plane);
-      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
-    }
-    if (amax[r] >= NONFINITE) continue;
-    const float sv[4] = {v.x, v.y, v.z, v.w};
-    float *o = C + (int64_t)r * ldc + c;
-    const bool fin = c + 4 <= N && max(max(bmax[c], bmax[c + 1]), max(bmax[c + 2], bmax[c + 3])) <
-                                       NONFINITE;
-    if (fin && ((ldc & 3) | ((uintptr_t)C & 15)) == 0) {  // one 16-B store (same values)
-      float4 ov = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      if (beta != 0.0f) ov = *reinterpret_cast<const float4 *>(o);
-      const float oi[4] = {ov.x, ov.y, ov.z, ov.w};
-      float w[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        w[i] = beta == 0.0f ? alpha * sv[i] : alpha * sv[i] + beta * oi[i];
-        if (bias) w[i] += bias[c + i];
+  const int lane = threadIdx.x & 63;
+  for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < total;
+       base += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = base + threadIdx.x;
+    int r = 0, c = 0;
+    uint64_t rej = 0;  // bit i: column c + i is rejected
+    if (e < total) {
+      r = (int)(e / nq);
+      c = (int)(e - (int64_t)r * nq) * 4;
+      const float *q = p.part + (int64_t)r * np4 + c;
+      float4 v = *reinterpret_cast<const float4 *>(q);
+      for (int k = 1; k < S; ++k) {
+        const float4 w = *reinterpret_cast<const float4 *>(q + k * plane);
+        v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
       }
-      *reinterpret_cast<float4 *>(o) = make_float4(w[0], w[1], w[2], w[3]);
-      continue;
-    }
+      const uint32_t ar = p.amax[r];
+      if (ar < NONFINITE) {
+        const float sv[4] = {v.x, v.y, v.z, v.w};
+        // the check's thresholds (0: no check) of the four columns
+        const bool sr = kcnn::f16x3::spread(ar, p.amin[r]);
+        const int er = scale_exp(ar);
+        float thr[4];
+        bool any = false;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (c + i >= N || bmax[c + i] >= NONFINITE) continue;
-      float r = beta == 0.0f ? alpha * sv[i] : alpha * sv[i] + beta * o[i];
-      if (bias) r += bias[c + i];
-      o[i] = r;
+        for (int i = 0; i < 4; ++i) {
+          thr[i] = 0.0f;
+          if (c + i >= N) continue;
+          const uint32_t bc = p.bmax[c + i];
+          const bool sc = bc < NONFINITE && kcnn::f16x3::spread(bc, p.bmin[c + i]);
+          if (sr || sc) {
+            thr[i] = __builtin_amdgcn_ldexpf((sr ? p.wspread : 0.0f) + (sc ? p.wspread : 0.0f),
+                                             -(er + scale_exp(bc)));
+            any = true;
+          }
+        }
+        float *o = p.C + (int64_t)r * p.ldc + c;
+        const bool fin = c + 4 <= N && max(max(p.bmax[c], p.bmax[c + 1]),
+                                           max(p.bmax[c + 2], p.bmax[c + 3])) < NONFINITE;
+        if (!any && fin && ((p.ldc & 3) | ((uintptr_t)p.C & 15)) == 0) {
+          // one 16-B store (the same values)
+          float4 ov = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          if (p.beta != 0.0f) ov = *reinterpret_cast<const float4 *>(o);
+          const float oi[4] = {ov.x, ov.y, ov.z, ov.w};
+          float w[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            w[i] = p.beta == 0.0f ? p.alpha * sv[i] : p.alpha * sv[i] + p.beta * oi[i];
+            if (p.bias) w[i] += p.bias[c + i];
+          }
+          *reinterpret_cast<float4 *>(o) = make_float4(w[0], w[1], w[2], w[3]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (c + i >= N || p.bmax[c + i] >= NONFINITE) continue;
+            if (thr[i] != 0.0f && !(fabsf(sv[i]) >= thr[i])) {
+              rej |= 1u << i;
+              continue;
+            }
+            o[i] = store_value(p, sv[i], o + i, c + i);
+          }
+        }
+      }
     }
+    fix_rejected(p, a_kc != 0, b_kc != 0, rej, lane, [&](int l, int n, int &row, int &col) {
+      row = __builtin_amdgcn_readlane(r, l);
+      col = __builtin_amdgcn_readlane(c, l) + n;
+    });
   }
 }
 
@@ -1010,6 +1151,11 @@ static int gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alph
   hipStream_t st = kcnn::as_stream(stream);
   GemmF16Args a{};
   a.A = A; a.B = B; a.C = C; a.amax = amax; a.bmax = bmax; a.bias = bias;
+  a.amin = amax + M;  // statistics blocks [max[n], min[n]] (stats_rows)
+  a.bmin = bmax + N;
+  // a spread group's share of the store's check threshold, scaled units:
+  // 2^9 K (f16-split.h; the bound is in DESIGN 3, "spread groups")
+  a.wspread = 512.0f * (float)K * (1.0f + 1.0f / 1024.0f);
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.alpha = alpha; a.beta = beta;
   a.tiles_m = (M + BM - 1) / BM;
@@ -1043,7 +1189,7 @@ static int gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alph
   int rc = kcnn::launch_status();
   if (rc || s == 1) return rc;
   hipLaunchKernelGGL(gemm_f16x3_reduce_kernel, dim3(kcnn::grid_for((int64_t)M * ((N + 3) / 4))),
-                     dim3(256), 0, st, a.part, s, M, N, alpha, beta, C, ldc, amax, bmax, bias);
+                     dim3(256), 0, st, a, a_kc ? 1 : 0, b_kc ? 1 : 0);
   return kcnn::launch_status();
 }
 extern "C" int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alpha,
@@ -1062,7 +1208,7 @@ namespace {
 size_t stats_ws_words(int M, int N, int K, int transA, int transB) {
   const size_t pa = transA ? stat_part_words(K, M, 1) : 0;
   const size_t pb = transB ? 0 : stat_part_words(K, N, 1);
-  return (size_t)M + N + 4 + pa + pb;
+  return 2 * ((size_t)M + N) + 4 + pa + pb;
 }
 }  // namespace
 extern "C" size_t kl_gemm_f16x3_full_workspace_bytes(int M, int N, int K) {
@@ -1101,8 +1247,8 @@ extern "C" int kl_gemm_f16x3_bias(int transA, int transB, int M, int N, int K, f
   if (!ws || ws_bytes < kl_gemm_f16x3_full_workspace_bytes(M, N, K))
     return (int)hipErrorInvalidValue;
   uint32_t *amax = reinterpret_cast<uint32_t *>(static_cast<char *>(ws) + pb);
-  uint32_t *bmax = amax + M;
-  uint32_t *parta = bmax + N + 4;
+  uint32_t *bmax = amax + 2 * M;  // statistics blocks: [max, min] per group
+  uint32_t *parta = bmax + 2 * N + 4;
   uint32_t *partb = parta + (transA ? stat_part_words(K, M, 1) : 0);
   const StatOp sa = amax_given ? StatOp{}
                     : transA   ? stat_op(A, K, M, lda, 1, amax, parta)

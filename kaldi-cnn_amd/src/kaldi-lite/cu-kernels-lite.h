@@ -30,9 +30,11 @@ int kl_gemm_x6(int transA, int transB, int M, int N, int K, float alpha,
                float *C, int ldc, void *ws, size_t ws_bytes, kcnn_stream_t st);
 /* fp32 GEMM on the f16 MFMAs: two-part f16 split under per-row / per-column
    power-of-two scales (cu-gemm-f16x3.hip).  kl_absmax_rows / kl_absmax_cols
-   write max |x| bit patterns per row / column (the column form needs
-   kl_absmax_cols_words of scratch); kl_gemm_f16x3_st takes them for op(A)'s
-   rows and op(B)'s columns, kl_gemm_f16x3 computes them in its workspace.
+   write a statistics block per row / column set: [max[n], min[n]], the max
+   |x| and the min nonzero |x| bit patterns (0: no nonzero element), 2 n
+   words (the column form needs kl_absmax_cols_words of scratch);
+   kl_gemm_f16x3_st takes the blocks of op(A)'s rows and op(B)'s columns,
+   kl_gemm_f16x3 computes them in its workspace.
    Both return hipErrorNotSupported for shapes outside the kernel's
    addressing limits. */
 int kl_absmax_rows(const float *X, int rows, int cols, int ld, uint32_t *rmax,

@@ -51,3 +51,24 @@ def test_dp_two_ranks_match_single_process(tmp_path, stack, n_params, split, bac
         ref = single[k]
         err = np.abs(a[k] - ref).max() / max(np.abs(ref).max(), 1e-30)
         assert err < 1e-5, f"{k}: DP vs single-process relative error {err:.2e}"
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`python bench.py --gpus 2` (no launcher in the environment) starts the
+    two ranks itself and reports a two-GPU line (gloo: both ranks share the
+    test box's one GPU)."""
+    import json
+    root = os.path.dirname(HERE)
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "2"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--dist-backend", "gloo", "--steps", "2", "--warmup", "1",
+                        "--frames-per-gpu", "256", "--no-cpu-baseline"],
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["dp"]["ranks_seen"] == 2
+    assert res["config"]["parallelism"] == "dp2" and res["config"]["global_batch"] == 512

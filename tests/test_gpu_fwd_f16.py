@@ -136,3 +136,34 @@ def test_fused_forward_nonfinite_is_exact(kc, f16, fusion):
     # the finite frames are untouched by their neighbours' Inf
     y = outs[0][0]
     assert np.isfinite(y[6:]).all() and np.isfinite(y[0]).all()
+
+
+@pytest.mark.parametrize("group", ["W", "position"])
+@pytest.mark.parametrize("spread", [24, 28, 32])
+def test_fwd_intra_group_range(kc, f16, group, spread):
+    """The forward's scale groups (one for all of W, one per output
+    position's im2col column) with their largest element meeting zeros in
+    the other operand and every other element 2^-spread below it; bias 0, so
+    the small elements carry all of S.  group "W": W's
+    channel-0 rows are 1, the rest N(0,1) * 2^-spread, X's channel 0 is 0;
+    "position": X's channel 0 is 1 (each position's largest taps), channels
+    1-2 N(0,1) * 2^-spread, W's channel-0 rows 0."""
+    comp, oc = make_pair(kc, C2, seed=41)
+    r = rng(42 + spread)
+    x = randn(r, (6, 40 * 11 * 3)).reshape(6, 3, 11 * 40)
+    Wm = randn(r, (24, 128), 0.01)
+    if group == "W":
+        Wm[:8] = 1.0                      # channel 0's 8 taps (row c*8 + ky)
+        Wm[8:] *= np.float32(2.0 ** -spread)
+        x[:, 0] = 0.0
+    else:
+        Wm[:8] = 0.0
+        x[:, 0] = 1.0
+        x[:, 1:] *= np.float32(2.0 ** -spread)
+    x = x.reshape(6, -1).astype(np.float32)
+    oc.W = Wm.astype(np.float32)
+    oc.b = np.zeros_like(oc.b)
+    comp.SetParam(kc.PARAM_LINEAR, dev(oc.W))
+    comp.SetParam(kc.PARAM_BIAS, dev(oc.b))
+    _, y_t, y_s = triple(lambda: oc.propagate(x))
+    assert_bound(host(comp.Propagate(dev(x))), y_t, y_s, what=f"{group} spread 2^{spread}")

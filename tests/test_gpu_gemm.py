@@ -184,14 +184,17 @@ def test_gemm_nonfinite_pattern(kc, mode, ta, tb, shape):
 def test_gemm_c2_fc_shapes(kc, name, m, n, k, ta, tb):
     """The c2 stack's three FC GEMMs at full size: both split kernels meet the
     bound; bf16x6's error is no worse than rocBLAS sgemm's (x 1.5), f16x3's
-    within 8x of it normwise and 2e-6 * S elementwise."""
+    within 2x of it normwise and 2e-6 * S elementwise (measured r05,
+    scripts/gemm_error_ratio.py: f16x3 0.44-0.89x sgemm's normwise error,
+    bf16x6 0.62-1.31x)."""
     import torch
     _, w3, r3 = _check(torch, kc, m, n, k, ta, tb, mode=2)
     _, w6, r6 = _check(torch, kc, m, n, k, ta, tb, mode=1)
     _, w0, r0 = _check(torch, kc, m, n, k, ta, tb, mode=0)
     assert w6 <= 1.5 * w0 + 1e-8 and r6 <= 1.5 * r0 + 1e-8, (w6, w0, r6, r0)
-    # f16x3 keeps 22 of fp32's 24 bits per operand: within a few times sgemm
-    assert w3 <= 2e-6 and r3 <= 8 * r0 + 1e-8, (w3, w0, r3, r0)
+    # f16x3: 22-23 of fp32's 24 bits per operand and 3 accumulator roundings
+    # per 16 products (sgemm: one per product)
+    assert w3 <= 2e-6 and r3 <= 2 * r0 + 1e-8, (w3, w0, r3, r0)
 
 
 @pytest.mark.parametrize("ta", [False, True])
@@ -266,3 +269,42 @@ def test_gemm_f16x3_ragged_rows(kc, ta, tb, shape, pitch):
         _gemm_mode(kc, 2, lambda: kc.gemm(a, b, c, ta, tb, alpha, beta))
         torch.cuda.synchronize()
         _bound(torch, a, b, c0, c, ta, tb, alpha, beta)
+
+
+C2_FC = [("fc_fwd", 4096, 1024, 11616, False, True),
+         ("fc_dgrad", 4096, 11616, 1024, False, False),
+         ("fc_wgrad", 1024, 11616, 4096, True, False)]
+
+
+@pytest.mark.parametrize("name,m,n,k,ta,tb", C2_FC, ids=[c[0] for c in C2_FC])
+@pytest.mark.parametrize("side", ["row", "col"])
+@pytest.mark.parametrize("spread", [24, 28, 32])
+def test_gemm_f16x3_intra_group_range(kc, name, m, n, k, ta, tb, side, spread):
+    """The f16x3 scale is one power of two per row of op(A) / column of
+    op(B), set by the group's largest element; elements far below it lose
+    their low part (an f16 subnormal).  Here one row of op(A) (side "row") or
+    one column of op(B) ("col") is N(0,1) * 2^-spread except one element of
+    size 1 whose partner in the other operand is 0 for every output: the
+    small elements carry all of S, and the elementwise 1e-5 * S bar must
+    hold.  c2's FC shapes, all three transposes."""
+    import torch
+    a, b, c0 = _mats(torch, m, n, k, ta, tb, seed=31)
+    A = a.t() if ta else a
+    B = b.t() if tb else b
+    g = torch.Generator(device="cuda")
+    g.manual_seed(32 + spread)
+    k0 = k // 3
+    if side == "row":
+        for i0 in (5, m - 2):
+            A[i0] = torch.randn(k, generator=g, device="cuda") * 2.0 ** -spread
+            A[i0, k0] = 1.0
+        B[k0, :] = 0.0
+    else:
+        for j0 in (7, n - 3):
+            B[:, j0] = torch.randn(k, generator=g, device="cuda") * (0.01 * 2.0 ** -spread)
+            B[k0, j0] = -0.01
+        A[:, k0] = 0.0
+    c = c0.clone()
+    _gemm_mode(kc, 2, lambda: kc.gemm(a, b, c, ta, tb, 1.0, 0.0))
+    torch.cuda.synchronize()
+    _bound(torch, a, b, c0, c, ta, tb, 1.0, 0.0)

@@ -44,6 +44,12 @@ STACKS = {
     "G40_pc4": (10, 6, 2, 3, 2, 40, 4, 8, 0, 0),    # bf16x6 forward: pooled rows past G
     "pc3_unfused": (8, 6, 1, 3, 1, 30, 3, 8, 0, 0),  # not fusable: plain path
     "G256_pc4": (12, 6, 2, 4, 2, 256, 4, 16, 0, 0),  # 2 filter chunks of 128
+    # G = 128, pc = 4 with 10 and 11 position tiles (P 300, 352): the f16x3
+    # forward's register-pooled statistics form needs all 12, so these take
+    # the generic item loop; the FC GEMM's scales from the fused forward's
+    # statistics must equal the unfused statistics pass's (bitwise FC output)
+    "G128_P300": (32, 10, 3, 3, 1, 128, 4, 16, 0, 0),
+    "G128_P352": (39, 11, 3, 8, 1, 128, 4, 16, 0, 0),
     # 3-D windows (qh x qw x pc, 16-bit routing mask): (..., pad_h, pad_w, qh, qw)
     "c5_P1_3x1x4": (40, 11, 3, 8, 1, 256, 4, 16, 0, 0, 3, 1),
     "win_2x2x2": (9, 8, 2, 2, 1, 64, 2, 8, 0, 0, 2, 2),

@@ -271,6 +271,21 @@ def cpu_baseline(frames_hint, budget_s=12.0):
     c1_1 = c1_forward()
     O.set_threads(threads)
     c1_n = c1_forward()
+    # The reference's threaded CPU trainer (nnet-train-parallel --num-threads,
+    # train_conv_dropout.sh:205-208; run_nnet.sh:48-50: 16 threads, minibatch
+    # 128): T threads, each running the single-thread step on its own
+    # minibatches against ONE shared model (Hogwild: unsynchronised in-place
+    # updates, as the reference's threads share their Nnet)
+    hog = {"unit": "frames/sec", "minibatch": 128,
+           "mode": "Hogwild: T threads x single-threaded C oracle step, one shared model",
+           "threads_1": hogwild(O, r, 1, 128, budget_s / 6),
+           f"threads_{threads}": hogwild(O, r, threads, 128, budget_s / 4)}
+    if avail > threads:
+        # every CPU of the affinity mask (shared with the other GPUs' jobs),
+        # smaller minibatches so the threads' im2col temporaries stay small
+        hog[f"threads_{avail}"] = hogwild(O, r, avail, 32, budget_s / 4)
+        hog[f"threads_{avail}_minibatch"] = 32
+    O.set_threads(threads)
     O.use_blas(False)
     model = ""
     try:
@@ -288,12 +303,70 @@ def cpu_baseline(frames_hint, budget_s=12.0):
             "seconds_per_leg": split,
             "single_thread": {"value": round(n1 / t1, 2), "sample": f"{n1} frames, 1 thread"},
             "all_affinity": all_cores,
+            "hogwild": hog,
             "c1_forward": {"unit": "frames/sec", "threads_1": c1_1, f"threads_{threads}": c1_n,
                            "sample": "BASELINE configs[0]: Conv+Maxpool forward, 256 frames, "
                                      "best of 3"},
             "host": {"cpu_model": model, "nproc": os.cpu_count(), "affinity": avail,
                      "threads_note": f"{threads} threads = one GPU's share of the box's "
                                      "host CPUs (the job's allotment)"}}
+
+
+def hogwild(O, r, nthreads, minibatch, budget_s):
+    """Aggregate frames/s of nthreads host threads, each training the c2
+    stack on its own minibatches (single-threaded C oracle, OpenBLAS on one
+    thread) against one shared model, for about budget_s seconds (every
+    thread finishes at least one step).  The oracle's ctypes calls release
+    the GIL; the model's arrays are updated in place by every thread."""
+    import threading
+    import numpy as np
+    O.set_threads(1)
+    oc = O.Conv(H, W, C, KH, KW, G)
+    oc.W = (r.standard_normal((KH * KW * C, G)) * 0.01).astype(np.float32)
+    oc.b = (r.standard_normal(G) * 0.5).astype(np.float32)
+    op = O.Pool(OH, OW, G, 1, 1, PC)
+    of = O.FC(POOL_OUT, FC_OUT)
+    of.W = (r.standard_normal((FC_OUT, POOL_OUT)) * 0.01).astype(np.float32)
+    of.b = np.ones(FC_OUT, np.float32)
+    for c in (oc, of):  # the shared state exists before the threads start
+        c._c()
+    data = [(r.standard_normal((minibatch, H * W * C)).astype(np.float32),
+             (r.standard_normal((minibatch, FC_OUT)) * 1e-2).astype(np.float32))
+            for _ in range(nthreads)]
+    done = [0] * nthreads
+    errors = []
+    start = threading.Barrier(nthreads + 1)
+    deadline = [0.0]
+
+    def worker(i):
+        x, dy = data[i]
+        start.wait()
+        try:
+            while True:
+                y1 = oc.propagate(x)
+                y2 = op.propagate(y1)
+                of.propagate(y2)
+                d2 = of.backprop(y2, dy, update=True)
+                d1 = op.backprop(y1, y2, d2)
+                oc.backprop(x, d1, update=True)
+                done[i] += 1
+                if time.perf_counter() >= deadline[0]:
+                    break
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(nthreads)]
+    for t in ths:
+        t.start()
+    t0 = time.perf_counter()
+    deadline[0] = t0 + budget_s
+    start.wait()
+    for t in ths:
+        t.join()
+    el = time.perf_counter() - t0
+    if errors:
+        return {"error": errors[0]}
+    return round(sum(done) * minibatch / el, 2)
 
 
 def cpu_baseline_stack(config_text, frames, splice_frames=1, budget_s=8.0):

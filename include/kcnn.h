@@ -67,12 +67,16 @@ int kcnn_set_fusion(int mode);
  *   0: rocBLAS sgemm on the fp32-input MFMA;
  *   1: the in-house kernel on the bf16 MFMA with each fp32 operand split
  *      exactly into three bf16 parts and the six leading cross products kept
- *      (cu-gemm-x6.hip); same error bound as sgemm;
+ *      (cu-gemm-x6.hip); the dot-product error bound of sgemm (1e-5 * S per
+ *      element) for operands above 2^-110;
  *   2 (default): the in-house kernel on the f16 MFMA with each operand scaled
  *      by a power of two per row of op(A) / column of op(B) and split into
- *      two f16 parts, three cross products kept (cu-gemm-f16x3.hip); same
- *      error bound, IEEE Inf / NaN rows and columns; shapes past its 32-bit
- *      addressing run mode 1.
+ *      two f16 parts, three cross products kept (cu-gemm-f16x3.hip); the
+ *      split's own bound is per scale group (f16-split.h), and the products
+ *      touching a group with elements far under its max are checked and
+ *      recomputed in fp32 where needed, so every element meets the 1e-5 * S
+ *      bound at any fp32 range; IEEE Inf / NaN rows and columns; shapes past
+ *      its 32-bit addressing run mode 1.
  * Env KCNN_GEMM (0/1/2) sets the initial mode. */
 int kcnn_set_gemm_mode(int mode);
 /* Kernel-family selectors (kaldi-lite/kcnn-knobs.h): each picks

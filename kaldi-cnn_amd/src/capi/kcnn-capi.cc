@@ -686,7 +686,7 @@ static std::unique_ptr<CuGemmStatsHint> input_stats(const kcnn_nnet *n, size_t i
   const CuMatrix<BaseFloat> &x = n->fwd[i];
   return std::unique_ptr<CuGemmStatsHint>(new CuGemmStatsHint(
       x.Data(), x.NumRows(), x.NumCols(), x.Stride(), n->fstat[i],
-      n->fstat[i] + 2 * (size_t)x.NumRows()));
+      n->fstat[i] + 3 * (size_t)x.NumRows()));
 }
 
 // Component i (Conv) and i+1 (channel-only Maxpool) in one fused pass;
@@ -710,9 +710,9 @@ static bool propagate_pair(kcnn_nnet *n, size_t i) {
   size_output(&n->fwd[i + 1], rows, conv->OutputDim());
   size_output(&n->fwd[i + 2], rows, pool->OutputDim());
   const bool store = g_fusion == 2;
-  // room for the pooled output's statistics (the row block [max, min] and the
-  // column block [max, min], kept) and the kernel's column partials (this
-  // call only)
+  // room for the pooled output's statistics (the row block [max, min, cnt]
+  // and the column block [max, min, cnt], kept) and the kernel's column
+  // partials (this call only)
   PoolStatsOut ps;
   const size_t pw = mask_bytes == 1 && conv->In_pad_height() == 0 && conv->In_pad_width() == 0
                         ? kcnn_conv2d_maxpool_stats_words(
@@ -722,14 +722,14 @@ static bool propagate_pair(kcnn_nnet *n, size_t i) {
                         : 0;
   CuScratch part(pw * 4);
   if (pw) {
-    const size_t need = 2 * ((size_t)rows + pool->OutputDim());
+    const size_t need = 3 * ((size_t)rows + pool->OutputDim());
     if (n->fstat_words[i + 2] < need) {
       if (n->fstat[i + 2]) CuDevice::Instantiate().Free(n->fstat[i + 2]);
       n->fstat[i + 2] = static_cast<uint32_t *>(CuDevice::Instantiate().Malloc(need * 4));
       n->fstat_words[i + 2] = need;
     }
     ps.rowmax = n->fstat[i + 2];
-    ps.colmax = n->fstat[i + 2] + 2 * (size_t)rows;
+    ps.colmax = n->fstat[i + 2] + 3 * (size_t)rows;
     ps.partials = static_cast<uint32_t *>(part.p);
     ps.partial_words = pw;
   }

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -285,19 +286,15 @@ __device__ __forceinline__ floatx16 fwd_item_fp32(
 // with |W'|, |x'| <= 2^15 the elements the split holds only to 2^-25
 // (scaled) add at most 2^-9 Kdim to a scaled sum, fct times that to y; an
 // output with |y| >= 2^10 Kdim fct therefore carries at most 2^-19 |y| <=
-// 2^-19 S of it.  Any output below that bound sends the whole item to
-// fwd_item_fp32 (every lane: a wave-uniform decision, the same in the fused
-// and the unfused epilogue).
-__device__ __forceinline__ void spread_check(floatx16 &y, float fct, const ConvGeom &g,
-                                             const float *__restrict__ K, int ks,
-                                             const float *__restrict__ bias, const float *Xs,
-                                             const int2 *koff, int gb, int tile, int lane) {
+// 2^-19 S of it.  True when some output of the item is below that bound:
+// the caller then recomputes the whole item by fwd_item_fp32 (every lane: a
+// wave-uniform decision, the same in the fused and the unfused epilogue).
+__device__ __forceinline__ bool spread_reject(const floatx16 &y, float fct, const ConvGeom &g) {
   const float thr = fct * (1024.0f * (float)g.Kdim * (1.0f + 1.0f / 1024.0f));
   float mn = fabsf(y[0]);
 #pragma unroll
   for (int r = 1; r < 16; r++) mn = fminf(mn, fabsf(y[r]));
-  if (__builtin_amdgcn_ballot_w64(!(mn >= thr)) != 0)
-    y = fwd_item_fp32(g, K, ks, bias, Xs, koff, gb, tile, lane);
+  return __builtin_amdgcn_ballot_w64(!(mn >= thr)) != 0;
 }
 
 // The routing mask of a 4-way pool group, bit c = (v_c == mx): the four
@@ -324,10 +321,11 @@ __device__ __forceinline__ unsigned tie_mask4(float v0, float v1, float v2, floa
 }
 
 // The register-pooled forward's statistics outputs (pool-stats.h): the
-// per-frame block rowmax [max[R], min[R]], the per-workgroup column partials
-// (exponent bytes: [nblk][npool] of the maxima, then of the minima) and the
-// column block colmax [max[npool], min[npool]] that pool_colmax_kernel fills
-// (initialised here first)
+// per-frame block rowmax [max[R], min[R], cnt[R]], the per-workgroup column
+// partials (exponent bytes: [nblk][npool] of the maxima, then of the minima)
+// and the column block colmax [max[npool], min[npool], cnt[npool]] that
+// pool_colmax_kernel fills (initialised here first); pool_count_kernel then
+// counts the spread groups' small elements
 struct RpStats {
   uint32_t *rowmax = nullptr, *partials = nullptr, *colmax = nullptr;
 };
@@ -376,6 +374,62 @@ __global__ __launch_bounds__(256) void pool_colmax_kernel(const uint8_t *__restr
   }
   atomicMax(colmax + c, (m << 23) | 0x7fffffu);
   atomicMin(colmax + npool + c, n == 0xff ? 0xffffffffu : max(n << 23, 1u));
+}
+
+// The pooled output's spread groups (f16-split.h) counted after
+// pool_colmax_kernel: a block per 64 frame rows or 64 pooled columns writes
+// their cnt (0 unless spread), then reads each of its spread groups (rare)
+// with all 256 threads, eight loads in flight each, and sums the count.
+__global__ __launch_bounds__(256) void pool_count_kernel(const float *__restrict__ P, int ps,
+                                                         int R, int npool,
+                                                         uint32_t *__restrict__ rowblk,
+                                                         uint32_t *__restrict__ colblk) {
+  __shared__ uint32_t cred[4];
+  const int nrb = (R + 63) / 64;
+  const bool isrow = (int)blockIdx.x < nrb;  // uniform
+  const int g0 = (isrow ? (int)blockIdx.x : (int)blockIdx.x - nrb) * 64;
+  const int n = isrow ? R : npool;
+  uint32_t *blk = isrow ? rowblk : colblk;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int gi = g0 + lane;
+  uint32_t mx = 0;
+  bool spr = false;
+  if (gi < n) {
+    mx = blk[gi];
+    spr = f16x3::spread(mx, blk[n + gi]);
+    if (wave == 0) blk[2 * (size_t)n + gi] = 0;
+  }
+  uint64_t todo = __ballot(spr);  // the same in every wave
+  const int len = isrow ? npool : R;
+  while (todo) {  // block-uniform
+    const int l = __builtin_ctzll(todo);
+    todo &= todo - 1;
+    const int grp = g0 + l;
+    const float bound = f16x3::small_bound(__builtin_amdgcn_readlane(mx, l));
+    // element e of the group: row grp's column e, or column grp's row e
+    auto at = [&](int e) {
+      return fabsf(isrow ? P[(int64_t)grp * ps + e] : P[(int64_t)e * ps + grp]);
+    };
+    uint32_t cnt = 0;
+    int e = threadIdx.x;
+    for (; e + 7 * 256 < len; e += 8 * 256) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = at(e + j * 256);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cnt += (v[j] < bound && v[j] != 0.0f) ? 1u : 0u;
+    }
+    for (; e < len; e += 256) {
+      const float v = at(e);
+      cnt += (v < bound && v != 0.0f) ? 1u : 0u;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, d);
+    __syncthreads();
+    if (lane == 0) cred[wave] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) blk[2 * (size_t)n + grp] = cred[0] + cred[1] + cred[2] + cred[3];
+  }
 }
 
 // RP: the register-pooled form only (out == nullptr, PC 2 or 4, G = 128 and
@@ -599,6 +653,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
           for (int e = 0; e < 8; e++) {
             v[s][e] = k0 + e < g.Kdim ? v[s][e] : 0.0f;
             m = fmaxf(m, fabsf(v[s][e]));
+#ifdef KCNN_EXPERIMENTS  // A/B: dbg & 2048 drops the position columns' min
+            if (!(dbg & 2048))
+#endif
             mn = min(mn, (__float_as_uint(v[s][e]) << 1) - 2u);
           }
         }
@@ -698,9 +755,13 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
         // the pooling of one item's accumulators (F16: y = acc * 2^-(sa +
         // sb(p)) + b first, in one rounding; fp32 items: acc * 1 + -0, i.e.
         // acc itself)
+        uint32_t redo = 0;    // F16: items (bit gb * FT + t) recomputed in fp32
         uint32_t rowrun = 0;  // RP: max |pooled| bits of this lane in the frame
         uint32_t rowmn = 0xffffffffu;  // RP: min (|pooled| - 1) of this lane in the frame
-        auto pool_item = [&](floatx16 &acc, int gb, int t, bool sl) {
+        // (chk: std::true_type in the frames that touch a spread group, which
+        // run their own copy of the item sequence, so the common one stays
+        // free of the check's branches)
+        auto pool_item = [&](floatx16 &acc, int gb, int t, bool sl, auto chk) {
           const int p = (wave_q + 4 * t) * 32 + l_f;
           // accumulator r = 4k + i of lane (l, h) is filter 8k + 4h + i at
           // position p: a pool group is PC consecutive registers (the
@@ -722,6 +783,22 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
           int boff = (sl ? 128 : gb * 32) + 4 * h_f;  // Bz = Bs + 128
           asm volatile("" : "+v"(boff));
           const float *bb = Bs + boff;
+          // RP: the item's column-min bytes, read first so their latency
+          // passes under the epilogue's arithmetic
+          uint32_t old[RP ? 16 / PC : 1];
+          if constexpr (RP) {
+            const int pc = min(p, g.P - 1) + h_f * (4 / PC) * Pq;
+#pragma unroll
+            for (int j = 0; j < 16 / PC; j++) {
+              const int r0 = j * PC;
+              const int U = (gb * 32 + (r0 & 3) + 8 * (r0 >> 2)) / PC;
+#ifdef KCNN_EXPERIMENTS  // A/B: dbg & 1024 drops the column min bytes
+              old[j] = (dbg & 1024) ? 0u : Tmn[U * Pq + pc];
+#else
+              old[j] = Tmn[U * Pq + pc];
+#endif
+            }
+          }
           if constexpr (F16) {
             // y = acc * 2^-(sa + sb(p)) + b in one rounding (fp32 items:
             // acc * 1 + -0, i.e. acc itself)
@@ -733,8 +810,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
               acc[4 * k + 2] = fmaf(acc[4 * k + 2], fct, b4.z);
               acc[4 * k + 3] = fmaf(acc[4 * k + 3], fct, b4.w);
             }
-            if (!sl && (wspread || (tsp >> t) & 1))  // uniform, rare
-              spread_check(acc, fct, g, K, ks, bias, Xs, koff, gb, wave_q + 4 * t, lane_f);
+            if constexpr (decltype(chk)::value) {
+              if (!sl && (wspread || (tsp >> t) & 1) && spread_reject(acc, fct, g)) {
+                redo |= 1u << (gb * FT + t);  // uniform, rare: pooled after the sequence
+                return;
+              }
+            }
           }
           // The pool value by IEEE max (v_max3: NaN skipped like the
           // reference's `val < x` test, ties between equal nonzero values
@@ -768,16 +849,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
           if constexpr (RP) {
             // lanes past P hold position P - 1's values: their max lands there
             const int pc = min(p, g.P - 1) + h_f * (4 / PC) * Pq;
-            // the column min bytes: each pooled column has one owner lane
-            // (two for column P - 1, holding the same value), so a plain
-            // read-modify-write (the reads first, one wait for the four)
-            uint32_t old[NGP];
-#pragma unroll
-            for (int j = 0; j < NGP; j++) {
-              const int r0 = j * PC;
-              const int U = (gb * 32 + (r0 & 3) + 8 * (r0 >> 2)) / PC;
-              old[j] = Tmn[U * Pq + pc];
-            }
+            // the column min bytes (old: read at the item's start): each
+            // pooled column has one owner lane (two for column P - 1,
+            // holding the same value), so a plain read-modify-write
 #pragma unroll
             for (int j = 0; j < NGP; j++) {
               const uint32_t a = __float_as_uint(mx[j]) & 0x7fffffffu;  // never NaN
@@ -787,7 +861,13 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
                                      __HIP_MEMORY_SCOPE_WORKGROUP);
               rowrun = max(rowrun, a);
               const uint32_t u = a - 1u;  // wraps for 0: never the min
+#ifdef KCNN_EXPERIMENTS  // A/B: dbg & 4096 drops the row min
+              if (!(dbg & 4096))
+#endif
               rowmn = min(rowmn, u);
+#ifdef KCNN_EXPERIMENTS  // A/B: dbg & 1024 drops the column min bytes
+              if (!(dbg & 1024))
+#endif
               Tmn[U * Pq + pc] = (uint8_t)min(old[j], u >> 23);
             }
             // (pinned per item: left free, the scheduler spreads the items'
@@ -823,15 +903,25 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
                                                  (unsigned)(U * Pq), 0);
           }
         };
+        // the items in fp32 (fwd_item_fp32, then pooled like any other):
+        // every valid item of a slow frame (Inf, range), or the items a
+        // spread check rejected; one code copy for both
+        auto fp32_items = [&]() {
+#pragma unroll 1
+          while (redo) {  // uniform
+            const int i = __builtin_ctz(redo);
+            redo &= redo - 1;
+            const int gb = i / FT, t = i % FT;
+            floatx16 a = fwd_item_fp32(g, K, ks, bias, Xs, koff, gb, wave_q + 4 * t, lane_f);
+            pool_item(a, gb, t, true, std::false_type{});
+          }
+        };
         if constexpr (F16) {
           if (slow) {  // uniform: the frame's items in fp32 (rare: Inf, range)
 #pragma unroll 1
-            for (int i = 0; i < NI; i++) {
-              if (!RP && !valid(i)) continue;
-              const int gb = i / FT, t = i % FT;
-              floatx16 a = fwd_item_fp32(g, K, ks, bias, Xs, koff, gb, wave_q + 4 * t, lane_f);
-              pool_item(a, gb, t, true);
-            }
+            for (int i = 0; i < NI; i++)
+              if (RP || valid(i)) redo |= 1u << i;
+            fp32_items();
             if constexpr (RP) frame_row_max(rslot + (it & 1) * 4 + wave_q, rowrun, rowmn, lane_f);
             KCNN_TMARK(2)
             continue;  // next frame
@@ -848,25 +938,33 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
           }
           return a;
         };
-        if (RP || (NG == 4 && wave_q + 4 * (FT - 1) < ntile)) {
-          // every item valid (c2: G = 128, P = 363): one straight-line
-          // sequence, the MFMA chain of item i beside the pooling of i - 1
-          floatx16 prev = chain(0, 0);
+        auto sequence = [&](auto chk) {
+          if (RP || (NG == 4 && wave_q + 4 * (FT - 1) < ntile)) {
+            // every item valid (c2: G = 128, P = 363): one straight-line
+            // sequence, the MFMA chain of item i beside the pooling of i - 1
+            floatx16 prev = chain(0, 0);
 #pragma unroll
-          for (int i = 1; i <= NI; i++) {
-            floatx16 cur;
-            if (i < NI) cur = chain(i / FT, i % FT);
-            pool_item(prev, (i - 1) / FT, (i - 1) % FT, false);
-            if (i < NI) prev = cur;
-          }
-        } else if constexpr (!RP) {
+            for (int i = 1; i <= NI; i++) {
+              floatx16 cur;
+              if (i < NI) cur = chain(i / FT, i % FT);
+              pool_item(prev, (i - 1) / FT, (i - 1) % FT, false, chk);
+              if (i < NI) prev = cur;
+            }
+          } else if constexpr (!RP) {
 #pragma unroll
-          for (int i = 0; i < NI; i++) {
-            if (!valid(i)) continue;  // uniform
-            floatx16 a = chain(i / FT, i % FT);
-            pool_item(a, i / FT, i % FT, false);
+            for (int i = 0; i < NI; i++) {
+              if (!valid(i)) continue;  // uniform
+              floatx16 a = chain(i / FT, i % FT);
+              pool_item(a, i / FT, i % FT, false, chk);
+            }
           }
-        }
+        };
+#ifdef KCNN_EXPERIMENTS  // A/B: dbg & 8192 never takes the checked sequence
+        if (dbg & 8192) tsp = 0;
+#endif
+        if (F16 && (wspread || tsp != 0)) sequence(std::true_type{});  // uniform, rare
+        else sequence(std::false_type{});
+        if constexpr (F16) fp32_items();  // the items a spread check rejected (rare)
         if constexpr (RP) frame_row_max(rslot + (it & 1) * 4 + wave_q, rowrun, rowmn, lane_f);
         KCNN_TMARK(2)
         continue;  // next frame
@@ -885,17 +983,16 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
         if (pt >= ntile) continue;  // wave_q-uniform
         floatx16 acc = zero16();
         if constexpr (F16) {
-          if (slow) {
-            acc = fwd_item_fp32(g, K, ks, bias, Xs, koff, gb, pt, lane_f);
-          } else {
+          bool fp = slow;  // uniform
+          if (!fp) {
 #pragma unroll
             for (int s = 0; s < KS; s++)
               acc = f16x3::mfma3(wh[gb][s], wl[gb][s], bxh[t][s], bxl[t][s], acc);
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[r] = fmaf(acc[r], ft[t], bsv[r]);
-            if (wspread || (tsp >> t) & 1)  // uniform, rare
-              spread_check(acc, ft[t], g, K, ks, bias, Xs, koff, gb, pt, lane_f);
+            fp = (wspread || (tsp >> t) & 1) && spread_reject(acc, ft[t], g);  // rare
           }
+          if (fp) acc = fwd_item_fp32(g, K, ks, bias, Xs, koff, gb, pt, lane_f);
         } else if constexpr (X6) {
 #pragma unroll
           for (int s = 0; s < KS; s++) acc = x6::mfma6(w6[gb][s], bx6[t][s], acc);
@@ -2169,6 +2266,8 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
                        dim3((npool + 255) / 256, (grid + COLMAX_ROWS - 1) / COLMAX_ROWS),
                        dim3(256), 0, st, reinterpret_cast<const uint8_t *>(pcol), (int)grid,
                        npool, stats->colmax);
+    hipLaunchKernelGGL(pool_count_kernel, dim3((g.R + 63) / 64 + (npool + 63) / 64), dim3(256),
+                       0, st, pool, ps, g.R, npool, stats->rowmax, stats->colmax);
     stats->produced = 1;
   }
   return (int)hipGetLastError();

@@ -17,9 +17,12 @@
 //
 // and the kernels keep the first three (one v_mfma_f32_32x32x16_f16 each,
 // smallest first, fp32 accumulation), then unscale by 2^-(s_a + s_b).  The
-// error per product is under 3 * 2^-22 of |a b|, 14x inside the 1e-5 * S
-// parity bound; the f16 MFMA runs at the bf16 rate, so this is
-// half the matrix-core work of bf16x6 (x6-util.h) for fewer split VALU.
+// error bound is normwise per group, not per product: elements far under
+// their group's max keep only 2^-25 absolute.  spread() below names the
+// groups where that can matter, and the kernels check (and recompute in
+// fp32) the products that touch them, which restores the 1e-5 * S parity
+// bar per element; the f16 MFMA runs at the bf16 rate, so this
+// is half the matrix-core work of bf16x6 (x6-util.h) for fewer split VALU.
 // Users: the FC GEMM (kaldi-lite/cu-gemm-f16x3.hip) and the frame-resident
 // conv forward (cnsl-conv-frame.hip).
 #ifndef KCNN_CNSLMAT_F16_SPLIT_H_
@@ -67,6 +70,21 @@ __device__ __forceinline__ int ebits(uint32_t b) {
 // cannot clear in fp32.
 __device__ __forceinline__ bool spread(uint32_t mx, uint32_t mn) {
   return mn != 0 && mx < NONFINITE && ebits(mn) < ebits(mx) - 20;
+}
+// The elements a spread group holds only to 2^-25 absolute (scaled): the
+// nonzero |x| below small_bound(mx) = 2^(-3 - s), i.e. under 2^-3 after the
+// scale.  A statistics block counts them per spread group (cnt).
+__device__ __forceinline__ float small_bound(uint32_t mx) {
+  return __builtin_amdgcn_ldexpf(1.0f, -3 - scale_exp(mx));
+}
+// A group's share of the GEMM store's check threshold in scaled units: each
+// of its cnt such elements adds at most 2^-25 |hi| <= 2^-10 to a scaled sum,
+// and a sum is kept when that part stays under 2^-19 |acc|: 2^9 per element
+// (x (1 + 2^-10) for the rounding of the check itself).  cnt is 0 exactly
+// when the group is not spread (a spread group's min is one of its small
+// elements), so the weight is 0 then.
+__device__ __forceinline__ float spread_weight(uint32_t cnt) {
+  return 512.0f * (1.0f + 1.0f / 1024.0f) * (float)cnt;
 }
 
 // a - (float)f16 half of h, in one v_fma_mix_f32: fma(h, m1, a) with m1 = -1

@@ -3,11 +3,12 @@
 //
 // The register-pooled frame forward (cnsl-conv-frame.hip) writes, besides the
 // pooled output and its routing mask, the pooled output's statistics blocks
-// (the GEMM's, cu-gemm-f16x3.hip: [max[n], min[n]]) per frame (rowmax[2R]:
-// max |value| bits, exact; min nonzero |value| bits, 0 for none) and per
-// pooled column (colmax[2 npool]: the max's binade with every mantissa bit
-// set, which is all the GEMM's power-of-two scale reads; the min's binade
-// with none, 0xffffffff for none, all the spread test reads), through
+// (the GEMM's, cu-gemm-f16x3.hip: [max[n], min[n], cnt[n]]) per frame
+// (rowmax[3R]: max |value| bits, exact; min nonzero |value| bits, 0 for
+// none) and per pooled column (colmax[3 npool]: the max's binade with every
+// mantissa bit set, which is all the GEMM's power-of-two scale reads; the
+// min's binade with none, 0xffffffff for none, all the spread test reads),
+// and the count of a spread group's small elements (f16-split.h), through
 // partial_words of scratch (kcnn_pool_stats_partial_words).  The FC
 // GEMMs that read the pooled output take them as its f16x3 operand scales
 // (kaldi-lite/cu-gemm-f16x3.hip via CuGemmStatsHint) instead of reading it

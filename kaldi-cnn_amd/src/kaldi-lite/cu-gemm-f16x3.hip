@@ -21,12 +21,17 @@
 //
 // and the kernel keeps the first three (one v_mfma_f32_32x32x16_f16 each,
 // smallest first, accumulated in fp32), then C = acc * 2^-(s_a + s_b) by an
-// exact ldexp.  The error per product is under 3 * 2^-22 of |a b|, 14x inside
-// the 1e-5 * S parity bound, and the f16 MFMA runs at the bf16
-// rate: half the matrix-core work of bf16x6 for the same split VALU.  The
-// scale also takes the operand range out of the question: a row of values
-// near FLT_MAX or below 2^-110 is scaled like any other (the bf16x6 split
-// loses bits there).
+// exact ldexp.  The bound is therefore per group, not per product: for two
+// groups that are not "spread" (no element more than 20 binades under the
+// group's max, f16-split.h) every element is held to 2^-19, and a product is
+// within (2 * 2^-19 + 2^-22) S of exact; a product touching a spread group
+// is checked at its store against the count of the group's small elements
+// and recomputed in fp32 when the check cannot clear it (tile_epilogue,
+// gemm_f16x3_reduce_kernel).  So every finite C element meets the 1e-5 * S
+// parity bar whatever the operands' range; the scale puts a
+// whole row near FLT_MAX or of fp32 subnormals into f16's range like any
+// other (the bf16x6 split loses bits there).  The f16 MFMA runs at the bf16
+// rate: half the matrix-core work of bf16x6 for the same split VALU.
 //
 // The scales come from per-row / per-column max |x| (kl_absmax_rows /
 // kl_absmax_cols: the bit patterns of |x|, whose unsigned order is the
@@ -42,12 +47,13 @@
 // of 32, operands loaded as fp32 by branch-free buffer loads two steps ahead,
 // split in registers into two f16 planes of swizzled [row][k] LDS images
 // (double-buffered, 2 x 48 KB), one barrier per step.  Thin outputs split K
-// over workgroups; the last workgroup of a tile sums the partial tiles in a
-// fixed order.
+// over workgroups into partial slabs, which gemm_f16x3_reduce_kernel sums in
+// a fixed order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "cnslmat/f16-split.h"
 #include "cnslmat/hip-util.h"
@@ -79,7 +85,7 @@ struct GemmF16Args {
   float *part;                   // ksplit > 1: the partial slabs [ksplit][M][N]
   const uint32_t *amax, *bmax;   // max |x| bits per row of op(A), per column of op(B)
   const uint32_t *amin, *bmin;   // min nonzero |x| bits (0: none), the same groups
-  float wspread;                 // a spread group's weight in the store's check (tile_epilogue)
+  const uint32_t *acnt, *bcnt;   // spread groups: their elements below 2^-3 after the scale
   const float *bias;             // nullable: C += bias[col] on every row (after alpha, beta)
   int M, N, K, lda, ldb, ldc;
   int kps, ksplit, tiles_m, tiles_n;
@@ -313,8 +319,8 @@ struct Loader {
 
 
 // The scale exponents of the tile's rows and columns into sexp, and each
-// one's spread weight into sw (wspread for a spread group, f16-split.h
-// spread(), else 0).  Returns bit 0: one of them is an Inf / NaN row or
+// one's spread weight into sw (f16-split.h spread_weight: 0 unless the group
+// is spread).  Returns bit 0: one of them is an Inf / NaN row or
 // column; bit 1: one of them is spread (both for the whole block).
 __device__ __forceinline__ int tile_scales(const GemmF16Args &p, int *sexp, float *sw, int row0,
                                            int col0, int tid) {
@@ -325,11 +331,11 @@ __device__ __forceinline__ int tile_scales(const GemmF16Args &p, int *sexp, floa
     if (i < BM) {
       if (row0 + i < p.M) {
         s = scale_exp(p.amax[row0 + i]);
-        if (kcnn::f16x3::spread(p.amax[row0 + i], p.amin[row0 + i])) w = p.wspread;
+        w = kcnn::f16x3::spread_weight(p.acnt[row0 + i]);
       }
     } else if (col0 + i - BM < p.N) {
       s = scale_exp(p.bmax[col0 + i - BM]);
-      if (kcnn::f16x3::spread(p.bmax[col0 + i - BM], p.bmin[col0 + i - BM])) w = p.wspread;
+      w = kcnn::f16x3::spread_weight(p.bcnt[col0 + i - BM]);
     }
     sexp[i] = s;
     sw[i] = w;
@@ -342,19 +348,28 @@ __device__ __forceinline__ int tile_scales(const GemmF16Args &p, int *sexp, floa
 
 // One C element by a whole wave, for the store's check (called with the same
 // row and column in every lane): fp32 products of op(A) row i and op(B)
-// column j, lane l summing k = l, l + 64, ... in order, then a butterfly over
-// the lanes (every lane ends with the same bits: deterministic)
+// column j in a fixed order per lane, then a butterfly over the lanes (every
+// lane ends with the same bits: deterministic)
 __device__ __forceinline__ float wave_dot(const GemmF16Args &p, bool a_kc, bool b_kc, int row,
                                           int col, int lane) {
-  float s = 0.0f;
-  for (int k = lane; k < p.K; k += 64) {
-    const float a = a_kc ? p.A[(int64_t)row * p.lda + k] : p.A[(int64_t)k * p.lda + row];
-    const float b = b_kc ? p.B[(int64_t)col * p.ldb + k] : p.B[(int64_t)k * p.ldb + col];
-    s = fmaf(a, b, s);
-  }
+  auto ak = [&](int k) {
+    return a_kc ? p.A[(int64_t)row * p.lda + k] : p.A[(int64_t)k * p.lda + row];
+  };
+  auto bk = [&](int k) {
+    return b_kc ? p.B[(int64_t)col * p.ldb + k] : p.B[(int64_t)k * p.ldb + col];
+  };
+  // four partial sums (k = lane + 64 (4 i + j) into sum j): eight loads in
+  // flight per lane instead of one
+  float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  int k = lane;
+  for (; k + 192 < p.K; k += 256)
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
-  return s;
+    for (int j = 0; j < 4; ++j) s[j] = fmaf(ak(k + 64 * j), bk(k + 64 * j), s[j]);
+  for (; k < p.K; k += 64) s[0] = fmaf(ak(k), bk(k), s[0]);
+  float t = (s[0] + s[1]) + (s[2] + s[3]);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) t += __shfl_xor(t, d);
+  return t;
 }
 __device__ __forceinline__ float store_value(const GemmF16Args &p, float v, float *o, int col) {
   float r = p.beta == 0.0f ? p.alpha * v : p.alpha * v + p.beta * *o;
@@ -425,13 +440,17 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
       const int ec = sexp[BM + cl];
       if (col >= p.N || ec == SKIP) continue;
       const float wc = check ? sw[BM + cl] : 0.0f;
+      // this 32 x 32 block's check: one of its columns or rows is spread
+      // (wave-uniform; most blocks skip it)
+      const bool bcheck =
+          check && (__ballot(wc != 0.0f || sw[wm * 64 + i * 32 + (lane & 31)] != 0.0f) != 0);
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int rl = wm * 64 + i * 32 + (g & 3) + 8 * (g >> 2) + 4 * half2;
         const int row = row0 + rl;
         const int er = sexp[rl];
         if (row >= p.M || er == SKIP) continue;
-        if (check) {
+        if (bcheck) {
           const float thr = wc + sw[rl];
           if (thr != 0.0f && !(fabsf(acc[i][j][g]) >= thr)) {
             rej |= (uint64_t)1 << ((2 * i + j) * 16 + g);
@@ -702,10 +721,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
 
     // step t: tile t+1 is in set (t+1) & 1 (split in phase A), which then
     // takes tile t+3 (phase B; a step past T issues its clamped loads too)
-    auto step = [&](int t, LA &lan, LB &lbn) {
+    // (more_c: std::true_type where the step is known not to be the last,
+    // so its split and next-fragment reads carry no branch; std::false_type
+    // for the last step, which has neither)
+    auto step = [&](int t, LA &lan, LB &lbn, auto more_c) {
       const char *buf = lds + (t & 1) * BUF;
       char *nbuf = lds + ((t + 1) & 1) * BUF;
-      const bool more = t + 1 < T;  // uniform
+      constexpr bool more = decltype(more_c)::value;
       const int kv = t + 2 == T ? klast : BK;
       uint32_t ph[4], pl[4];
       // phase A
@@ -733,11 +755,17 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
       }
     };
     int t = 0;
-    for (; t + 1 < T; t += 2) {
-      step(t, la[1], lb[1]);
-      step(t + 1, la[0], lb[0]);
+    // every step of the loop has a successor; the last one or two after it
+    for (; t + 2 < T; t += 2) {
+      step(t, la[1], lb[1], std::true_type{});
+      step(t + 1, la[0], lb[0], std::true_type{});
     }
-    if (t < T) step(t, la[1], lb[1]);
+    if (t + 1 < T) {
+      step(t, la[1], lb[1], std::true_type{});
+      step(t + 1, la[0], lb[0], std::false_type{});
+    } else {
+      step(t, la[1], lb[1], std::false_type{});
+    }
   }
 
   tile_epilogue<A_KC, B_KC>(p, sexp, sw, acc, split, row0, col0, flags, tid);
@@ -746,11 +774,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
 // Max |x| and min nonzero |x| per row or per column of a pitched fp32 matrix,
 // as the bit patterns of |x| (unsigned order = magnitude order, Inf / NaN
 // above every finite value; max and min are order-independent, so the
-// results are deterministic).  A group's statistics block is [max[n], min[n]]
-// (n groups): max[i] sets the group's f16x3 scale, min[i] (0: no nonzero
-// element) says whether the group is "spread" (f16-split.h: an element far
-// enough below the max to lose low bits, which the GEMM's store then checks,
-// tile_epilogue).  The min is taken as min(|x| - 1) in wrapping unsigned
+// results are deterministic), and for a spread group (f16-split.h: an
+// element far enough below the max to lose low bits, which the GEMM's store
+// then checks, tile_epilogue) the count of its elements held only to 2^-25
+// (an integer: deterministic).  A group set's statistics block is
+// [max[n], min[n], cnt[n]] (n groups): max[i] sets the group's f16x3 scale,
+// min[i] (0: no nonzero element) says whether the group is spread, cnt[i]
+// (0 unless spread) sizes its check.  The min is taken as min(|x| - 1) in wrapping unsigned
 // arithmetic, so a zero (0 - 1 = 0xffffffff) never wins, then + 1.
 // A GEMM needs op(A)'s rows and op(B)'s columns; both operands' statistics
 // go in one launch (stats_kernel: blocks [0, a.blocks) for A, then B's) and
@@ -764,7 +794,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
 //    x 4 chunk groups per block, combined through LDS).
 struct StatOp {
   const float *X;
-  uint32_t *out;   // the statistics block: maxima then minima, per row (mode 0) or column (1)
+  uint32_t *out;   // the statistics block [max, min, cnt], per row (mode 0) or column (1)
   uint32_t *part;  // mode 1: [2][rbk][cols] partials (maxima, then minima - 1)
   int rows, cols, ld, mode, vec;
   int blocks;      // of stats_kernel
@@ -789,6 +819,21 @@ __device__ __forceinline__ void mm1(uint32_t &m, uint32_t &n, float x) {
   n = min(n, a - 1u);
 }
 
+// the nonzero |x| of row r below bound (a spread row's count; sweep of
+// stats_rows' shape)
+__device__ __forceinline__ uint32_t count_small_row(const StatOp &o, const float *x, float bound,
+                                                    int c, int step) {
+  uint32_t n = 0;
+  for (; c < o.cols; c += step)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (c + i < o.cols) {
+        const float a = fabsf(x[c + i]);
+        n += (a < bound && a != 0.0f) ? 1u : 0u;
+      }
+  return n;
+}
+
 __device__ __forceinline__ void stats_rows(const StatOp &o, int blk, uint32_t *red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool wide = o.rpb == 1;
@@ -796,7 +841,8 @@ __device__ __forceinline__ void stats_rows(const StatOp &o, int blk, uint32_t *r
   if (r >= o.rows) return;  // (wide: uniform over the block)
   const float *x = X_row(o, r);
   const int step = wide ? 1024 : 256;  // floats per sweep of the row
-  int c = (wide ? threadIdx.x : lane) * 4;
+  const int c0 = (wide ? threadIdx.x : lane) * 4;
+  int c = c0;
   uint32_t m = 0, n = 0xffffffffu;
   if (o.vec) {
     for (; c + 3 * step + 4 <= o.cols; c += 4 * step) {
@@ -817,21 +863,33 @@ __device__ __forceinline__ void stats_rows(const StatOp &o, int blk, uint32_t *r
     m = max(m, (uint32_t)__shfl_xor((int)m, d));
     n = min(n, (uint32_t)__shfl_xor((int)n, d));
   }
-  if (!wide) {
+  if (wide) {  // the block's maxima / minima through LDS, to every thread
     if (lane == 0) {
-      o.out[r] = m;
-      o.out[o.rows + r] = n + 1u;
+      red[wave] = m;
+      red[4 + wave] = n;
     }
-    return;
+    __syncthreads();
+    m = max(max(red[0], red[1]), max(red[2], red[3]));
+    n = min(min(red[4], red[5]), min(red[6], red[7]));
   }
-  if (lane == 0) {
-    red[wave] = m;
-    red[4 + wave] = n;
+  // a spread row (f16-split.h) counts its small elements (a second sweep
+  // of the row, from L2); every other row's count is 0
+  uint32_t cnt = 0;
+  if (kcnn::f16x3::spread(m, n + 1u)) {  // uniform over the wave (the block)
+    cnt = count_small_row(o, x, kcnn::f16x3::small_bound(m), c0, step);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, d);
+    if (wide) {
+      __syncthreads();  // (red's maxima read above)
+      if (lane == 0) red[8 + wave] = cnt;
+      __syncthreads();
+      cnt = red[8] + red[9] + red[10] + red[11];
+    }
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    o.out[r] = max(max(red[0], red[1]), max(red[2], red[3]));
-    o.out[o.rows + r] = min(min(red[4], red[5]), min(red[6], red[7])) + 1u;
+  if (wide ? threadIdx.x == 0 : lane == 0) {
+    o.out[r] = m;
+    o.out[o.rows + r] = n + 1u;
+    o.out[2 * (size_t)o.rows + r] = cnt;
   }
 }
 
@@ -879,7 +937,7 @@ __device__ __forceinline__ void stats_cols(const StatOp &o, int blk) {
 }
 
 __global__ __launch_bounds__(256) void stats_kernel(StatOp a, StatOp b) {
-  __shared__ uint32_t red[8];
+  __shared__ uint32_t red[12];
   const bool isa = (int)blockIdx.x < a.blocks;  // uniform
   const StatOp &o = isa ? a : b;
   const int blk = isa ? blockIdx.x : blockIdx.x - a.blocks;
@@ -887,13 +945,16 @@ __global__ __launch_bounds__(256) void stats_kernel(StatOp a, StatOp b) {
   else stats_cols(o, blk);
 }
 
+// The column maxima / minima over the partials (64 columns per block, 4
+// groups of partials through LDS); the counts zeroed for stats_count_kernel.
 __global__ __launch_bounds__(256) void stats_finalize_kernel(StatOp a, StatOp b) {
   __shared__ uint32_t red[2][4][64];
   const int fa = a.mode == 1 ? a.fblocks : 0;
   const bool isa = (int)blockIdx.x < fa;
   const StatOp &o = isa ? a : b;
   const int blk = isa ? blockIdx.x : blockIdx.x - fa;
-  const int c = blk * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blk * 64 + lane;
   uint32_t m = 0, n = 0xffffffffu;
   if (c < o.cols) {
     const uint32_t *pm = o.part, *pn = o.part + (size_t)o.rbk * o.cols;
@@ -902,15 +963,51 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(StatOp a, StatOp b)
       n = min(n, pn[(size_t)q * o.cols + c]);
     }
   }
-  red[0][grp][threadIdx.x & 63] = m;
-  red[1][grp][threadIdx.x & 63] = n;
+  red[0][grp][lane] = m;
+  red[1][grp][lane] = n;
   __syncthreads();
+  m = max(max(red[0][0][lane], red[0][1][lane]), max(red[0][2][lane], red[0][3][lane]));
+  n = min(min(red[1][0][lane], red[1][1][lane]), min(red[1][2][lane], red[1][3][lane]));
   if (grp == 0 && c < o.cols) {
-    o.out[c] = max(max(red[0][0][threadIdx.x], red[0][1][threadIdx.x]),
-                   max(red[0][2][threadIdx.x], red[0][3][threadIdx.x]));
-    o.out[o.cols + c] = min(min(red[1][0][threadIdx.x], red[1][1][threadIdx.x]),
-                            min(red[1][2][threadIdx.x], red[1][3][threadIdx.x])) + 1u;
+    o.out[c] = m;
+    o.out[o.cols + c] = n + 1u;
+    o.out[2 * (size_t)o.cols + c] = 0;
   }
+}
+
+// The spread columns' counts (f16-split.h) after the finalize: block (cb,
+// rc) takes 64 columns x a chunk of 64 rows, leaves at once unless one of
+// its columns is spread (rare), and otherwise reads its rows' 64-column
+// segments (one coalesced 256-B row piece per wave and row) and adds each
+// spread column's count of small elements by an integer atomic (exact and
+// order-independent).
+constexpr int CNT_ROWS = 64;
+__global__ __launch_bounds__(256) void stats_count_kernel(StatOp a, StatOp b) {
+  const int na = a.mode == 1 && a.blocks ? ((a.cols + 63) / 64) * ((a.rows + CNT_ROWS - 1) / CNT_ROWS)
+                                         : 0;
+  const bool isa = (int)blockIdx.x < na;
+  const StatOp &o = isa ? a : b;
+  const int blk = isa ? blockIdx.x : blockIdx.x - na;
+  const int ncb = (o.cols + 63) / 64;
+  const int cb = blk % ncb, rc = blk / ncb;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = cb * 64 + lane;
+  bool spr = false;
+  float bound = 0.0f;
+  if (c < o.cols) {
+    const uint32_t mx = o.out[c];
+    spr = kcnn::f16x3::spread(mx, o.out[o.cols + c]);
+    if (spr) bound = kcnn::f16x3::small_bound(mx);
+  }
+  if (__ballot(spr) == 0) return;  // block-uniform (the same columns in every wave)
+  const int r0 = rc * CNT_ROWS, r1 = min(o.rows, r0 + CNT_ROWS);
+  uint32_t cnt = 0;
+  if (spr)
+    for (int r = r0 + wave; r < r1; r += 4) {
+      const float v = fabsf(X_row(o, r)[c]);
+      cnt += (v < bound && v != 0.0f) ? 1u : 0u;
+    }
+  if (cnt) atomicAdd(o.out + 2 * (size_t)o.cols + c, cnt);
 }
 
 // a statistics pass over X (rows x cols, pitch ld): mode 0 per row, 1 per
@@ -946,7 +1043,7 @@ int stats_launch(const StatOp &a, const StatOp &b, hipStream_t st) {
   for (const StatOp *o : {&a, &b})
     if (o->blocks == 0 && o->out) {
       const size_t n = o->mode == 0 ? (size_t)std::max(o->rows, 0) : (size_t)std::max(o->cols, 0);
-      if (n && hipMemsetAsync(o->out, 0, 2 * n * 4, st) != hipSuccess) return (int)hipGetLastError();
+      if (n && hipMemsetAsync(o->out, 0, 3 * n * 4, st) != hipSuccess) return (int)hipGetLastError();
     }
   const int nb = a.blocks + b.blocks;
   if (nb == 0) return 0;
@@ -959,6 +1056,13 @@ int stats_launch(const StatOp &a, const StatOp &b, hipStream_t st) {
   if (a2.blocks == 0) a2.mode = 0;  // nothing to finalize
   if (b2.blocks == 0) b2.mode = 0;
   hipLaunchKernelGGL(stats_finalize_kernel, dim3(nf), dim3(256), 0, st, a2, b2);
+  rc = kcnn::launch_status();
+  if (rc) return rc;
+  auto ncnt = [](const StatOp &o) {
+    return o.mode == 1 && o.blocks ? ((o.cols + 63) / 64) * ((o.rows + CNT_ROWS - 1) / CNT_ROWS)
+                                   : 0;
+  };
+  hipLaunchKernelGGL(stats_count_kernel, dim3(ncnt(a2) + ncnt(b2)), dim3(256), 0, st, a2, b2);
   return kcnn::launch_status();
 }
 
@@ -966,80 +1070,125 @@ int stats_launch(const StatOp &a, const StatOp &b, hipStream_t st) {
 // (slab rows padded to np4 = N rounded up to 4: 16-B reads; a quad's columns
 // past N are not stored); elements of an Inf / NaN row or column are the
 // epilogue's (split 0).  The spread check of tile_epilogue on the summed
-// value (unscaled: the threshold times 2^-(s_row + s_col)); rejected elements
-// are recomputed by their wave (fix_rejected).  The grid-stride loop runs a
-// block-uniform number of times, so every lane of a wave reaches the fix.
-__global__ void gemm_f16x3_reduce_kernel(GemmF16Args p, int a_kc, int b_kc) {
-  const int S = p.ksplit, M = p.M, N = p.N;
-  const int np4 = (N + 3) & ~3, nq = np4 >> 2;
-  const int64_t total = (int64_t)M * nq;
-  const int64_t plane = (int64_t)M * np4;
-  const int lane = threadIdx.x & 63;
+// value (unscaled: the threshold times 2^-(s_row + s_col)); a rejected
+// element is not stored but listed in LDS, and after the block's elements
+// the block's waves recompute the listed ones (wave_dot).  A block with more
+// rejections than the list holds stores none of the list and instead re-runs
+// its elements, recomputing every rejected one in a wave-uniform loop.
+constexpr int REJ_CAP = 256;
+__device__ __forceinline__ uint32_t reduce_quad(const GemmF16Args &p, int64_t e, int nq, int np4,
+                                                int64_t plane, int &r, int &c, bool store) {
+  const int N = p.N;
+  r = (int)(e / nq);
+  c = (int)(e - (int64_t)r * nq) * 4;
+  const uint32_t ar = p.amax[r];
+  if (ar >= NONFINITE) return 0;
+  const float *q = p.part + (int64_t)r * np4 + c;
+  float4 v = *reinterpret_cast<const float4 *>(q);
+  for (int k = 1; k < p.ksplit; ++k) {
+    const float4 w = *reinterpret_cast<const float4 *>(q + k * plane);
+    v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+  }
+  const float sv[4] = {v.x, v.y, v.z, v.w};
+  // the check's thresholds (0: no check) of the four columns; the counts
+  // are 0 unless a group is spread, so one test skips it all
+  float thr[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  const uint32_t cr = p.acnt[r];
+  uint32_t cc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) cc[i] = c + i < N ? p.bcnt[c + i] : 0u;
+  const bool any = (cr | cc[0] | cc[1] | cc[2] | cc[3]) != 0;
+  if (any) {
+    const int er = scale_exp(ar);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (c + i >= N) continue;
+      const uint32_t bc = p.bmax[c + i];
+      if (bc >= NONFINITE || (cr | cc[i]) == 0) continue;
+      thr[i] = __builtin_amdgcn_ldexpf(
+          kcnn::f16x3::spread_weight(cr) + kcnn::f16x3::spread_weight(cc[i]),
+          -(er + scale_exp(bc)));
+    }
+  }
+  float *o = p.C + (int64_t)r * p.ldc + c;
+  const bool fin = c + 4 <= N && max(max(p.bmax[c], p.bmax[c + 1]),
+                                     max(p.bmax[c + 2], p.bmax[c + 3])) < NONFINITE;
+  if (!any && fin && ((p.ldc & 3) | ((uintptr_t)p.C & 15)) == 0) {
+    if (store) {  // one 16-B store (the same values)
+      float4 ov = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (p.beta != 0.0f) ov = *reinterpret_cast<const float4 *>(o);
+      const float oi[4] = {ov.x, ov.y, ov.z, ov.w};
+      float w[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        w[i] = p.beta == 0.0f ? p.alpha * sv[i] : p.alpha * sv[i] + p.beta * oi[i];
+        if (p.bias) w[i] += p.bias[c + i];
+      }
+      *reinterpret_cast<float4 *>(o) = make_float4(w[0], w[1], w[2], w[3]);
+    }
+    return 0;
+  }
+  uint32_t rej = 0;  // bit i: column c + i is rejected
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (c + i >= N || p.bmax[c + i] >= NONFINITE) continue;
+    if (thr[i] != 0.0f && !(fabsf(sv[i]) >= thr[i])) {
+      rej |= 1u << i;
+      continue;
+    }
+    if (store) o[i] = store_value(p, sv[i], o + i, c + i);
+  }
+  return rej;
+}
+
+__global__ __launch_bounds__(256) void gemm_f16x3_reduce_kernel(GemmF16Args p, int a_kc,
+                                                                int b_kc) {
+  __shared__ int rej_r[REJ_CAP], rej_c[REJ_CAP];
+  __shared__ int rej_n;
+  const int np4 = (p.N + 3) & ~3, nq = np4 >> 2;
+  const int64_t total = (int64_t)p.M * nq;
+  const int64_t plane = (int64_t)p.M * np4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) rej_n = 0;
+  __syncthreads();
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    int r, c;
+    uint32_t rej = reduce_quad(p, e, nq, np4, plane, r, c, true);
+    while (rej) {  // rare
+      const int i = __builtin_ctz(rej);
+      rej &= rej - 1;
+      const int slot = atomicAdd(&rej_n, 1);
+      if (slot < REJ_CAP) {
+        rej_r[slot] = r;
+        rej_c[slot] = c + i;
+      }
+    }
+  }
+  __syncthreads();
+  const int n = rej_n;  // block-uniform
+  if (n == 0) return;
+  if (n <= REJ_CAP) {
+    for (int j = wave; j < n; j += 4) {
+      const int row = rej_r[j], col = rej_c[j];
+      const float v = wave_dot(p, a_kc != 0, b_kc != 0, row, col, lane);
+      if (lane == 0) {
+        float *o = p.C + (int64_t)row * p.ldc + col;
+        *o = store_value(p, v, o, col);
+      }
+    }
+    return;
+  }
+  // the list overflowed (none of it stored): find every rejected element
+  // again (the kept ones are stored already) and recompute it by its wave
   for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < total;
        base += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = base + threadIdx.x;
     int r = 0, c = 0;
-    uint64_t rej = 0;  // bit i: column c + i is rejected
-    if (e < total) {
-      r = (int)(e / nq);
-      c = (int)(e - (int64_t)r * nq) * 4;
-      const float *q = p.part + (int64_t)r * np4 + c;
-      float4 v = *reinterpret_cast<const float4 *>(q);
-      for (int k = 1; k < S; ++k) {
-        const float4 w = *reinterpret_cast<const float4 *>(q + k * plane);
-        v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
-      }
-      const uint32_t ar = p.amax[r];
-      if (ar < NONFINITE) {
-        const float sv[4] = {v.x, v.y, v.z, v.w};
-        // the check's thresholds (0: no check) of the four columns
-        const bool sr = kcnn::f16x3::spread(ar, p.amin[r]);
-        const int er = scale_exp(ar);
-        float thr[4];
-        bool any = false;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          thr[i] = 0.0f;
-          if (c + i >= N) continue;
-          const uint32_t bc = p.bmax[c + i];
-          const bool sc = bc < NONFINITE && kcnn::f16x3::spread(bc, p.bmin[c + i]);
-          if (sr || sc) {
-            thr[i] = __builtin_amdgcn_ldexpf((sr ? p.wspread : 0.0f) + (sc ? p.wspread : 0.0f),
-                                             -(er + scale_exp(bc)));
-            any = true;
-          }
-        }
-        float *o = p.C + (int64_t)r * p.ldc + c;
-        const bool fin = c + 4 <= N && max(max(p.bmax[c], p.bmax[c + 1]),
-                                           max(p.bmax[c + 2], p.bmax[c + 3])) < NONFINITE;
-        if (!any && fin && ((p.ldc & 3) | ((uintptr_t)p.C & 15)) == 0) {
-          // one 16-B store (the same values)
-          float4 ov = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-          if (p.beta != 0.0f) ov = *reinterpret_cast<const float4 *>(o);
-          const float oi[4] = {ov.x, ov.y, ov.z, ov.w};
-          float w[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            w[i] = p.beta == 0.0f ? p.alpha * sv[i] : p.alpha * sv[i] + p.beta * oi[i];
-            if (p.bias) w[i] += p.bias[c + i];
-          }
-          *reinterpret_cast<float4 *>(o) = make_float4(w[0], w[1], w[2], w[3]);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if (c + i >= N || p.bmax[c + i] >= NONFINITE) continue;
-            if (thr[i] != 0.0f && !(fabsf(sv[i]) >= thr[i])) {
-              rej |= 1u << i;
-              continue;
-            }
-            o[i] = store_value(p, sv[i], o + i, c + i);
-          }
-        }
-      }
-    }
-    fix_rejected(p, a_kc != 0, b_kc != 0, rej, lane, [&](int l, int n, int &row, int &col) {
+    const uint32_t rej = e < total ? reduce_quad(p, e, nq, np4, plane, r, c, false) : 0u;
+    fix_rejected(p, a_kc != 0, b_kc != 0, rej, lane, [&](int l, int bit, int &row, int &col) {
       row = __builtin_amdgcn_readlane(r, l);
-      col = __builtin_amdgcn_readlane(c, l) + n;
+      col = __builtin_amdgcn_readlane(c, l) + bit;
     });
   }
 }
@@ -1151,11 +1300,11 @@ static int gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alph
   hipStream_t st = kcnn::as_stream(stream);
   GemmF16Args a{};
   a.A = A; a.B = B; a.C = C; a.amax = amax; a.bmax = bmax; a.bias = bias;
-  a.amin = amax + M;  // statistics blocks [max[n], min[n]] (stats_rows)
+  // statistics blocks [max[n], min[n], cnt[n]] (stats_rows, stats_finalize_kernel)
+  a.amin = amax + M;
+  a.acnt = amax + 2 * (size_t)M;
   a.bmin = bmax + N;
-  // a spread group's share of the store's check threshold, scaled units:
-  // 2^9 K (f16-split.h; the bound is in DESIGN 3, "spread groups")
-  a.wspread = 512.0f * (float)K * (1.0f + 1.0f / 1024.0f);
+  a.bcnt = bmax + 2 * (size_t)N;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.alpha = alpha; a.beta = beta;
   a.tiles_m = (M + BM - 1) / BM;
@@ -1208,7 +1357,7 @@ namespace {
 size_t stats_ws_words(int M, int N, int K, int transA, int transB) {
   const size_t pa = transA ? stat_part_words(K, M, 1) : 0;
   const size_t pb = transB ? 0 : stat_part_words(K, N, 1);
-  return 2 * ((size_t)M + N) + 4 + pa + pb;
+  return 3 * ((size_t)M + N) + 4 + pa + pb;
 }
 }  // namespace
 extern "C" size_t kl_gemm_f16x3_full_workspace_bytes(int M, int N, int K) {
@@ -1247,8 +1396,8 @@ extern "C" int kl_gemm_f16x3_bias(int transA, int transB, int M, int N, int K, f
   if (!ws || ws_bytes < kl_gemm_f16x3_full_workspace_bytes(M, N, K))
     return (int)hipErrorInvalidValue;
   uint32_t *amax = reinterpret_cast<uint32_t *>(static_cast<char *>(ws) + pb);
-  uint32_t *bmax = amax + 2 * M;  // statistics blocks: [max, min] per group
-  uint32_t *parta = bmax + 2 * N + 4;
+  uint32_t *bmax = amax + 3 * (size_t)M;  // statistics blocks: [max, min, cnt] per group
+  uint32_t *parta = bmax + 3 * (size_t)N + 4;
   uint32_t *partb = parta + (transA ? stat_part_words(K, M, 1) : 0);
   const StatOp sa = amax_given ? StatOp{}
                     : transA   ? stat_op(A, K, M, lda, 1, amax, parta)

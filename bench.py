@@ -634,6 +634,7 @@ def main():
     # blocks are warm, so the capture allocates nothing).  Data-parallel steps
     # (RCCL inside) and a failed capture run the step eagerly.
     graph = None
+    graph_mallocs = None
     if not dist and args.graph:
         try:
             gs = torch.cuda.Stream()
@@ -647,6 +648,10 @@ def main():
             g.replay()
             torch.cuda.synchronize()
             graph = g
+            # the graph writes into the caching allocator's blocks that the
+            # capture step held; freed after it, they stay unused only while
+            # nothing allocates: checked around every replay
+            graph_mallocs = kcnn.device_malloc_calls()
         except Exception as e:  # noqa: BLE001 -- reported, eager fallback
             print(f"bench: HIP graph capture failed ({e!r}); eager steps", file=sys.stderr)
         kcnn.sync_stream()  # back to the current stream
@@ -659,9 +664,13 @@ def main():
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
+        replay = graph is not None and not profiled
+        if replay and kcnn.device_malloc_calls() != graph_mallocs:
+            raise SystemExit("bench: a device allocation since the HIP graph's capture; "
+                             "its blocks may be reused, the replays are not safe")
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            if graph is not None and not profiled:
+            if replay:
                 graph.replay()
             else:
                 step()

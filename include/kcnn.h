@@ -45,6 +45,10 @@ extern "C" {
 /* ---- runtime ------------------------------------------------------------ */
 const char *kcnn_last_error(void);
 const char *kcnn_version(void);
+/* Device allocations (CuDevice::Malloc calls) so far: a HIP graph captured
+ * over the caching allocator's blocks stays valid while this does not move
+ * (bench.py --graph). */
+unsigned long long kcnn_device_malloc_calls(void);
 /* CuDevice::SelectGpuId(use_gpu, device) (upstream cu-device.h). */
 int kcnn_init(int device);
 int kcnn_set_stream(kcnn_stream_t stream);

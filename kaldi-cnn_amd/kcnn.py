@@ -58,6 +58,7 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         L.kcnn_last_error.restype = ctypes.c_char_p
         L.kcnn_version.restype = ctypes.c_char_p
+        L.kcnn_device_malloc_calls.restype = ctypes.c_ulonglong
         for name in ("kcnn_component_new_from_string", "kcnn_component_read",
                      "kcnn_component_copy"):
             getattr(L, name).restype = ctypes.c_void_p
@@ -137,6 +138,11 @@ def set_fusion(mode):
     """kcnn_nnet runtime: fuse Conv -> Maxpool (see kcnn.h).  0 / False: off;
     1 / True: on, the conv output not stored; 2: on, the conv output stored."""
     check(lib().kcnn_set_fusion(int(mode)))
+
+
+def device_malloc_calls() -> int:
+    """CuDevice::Malloc calls so far (kcnn_device_malloc_calls)."""
+    return int(lib().kcnn_device_malloc_calls())
 
 
 def profile_string() -> str:

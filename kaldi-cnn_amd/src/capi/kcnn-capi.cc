@@ -192,6 +192,9 @@ extern "C" {
 
 const char *kcnn_last_error(void) { return g_err.c_str(); }
 const char *kcnn_version(void) { return "kcnn-mi355x 0.1 (gfx950)"; }
+unsigned long long kcnn_device_malloc_calls(void) {
+  return (unsigned long long)CuDevice::Instantiate().MallocCalls();
+}
 
 int kcnn_init(int device) {
   return guard([&] { CuDevice::Instantiate().SelectGpuId("yes", device); });

@@ -144,11 +144,17 @@ void CuDevice::SetStream(hipStream_t s) {
   rocblas_set_stream(blas_, stream_);
 }
 
+uint64_t CuDevice::MallocCalls() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return malloc_calls_;
+}
+
 void *CuDevice::Malloc(size_t bytes) {
   EnsureInit();
   if (bytes == 0) bytes = 1;
   const size_t sz = round_block(bytes);
   std::lock_guard<std::mutex> lk(mu_);
+  ++malloc_calls_;
   auto it = free_blocks_.find(sz);
   void *p = nullptr;
   if (it != free_blocks_.end()) {

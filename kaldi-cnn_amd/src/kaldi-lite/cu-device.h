@@ -61,6 +61,9 @@ class CuDevice {
   // Caching allocator (stream-ordered reuse on Stream()).
   void *Malloc(size_t bytes);
   void Free(void *ptr);
+  // Malloc calls so far (a HIP graph captured over cached blocks is replayed
+  // safely only while none is made: bench.py --graph checks it)
+  uint64_t MallocCalls();
   void ReleaseCache();
   size_t BytesInUse() const { return bytes_in_use_; }
   size_t BytesCached() const { return bytes_cached_; }
@@ -97,6 +100,7 @@ class CuDevice {
   std::multimap<size_t, void *> free_blocks_;
   std::map<void *, size_t> live_blocks_;
   size_t bytes_in_use_ = 0, bytes_cached_ = 0;
+  uint64_t malloc_calls_ = 0;
 };
 
 // Per-call scratch (split-K partials, GEMM workspaces) from the caching

@@ -33,6 +33,11 @@ POOL_OUT = P * G // PC
 PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 matrix (dense)
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 matrix (dense, spec)
+PEAK_F16_MFMA_TFLOPS = 2500.0   # MI355X_MICROARCH.md: f16 matrix (dense, spec; = bf16)
+# fp32-equivalent ceiling of each engine the kernels run fp32 products on:
+# the dense peak of its matrix type over its products per fp32 product
+ENGINE_PEAK_TFLOPS = {"fp32": PEAK_FP32_MFMA_TFLOPS, "bf16x6": PEAK_BF16_MFMA_TFLOPS / 6,
+                      "f16x3": PEAK_F16_MFMA_TFLOPS / 3}
 
 # Algorithmic work per frame (SURVEY 8d / BASELINE.md 3).
 CONV_FLOP_PER_PASS = 2 * P * G * KH * KW * C          # 2,230,272
@@ -727,16 +732,12 @@ def main():
                            "parallelism": f"dp{world}"},
                 "conv": {"ms_per_step": round(conv_ms, 4),
                          "TFLOP/s": round(conv_flop / conv_ms / 1e9, 2) if conv_ms else None,
-                         # fp32 work over the fp32 MFMA peak; the layers compute
-                         # on the bf16 matrix cores (3-way operand splits, six
-                         # products), so this can pass 1.0: frac_of_bf16_peak
-                         # is what the six products occupy of that engine
-                         "mfma_frac": round(conv_flop / conv_ms / 1e9 / PEAK_FP32_MFMA_TFLOPS, 4)
-                         if conv_ms else None,
+                         # fp32 work over the bf16x6 engine's ceiling (the bf16
+                         # dense peak over its six products per fp32 product)
                          "engine": "bf16x6 (v_mfma_f32_32x32x16_bf16, fp32 operands split 3-way, "
                                    "6 products)",
-                         "frac_of_bf16_peak": round(6 * conv_flop / conv_ms / 1e9 /
-                                                    PEAK_BF16_MFMA_TFLOPS, 4) if conv_ms else None},
+                         "engine_frac": round(conv_flop / conv_ms / 1e9 /
+                                              ENGINE_PEAK_TFLOPS["bf16x6"], 4) if conv_ms else None},
                 "scopes_ms_per_step": scopes,
             }
             if conv_ms:
@@ -813,26 +814,42 @@ def main():
                              "bound": "mfma" if t_mfma > t_hbm else "hbm",
                              "GB/s": round(byts / ms / 1e6, 1),
                              "hbm_frac": round(byts / ms / 1e6 / PEAK_HBM_GBS, 4),
-                             "TFLOP/s": round(flop / ms / 1e9, 2) if flop else None,
-                             "mfma_frac": round(flop / ms / 1e9 / PEAK_FP32_MFMA_TFLOPS, 4) if flop else None}
+                             "TFLOP/s": round(flop / ms / 1e9, 2) if flop else None}
     gemm_mode = kcnn.get_kernel_family("gemm")
+    # each kernel's fp32 work against the engine it runs on: the f16x3 /
+    # bf16x6 split engines reach at most the f16 / bf16 dense peak over
+    # their products per fp32 product, so every engine_frac is <= 1
+    fam = {n: kcnn.get_kernel_family(n) for n in ("fwd_x6", "bwd_x6", "igemm_x6", "wgrad_x6")}
+    split = {2: "f16x3", 1: "bf16x6", 0: "fp32"}
+    role_family = {"conv_fwd": "fwd_x6", "conv_fwd_maxpool": "fwd_x6", "conv_bwd_fused": "bwd_x6",
+                   "conv_bwd_pooled": "bwd_x6", "conv_dgrad": "igemm_x6", "conv_wgrad": "wgrad_x6"}
+    for name, k in kernels.items():
+        if not k["flop"]:
+            continue
+        f = fam[role_family[name]]
+        eng = split.get(min(f, 2), "fp32") if name not in ("conv_bwd_fused", "conv_bwd_pooled",
+                                                            "conv_dgrad", "conv_wgrad") \
+            else ("bf16x6" if f else "fp32")
+        k["engine"], k["engine_peak_tflops"] = eng, round(ENGINE_PEAK_TFLOPS[eng], 1)
+        k["engine_frac"] = round(k["TFLOP/s"] / ENGINE_PEAK_TFLOPS[eng], 4)
     if k_fc[1]:
         # FullyConnectedComponent's three GEMMs (CuMatrixBase::AddMatMat): the
         # in-house f16x3 kernel (kaldi-lite/cu-gemm-f16x3.hip, 3 f16 products
         # per fp32 product) by default, bf16x6 (cu-gemm-x6.hip, 6 bf16
         # products) with KCNN_GEMM=1, rocBLAS sgemm with KCNN_GEMM=0
         fc_tf = FC_FLOP * B / (k_fc[0] / args.steps) / 1e9
-        nprod = {2: 3, 1: 6}.get(gemm_mode)
+        eng = {2: "f16x3", 1: "bf16x6"}.get(gemm_mode, "fp32")
         kernels["fc_gemms"] = {
             "engine": {2: "f16x3 (cu-gemm-f16x3.hip)", 1: "bf16x6 (cu-gemm-x6.hip)"}.get(
                 gemm_mode, "rocBLAS sgemm"),
             "ms_per_step": round(k_fc[0] / args.steps, 4),
             "TFLOP/s": round(fc_tf, 2),
-            "mfma_frac": round(fc_tf / PEAK_FP32_MFMA_TFLOPS, 4),
-            # split products per fp32 product: the share of the f16 / bf16
-            # engine (same dense peak) they occupy
-            "frac_of_bf16_peak": round(nprod * fc_tf / PEAK_BF16_MFMA_TFLOPS, 4) if nprod
-            else None}
+            # the three GEMMs' fp32 work over their engine's ceiling (f16 dense
+            # peak / 3 products for f16x3)
+            "roofline": {"bound": "mfma", "achieved": round(fc_tf, 2),
+                         "peak": round(ENGINE_PEAK_TFLOPS[eng], 1), "unit": "TFLOP/s",
+                         "frac": round(fc_tf / ENGINE_PEAK_TFLOPS[eng], 4), "engine": eng,
+                         "algorithmic_flop_per_step": FC_FLOP * B}}
 
     # Dominant hand-written hot-path kernel by time.
     dom = max((k for k in kernels if not k.startswith("fc_")),
@@ -864,17 +881,14 @@ def main():
                     "algorithmic_bytes_per_launch": dk["bytes"],
                     "algorithmic_flop_per_launch": dk["flop"],
                     "launch_ms": dk["ms"]}
-        if dk["bound"] == "mfma" and dom.startswith("conv_bwd") and \
-                os.environ.get("KCNN_BWD_X6", "1") != "0":
-            # the backward computes its fp32 products on the bf16 matrix cores
-            # (cnsl-conv-x6.hip: each operand split exactly into three bf16
-            # parts, six products kept).  `frac` prices the fp32 work against
-            # the fp32 MFMA peak (north_star's target); this is the fraction of
-            # the bf16 engine's dense peak that the six products occupy.
-            roofline["engine"] = {
-                "mfma": "v_mfma_f32_32x32x16_bf16, fp32 operands split 3-way, 6 products",
-                "bf16_dense_peak_tflops": PEAK_BF16_MFMA_TFLOPS,
-                "frac_of_bf16_peak": round(6 * achieved / PEAK_BF16_MFMA_TFLOPS, 4)}
+        if dk["bound"] == "mfma" and dk.get("engine"):
+            # `frac` prices the fp32 work against the fp32 MFMA peak
+            # (north_star's target); this is the same work against the engine
+            # the kernel runs on (bf16x6: each fp32 operand split exactly into
+            # three bf16 parts, six products kept; f16x3: two f16 planes,
+            # three products)
+            roofline["engine"] = {"name": dk["engine"], "peak": dk["engine_peak_tflops"],
+                                  "unit": "TFLOP/s", "frac": dk["engine_frac"]}
 
     if rank == 0:
         result = {

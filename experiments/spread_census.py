@@ -28,3 +28,19 @@ x = torch.randn((4096, 1320), generator=g, device="cuda")
 net.Propagate(x)
 P = net.Output(1).cpu().numpy()
 print("P rows:", spread_frac(P, 1), " P cols:", spread_frac(P, 0))
+# r05: pool_count_kernel's suspect frames (row min below 2^(E - 17), E the
+# largest value's binade) and the small elements they hold per column
+bits = np.abs(P).view(np.uint32).astype(np.int64)
+gm = bits.max()
+eg = int(ebits(np.array([max(gm, 0x7fffff)]))[0]) - 17
+rmin = np.where(bits > 0, bits, 0xffffffff).min(1)
+sus = (rmin != 0xffffffff) & (ebits(rmin) < eg)
+ecol = ebits(((bits >> 23).max(0) << 23) | 0x7fffff)
+small = (bits != 0) & (ebits(np.maximum(bits, 1)) < ecol[None, :] - 17)
+print("suspect frames:", int(sus.sum()), "of", P.shape[0], " small elements:", int(small.sum()),
+      " columns with one:", int(small.any(0).sum()), " E:", eg + 17)
+U = P.shape[1] // 363
+segmin = np.where(bits > 0, bits, 0xffffffff).reshape(P.shape[0], U, 363).min(2)
+ecolU = ecol.reshape(U, 363).max(1)
+print("suspect (frame, channel) segments:", int(((segmin != 0xffffffff) & (ebits(segmin) < ecolU[None, :] - 17)).sum()),
+      "of", P.shape[0] * U)

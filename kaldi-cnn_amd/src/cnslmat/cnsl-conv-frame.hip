@@ -322,10 +322,10 @@ __device__ __forceinline__ unsigned tie_mask4(float v0, float v1, float v2, floa
 
 // The register-pooled forward's statistics outputs (pool-stats.h): the
 // per-frame block rowmax [max[R], min[R], cnt[R]], the per-workgroup column
-// partials (exponent bytes: [nblk][npool] of the maxima, then of the minima)
-// and the column block colmax [max[npool], min[npool], cnt[npool]] that
-// pool_colmax_kernel fills (initialised here first); pool_count_kernel then
-// counts the spread groups' small elements
+// partials (the maxima's exponent bytes, [nblk][npool]) and the column block
+// colmax [max[npool], min[npool], cnt[npool]], which this kernel initialises
+// for pool_colmax_kernel (the maxima) and pool_count_kernel (the minima and
+// counts)
 struct RpStats {
   uint32_t *rowmax = nullptr, *partials = nullptr, *colmax = nullptr;
 };
@@ -351,14 +351,8 @@ __device__ __forceinline__ void frame_row_max(uint32_t *rslot, uint32_t v, uint3
 // GEMM's scale needs only the binade).  colmax[c] = the largest partial's
 // binade with every mantissa bit set, an upper bound in the max's binade (so
 // the same scale; 0x7f... for Inf; an all-zero column gets the subnormal
-// bound, harmless).  The minima the same way from the partials after them
-// ((|x| - 1) >> 23 per byte, 0xff: no nonzero value): colmax[npool + c] =
-// the smallest partial's binade with no mantissa bit (1 for the subnormal
-// binade; 0xffffffff when the column has no nonzero value, which the spread
-// test of f16-split.h reads as "none"), a lower bound in the min's binade
-// (the test reads only binades; one binade low where |x| is a power of two:
-// conservative).  colmax zeroed, the minima set to 0xffffffff; blockIdx.y
-// takes 32 workgroups' rows, atomic max / min across those chunks.
+// bound, harmless).  colmax zeroed by the forward; blockIdx.y takes 32
+// workgroups' rows, atomic max across those chunks.
 constexpr int COLMAX_ROWS = 32;
 __global__ __launch_bounds__(256) void pool_colmax_kernel(const uint8_t *__restrict__ pcol,
                                                            int nblk, int npool,
@@ -366,69 +360,169 @@ __global__ __launch_bounds__(256) void pool_colmax_kernel(const uint8_t *__restr
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= npool) return;
   const int b0 = blockIdx.y * COLMAX_ROWS, b1 = min(nblk, b0 + COLMAX_ROWS);
-  const uint8_t *pmin = pcol + (int64_t)nblk * npool;
-  uint32_t m = 0, n = 0xff;
-  for (int b = b0; b < b1; b++) {
-    m = max(m, (uint32_t)pcol[(int64_t)b * npool + c]);
-    n = min(n, (uint32_t)pmin[(int64_t)b * npool + c]);
-  }
+  uint32_t m = 0;
+  for (int b = b0; b < b1; b++) m = max(m, (uint32_t)pcol[(int64_t)b * npool + c]);
   atomicMax(colmax + c, (m << 23) | 0x7fffffu);
-  atomicMin(colmax + npool + c, n == 0xff ? 0xffffffffu : max(n << 23, 1u));
 }
 
-// The pooled output's spread groups (f16-split.h) counted after
-// pool_colmax_kernel: a block per 64 frame rows or 64 pooled columns writes
-// their cnt (0 unless spread), then reads each of its spread groups (rare)
-// with all 256 threads, eight loads in flight each, and sums the count.
-__global__ __launch_bounds__(256) void pool_count_kernel(const float *__restrict__ P, int ps,
-                                                         int R, int npool,
-                                                         uint32_t *__restrict__ rowblk,
-                                                         uint32_t *__restrict__ colblk) {
-  __shared__ uint32_t cred[4];
-  const int nrb = (R + 63) / 64;
-  const bool isrow = (int)blockIdx.x < nrb;  // uniform
-  const int g0 = (isrow ? (int)blockIdx.x : (int)blockIdx.x - nrb) * 64;
-  const int n = isrow ? R : npool;
-  uint32_t *blk = isrow ? rowblk : colblk;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int gi = g0 + lane;
-  uint32_t mx = 0;
-  bool spr = false;
-  if (gi < n) {
-    mx = blk[gi];
-    spr = f16x3::spread(mx, blk[n + gi]);
-    if (wave == 0) blk[2 * (size_t)n + gi] = 0;
+// The pooled output's small elements (f16-split.h) after pool_colmax_kernel,
+// from the exact row statistics and the column maxima, without a column
+// pass.  Every small element of any finite column lies below 2^eg, eg = E -
+// 17 for E the binade of the largest finite value (the largest row max), so
+// only the frames whose row min lies below 2^eg hold any ("suspect" frames:
+// 41 of c2's 4096), and reading those frame rows alone gives every
+// column's small elements: their count (atomic add) and min (atomic min;
+// 0xffffffff for none), which is all the spread test reads.  A column's
+// count covers its small elements whether or not it is spread: the 2^-25
+// bound the GEMM's check prices holds for every small element, so a count in
+// a column that is not spread only adds checks (rare: 4 of c2's 11616
+// columns have one).  A frame row's count is the GEMM's (0 unless spread),
+// taken on the same read.  Every block derives the suspect list from the
+// row statistics (the same list in every block) and takes its entries
+// block, block + grid, ...; a non-suspect frame's count is zeroed by the
+// block that owns the frame index in the same stride.
+constexpr int CNT_LIST = 16;  // suspect frames per block and pass (4096 frames / 256 blocks)
+__device__ __forceinline__ void count_elem(float x, float rbound, int eg, int c, int npool,
+                                           uint32_t *colblk, uint32_t &rcnt) {
+  const uint32_t v = __float_as_uint(x) & 0x7fffffffu;
+  if (v == 0) return;
+  rcnt += __uint_as_float(v) < rbound ? 1u : 0u;
+  const int ev = f16x3::ebits(v);
+  if (ev >= eg) return;  // the common case: small in no column
+  const uint32_t cm = colblk[c];
+  if (cm < f16x3::NONFINITE && ev < f16x3::ebits(cm) - 17) {
+    atomicMin(colblk + npool + c, v);
+    atomicAdd(colblk + 2 * (size_t)npool + c, 1u);
   }
-  uint64_t todo = __ballot(spr);  // the same in every wave
-  const int len = isrow ? npool : R;
-  while (todo) {  // block-uniform
-    const int l = __builtin_ctzll(todo);
-    todo &= todo - 1;
-    const int grp = g0 + l;
-    const float bound = f16x3::small_bound(__builtin_amdgcn_readlane(mx, l));
-    // element e of the group: row grp's column e, or column grp's row e
-    auto at = [&](int e) {
-      return fabsf(isrow ? P[(int64_t)grp * ps + e] : P[(int64_t)e * ps + grp]);
-    };
-    uint32_t cnt = 0;
-    int e = threadIdx.x;
-    for (; e + 7 * 256 < len; e += 8 * 256) {
-      float v[8];
+}
+__global__ __launch_bounds__(256) void pool_count_kernel(const float *__restrict__ P, int ps,
+                                                         int R, int npool, int vec,
+                                                         uint32_t *__restrict__ rowblk,
+                                                         uint32_t *colblk) {
+  __shared__ uint32_t red[2][4];
+  __shared__ int wsum[4];
+  __shared__ uint32_t list[CNT_LIST][3];  // (frame, row max, row min)
+  __shared__ int nlist;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x, nb = gridDim.x;
+  if (tid == 0) nlist = 0;
+  // thread t's frames t + 256 i, RF per pass (c2: one pass), their maxima
+  // and minima loaded together: one memory latency
+  constexpr int RF = 16;
+  int base = 0;
+  for (int f0 = 0; f0 < R; f0 += 256 * RF) {
+    uint32_t m[RF], mn[RF];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = at(e + j * 256);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) cnt += (v[j] < bound && v[j] != 0.0f) ? 1u : 0u;
+    for (int i = 0; i < RF; i++) {
+      const int f = f0 + tid + 256 * i;
+      m[i] = f < R ? rowblk[f] : 0u;
+      mn[i] = f < R ? rowblk[R + f] : 0u;
     }
-    for (; e < len; e += 256) {
-      const float v = at(e);
-      cnt += (v < bound && v != 0.0f) ? 1u : 0u;
+    // eg from the largest finite row max over all frames (any Inf / NaN
+    // row: every frame with a nonzero min is suspect, the safe side).  Only
+    // the first pass can hold them all: with more than one pass (R > 4096)
+    // the maxima are gathered by a first sweep below.
+    uint32_t gm = 0, inf = 0;
+    if (R <= 256 * RF) {
+#pragma unroll
+      for (int i = 0; i < RF; i++) {
+        if (m[i] < f16x3::NONFINITE) gm = max(gm, m[i]);
+        else inf = 1;
+      }
+    } else {
+      for (int f = tid; f < R; f += 256) {
+        const uint32_t x = rowblk[f];
+        if (x < f16x3::NONFINITE) gm = max(gm, x);
+        else inf = 1;
+      }
     }
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, d);
+    for (int d = 32; d >= 1; d >>= 1) {
+      gm = max(gm, (uint32_t)__shfl_xor((int)gm, d));
+      inf |= (uint32_t)__shfl_xor((int)inf, d);
+    }
+    if (lane == 0) {
+      red[0][wave] = gm;
+      red[1][wave] = inf;
+    }
     __syncthreads();
-    if (lane == 0) cred[wave] = cnt;
+    gm = max(max(red[0][0], red[0][1]), max(red[0][2], red[0][3]));
+    inf = red[1][0] | red[1][1] | red[1][2] | red[1][3];
+    const int eg = inf ? 1 << 20 : gm ? f16x3::ebits(max(gm, 0x7fffffu)) - 17 : -(1 << 20);
+    // the suspect frames, numbered in (pass, thread, i) order (the same list
+    // in every block): per-thread counts, then a block prefix sum
+    uint32_t sus = 0;
+#pragma unroll
+    for (int i = 0; i < RF; i++)
+      if (mn[i] != 0 && f16x3::ebits(mn[i]) < eg) sus |= 1u << i;
+    const int cnt = __builtin_popcount(sus);
+    int inc = cnt;  // inclusive prefix over the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(inc, d);
+      if (lane >= d) inc += v;
+    }
+    if (lane == 63) wsum[wave] = inc;
     __syncthreads();
-    if (threadIdx.x == 0) blk[2 * (size_t)n + grp] = cred[0] + cred[1] + cred[2] + cred[3];
+    int idx = base + inc - cnt;
+    for (int w = 0; w < wave; w++) idx += wsum[w];
+    const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+#pragma unroll
+    for (int i = 0; i < RF; i++) {
+      const int f = f0 + tid + 256 * i;
+      if ((sus >> i) & 1) {
+        if (idx % nb == b) {  // (< CNT_LIST entries: host grid)
+          const int k = atomicAdd(&nlist, 1);
+          list[k][0] = (uint32_t)f;
+          list[k][1] = m[i];
+          list[k][2] = mn[i];
+        }
+        idx++;
+      } else if (f < R && f % nb == b) {
+        rowblk[2 * (size_t)R + f] = 0;
+      }
+    }
+    base += total;
+    __syncthreads();  // (wsum, red reused)
+    // the block's suspect frames of this pass: each row read once, every
+    // thread's float4s of it loaded together
+    const int n = nlist;
+    constexpr int V = 12;  // float4 loads in flight per thread (c2: the whole row)
+    for (int e = 0; e < n; e++) {
+      const int f = (int)list[e][0];
+      const uint32_t rmx = list[e][1], rmn = list[e][2];
+      const float rbound = f16x3::spread(rmx, rmn) ? f16x3::small_bound(rmx) : 0.0f;
+      const float *x = P + (int64_t)f * ps;
+      uint32_t rcnt = 0;
+      if (vec) {
+        for (int c0 = tid * 4; c0 < npool; c0 += V * 1024) {
+          float4 q[V];
+#pragma unroll
+          for (int j = 0; j < V; j++)
+            if (c0 + j * 1024 < npool)
+              q[j] = *reinterpret_cast<const float4 *>(x + c0 + j * 1024);
+#pragma unroll
+          for (int j = 0; j < V; j++) {
+            const int c = c0 + j * 1024;
+            if (c >= npool) break;
+            count_elem(q[j].x, rbound, eg, c, npool, colblk, rcnt);
+            count_elem(q[j].y, rbound, eg, c + 1, npool, colblk, rcnt);
+            count_elem(q[j].z, rbound, eg, c + 2, npool, colblk, rcnt);
+            count_elem(q[j].w, rbound, eg, c + 3, npool, colblk, rcnt);
+          }
+        }
+      } else {
+        for (int c = tid; c < npool; c += 256) count_elem(x[c], rbound, eg, c, npool, colblk, rcnt);
+      }
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) rcnt += (uint32_t)__shfl_xor((int)rcnt, d);
+      if (lane == 0) red[0][wave] = rcnt;
+      __syncthreads();
+      if (tid == 0) rowblk[2 * (size_t)R + f] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+      __syncthreads();  // (red reused)
+    }
+    if (tid == 0) nlist = 0;
+    __syncthreads();
   }
 }
 
@@ -451,7 +545,6 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
   constexpr int NKT = SPL ? 16 * KS : 2 * KS;                   // tap entries (<= 32)
   float *Xs = reinterpret_cast<float *>(koff + NKT);            // [C*HW]
   uint32_t *rslot = reinterpret_cast<uint32_t *>(Xs + g.C * g.HW);  // [2][2][4] RP row max / min
-  uint8_t *Tmn = reinterpret_cast<uint8_t *>(rslot + 16);  // [npool] RP column min bytes
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = lane & 31, h = lane >> 5;
@@ -571,16 +664,15 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
   uint32_t *Tcol = reinterpret_cast<uint32_t *>(T);
   uint32_t *const prow = rps.rowmax, *const pcol = rps.partials;
   if constexpr (RP) {
-    for (int e = tid; e < g.G / PC * g.P; e += 256) {
-      Tcol[e] = 0;
-      Tmn[e] = 0xff;
-    }
-    // pool_colmax_kernel's atomic maxima start from 0, its minima from
-    // 0xffffffff (it runs after this grid)
+    for (int e = tid; e < g.G / PC * g.P; e += 256) Tcol[e] = 0;
+    // the column block for the kernels after this grid: pool_colmax_kernel's
+    // atomic maxima start from 0, pool_count_kernel's minima from 0xffffffff
+    // and its counts from 0
     const int c = blockIdx.x * 256 + tid;
     if (rps.colmax && c < g.G / PC * g.P) {
       rps.colmax[c] = 0;
       rps.colmax[g.G / PC * g.P + c] = 0xffffffffu;
+      rps.colmax[2 * g.G / PC * g.P + c] = 0;
     }
   }
   // the next frame's map is prefetched into registers while this one runs
@@ -783,22 +875,6 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
           int boff = (sl ? 128 : gb * 32) + 4 * h_f;  // Bz = Bs + 128
           asm volatile("" : "+v"(boff));
           const float *bb = Bs + boff;
-          // RP: the item's column-min bytes, read first so their latency
-          // passes under the epilogue's arithmetic
-          uint32_t old[RP ? 16 / PC : 1];
-          if constexpr (RP) {
-            const int pc = min(p, g.P - 1) + h_f * (4 / PC) * Pq;
-#pragma unroll
-            for (int j = 0; j < 16 / PC; j++) {
-              const int r0 = j * PC;
-              const int U = (gb * 32 + (r0 & 3) + 8 * (r0 >> 2)) / PC;
-#ifdef KCNN_EXPERIMENTS  // A/B: dbg & 1024 drops the column min bytes
-              old[j] = (dbg & 1024) ? 0u : Tmn[U * Pq + pc];
-#else
-              old[j] = Tmn[U * Pq + pc];
-#endif
-            }
-          }
           if constexpr (F16) {
             // y = acc * 2^-(sa + sb(p)) + b in one rounding (fp32 items:
             // acc * 1 + -0, i.e. acc itself)
@@ -849,9 +925,6 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
           if constexpr (RP) {
             // lanes past P hold position P - 1's values: their max lands there
             const int pc = min(p, g.P - 1) + h_f * (4 / PC) * Pq;
-            // the column min bytes (old: read at the item's start): each
-            // pooled column has one owner lane (two for column P - 1,
-            // holding the same value), so a plain read-modify-write
 #pragma unroll
             for (int j = 0; j < NGP; j++) {
               const uint32_t a = __float_as_uint(mx[j]) & 0x7fffffffu;  // never NaN
@@ -865,10 +938,6 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
               if (!(dbg & 4096))
 #endif
               rowmn = min(rowmn, u);
-#ifdef KCNN_EXPERIMENTS  // A/B: dbg & 1024 drops the column min bytes
-              if (!(dbg & 1024))
-#endif
-              Tmn[U * Pq + pc] = (uint8_t)min(old[j], u >> 23);
             }
             // (pinned per item: left free, the scheduler spreads the items'
             // statistics and holds 34 more VGPRs)
@@ -1159,9 +1228,6 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_regs_kernel(
       } else {
         for (int e = tid; e < npool; e += 256) dst[e] = (uint8_t)(Tcol[e] >> 23);
       }
-      // the minima's bytes after every workgroup's maxima
-      uint8_t *dsn = reinterpret_cast<uint8_t *>(pcol) + ((int64_t)gridDim.x + blockIdx.x) * npool;
-      for (int e = tid; e < npool; e += 256) dsn[e] = Tmn[e];
     }
   }
 #ifdef KCNN_PHASE_TIMING
@@ -2213,15 +2279,15 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
   // runs every item unfiltered: with 9-11 tiles a wave's third tile would
   // pool and take statistics from registers no gather wrote)
   const int ntile = (g.P + 31) / 32;
-  // (its LDS: 16 more words of row slots and a min byte per pooled column)
-  const size_t lds_rp = lds + 8 * 4 + ((((size_t)g.G / 4) * g.P + 15) & ~(size_t)15);
+  // (its LDS: 8 more words of row slots)
+  const size_t lds_rp = lds + 8 * 4;
   const bool rp = out == nullptr && pc == 4 && !win3 && g.G == 128 && ntile == 4 * 3 &&
                   ar == 2 && lds_rp <= (size_t)kFrameLdsMax;
   // the register-pooled kernel also gives the pooled output's max |value|
   // bits per frame and per column (stats, when the caller passes room)
   RpStats rps;
   if (rp && stats && stats->partials &&
-      stats->partial_words * 4 >= 2 * (size_t)grid * (g.G / pc) * g.P &&
+      stats->partial_words >= ((size_t)grid * (g.G / pc) * g.P + 3) / 4 &&
       (size_t)grid * 256 >= (size_t)(g.G / pc) * g.P) {
     rps.rowmax = stats->rowmax;
     rps.partials = stats->partials;
@@ -2266,8 +2332,12 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
                        dim3((npool + 255) / 256, (grid + COLMAX_ROWS - 1) / COLMAX_ROWS),
                        dim3(256), 0, st, reinterpret_cast<const uint8_t *>(pcol), (int)grid,
                        npool, stats->colmax);
-    hipLaunchKernelGGL(pool_count_kernel, dim3((g.R + 63) / 64 + (npool + 63) / 64), dim3(256),
-                       0, st, pool, ps, g.R, npool, stats->rowmax, stats->colmax);
+    const int vec = ps % 4 == 0 && (uintptr_t)pool % 16 == 0;
+    // 256 blocks (c2: 41 suspect frames of 4096, at most one each); a pass
+    // of 4096 frames gives a block at most 4096 / 256 = CNT_LIST of them
+    const int cgrid = std::min(g.R, 256);
+    hipLaunchKernelGGL(pool_count_kernel, dim3(cgrid), dim3(256), 0, st, pool, ps, g.R, npool,
+                       vec, stats->rowmax, stats->colmax);
     stats->produced = 1;
   }
   return (int)hipGetLastError();
@@ -2275,8 +2345,8 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
 
 size_t kcnn_pool_stats_partial_words(const ConvGeom &g, int pc) {
   // frame_grid(g, 2) workgroups (the f16x3 register kernel) x pooled columns
-  // exponent bytes, for the maxima and the minima
-  return pc > 0 ? (2 * (size_t)frame_grid(g, 2) * (g.G / pc) * g.P + 3) / 4 : 0;
+  // exponent bytes of the maxima
+  return pc > 0 ? ((size_t)frame_grid(g, 2) * (g.G / pc) * g.P + 3) / 4 : 0;
 }
 
 int kcnn_conv_dgrad_frame(const ConvGeom &g, const float *dY, int dys,

@@ -7,12 +7,14 @@
 // (rowmax[3R]: max |value| bits, exact; min nonzero |value| bits, 0 for
 // none) and per pooled column (colmax[3 npool]: the max's binade with every
 // mantissa bit set, which is all the GEMM's power-of-two scale reads; the
-// min's binade with none, 0xffffffff for none, all the spread test reads),
-// and the count of a spread group's small elements (f16-split.h), through
-// partial_words of scratch (kcnn_pool_stats_partial_words).  The FC
-// GEMMs that read the pooled output take them as its f16x3 operand scales
-// (kaldi-lite/cu-gemm-f16x3.hip via CuGemmStatsHint) instead of reading it
-// once more.  produced = 1 when the launch wrote them.
+// min over the column's elements under its small bound, 0xffffffff for
+// none, which is all the spread test reads), and the count of the small
+// elements (f16-split.h; a frame's only when it is spread, a column's in any
+// case), through partial_words of scratch
+// (kcnn_pool_stats_partial_words).  The FC GEMMs that read the pooled output
+// take them as its f16x3 operand scales (kaldi-lite/cu-gemm-f16x3.hip via
+// CuGemmStatsHint) instead of reading it once more.  produced = 1 when the
+// launch wrote them.
 #ifndef KCNN_CNSLMAT_POOL_STATS_H_
 #define KCNN_CNSLMAT_POOL_STATS_H_
 

@@ -88,6 +88,8 @@ struct GemmF16Args {
   const uint32_t *acnt, *bcnt;   // spread groups: their elements below 2^-3 after the scale
   const float *bias;             // nullable: C += bias[col] on every row (after alpha, beta)
   int M, N, K, lda, ldb, ldc;
+  int bvec;                      // bmax, bcnt 16-B aligned and N % 4 == 0 (the reduce's loads)
+  int dbg;                       // KCNN_EXPERIMENTS builds: A/B switches
   int kps, ksplit, tiles_m, tiles_n;
   float alpha, beta;
 };
@@ -352,20 +354,35 @@ __device__ __forceinline__ int tile_scales(const GemmF16Args &p, int *sexp, floa
 // lane ends with the same bits: deterministic)
 __device__ __forceinline__ float wave_dot(const GemmF16Args &p, bool a_kc, bool b_kc, int row,
                                           int col, int lane) {
-  auto ak = [&](int k) {
-    return a_kc ? p.A[(int64_t)row * p.lda + k] : p.A[(int64_t)k * p.lda + row];
-  };
-  auto bk = [&](int k) {
-    return b_kc ? p.B[(int64_t)col * p.ldb + k] : p.B[(int64_t)k * p.ldb + col];
-  };
+  // element k of the row of op(A) / column of op(B): qa[k * sa], qb[k * sb]
+  // (wave-uniform strides; the pointers step, no per-load index products)
+  const int64_t sa = a_kc ? 1 : p.lda, sb = b_kc ? 1 : p.ldb;
+  const float *qa = (a_kc ? p.A + (int64_t)row * p.lda : p.A + row) + lane * sa;
+  const float *qb = (b_kc ? p.B + (int64_t)col * p.ldb : p.B + col) + lane * sb;
+  const int64_t da = 64 * sa, db = 64 * sb;
   // four partial sums (k = lane + 64 (4 i + j) into sum j): eight loads in
   // flight per lane instead of one
   float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   int k = lane;
-  for (; k + 192 < p.K; k += 256)
+#pragma unroll 1
+  for (; k + 192 < p.K; k += 256) {
+    float x[4], y[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) s[j] = fmaf(ak(k + 64 * j), bk(k + 64 * j), s[j]);
-  for (; k < p.K; k += 64) s[0] = fmaf(ak(k), bk(k), s[0]);
+    for (int j = 0; j < 4; ++j) {
+      x[j] = qa[j * da];
+      y[j] = qb[j * db];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[j] = fmaf(x[j], y[j], s[j]);
+    qa += 4 * da;
+    qb += 4 * db;
+  }
+#pragma unroll 1
+  for (; k < p.K; k += 64) {
+    s[0] = fmaf(*qa, *qb, s[0]);
+    qa += da;
+    qb += db;
+  }
   float t = (s[0] + s[1]) + (s[2] + s[3]);
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) t += __shfl_xor(t, d);
@@ -780,8 +797,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
 // (an integer: deterministic).  A group set's statistics block is
 // [max[n], min[n], cnt[n]] (n groups): max[i] sets the group's f16x3 scale,
 // min[i] (0: no nonzero element) says whether the group is spread, cnt[i]
-// (0 unless spread) sizes its check.  The min is taken as min(|x| - 1) in wrapping unsigned
-// arithmetic, so a zero (0 - 1 = 0xffffffff) never wins, then + 1.
+// (0 unless spread here) sizes its check.  The check is sound for any count
+// that covers the group's small elements (each is held to 2^-25, spread or
+// not), so a producer may also count them in a group that is not spread
+// (the pooled output's columns, pool-stats.h): that only adds checks.  The
+// min is taken as min(|x| - 1) in wrapping unsigned arithmetic, so a zero
+// (0 - 1 = 0xffffffff) never wins, then + 1.
 // A GEMM needs op(A)'s rows and op(B)'s columns; both operands' statistics
 // go in one launch (stats_kernel: blocks [0, a.blocks) for A, then B's) and
 // one more (stats_finalize_kernel) when either is per column:
@@ -957,10 +978,24 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(StatOp a, StatOp b)
   const int c = blk * 64 + lane;
   uint32_t m = 0, n = 0xffffffffu;
   if (c < o.cols) {
-    const uint32_t *pm = o.part, *pn = o.part + (size_t)o.rbk * o.cols;
-    for (int q = grp; q < o.rbk; q += 4) {
-      m = max(m, pm[(size_t)q * o.cols + c]);
-      n = min(n, pn[(size_t)q * o.cols + c]);
+    const uint32_t *pm = o.part + c, *pn = o.part + (size_t)o.rbk * o.cols + c;
+    int q = grp;
+    for (; q + 28 < o.rbk; q += 32) {  // eight maxima and eight minima in flight
+      uint32_t a[8], b[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a[j] = pm[(size_t)(q + 4 * j) * o.cols];
+        b[j] = pn[(size_t)(q + 4 * j) * o.cols];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        m = max(m, a[j]);
+        n = min(n, b[j]);
+      }
+    }
+    for (; q < o.rbk; q += 4) {
+      m = max(m, pm[(size_t)q * o.cols]);
+      n = min(n, pn[(size_t)q * o.cols]);
     }
   }
   red[0][grp][lane] = m;
@@ -1002,11 +1037,16 @@ __global__ __launch_bounds__(256) void stats_count_kernel(StatOp a, StatOp b) {
   if (__ballot(spr) == 0) return;  // block-uniform (the same columns in every wave)
   const int r0 = rc * CNT_ROWS, r1 = min(o.rows, r0 + CNT_ROWS);
   uint32_t cnt = 0;
-  if (spr)
-    for (int r = r0 + wave; r < r1; r += 4) {
-      const float v = fabsf(X_row(o, r)[c]);
-      cnt += (v < bound && v != 0.0f) ? 1u : 0u;
+  if (spr) {  // the wave's CNT_ROWS / 4 rows loaded together
+    float v[CNT_ROWS / 4];
+#pragma unroll
+    for (int i = 0; i < CNT_ROWS / 4; ++i) {
+      const int r = r0 + wave + 4 * i;
+      v[i] = r < r1 ? fabsf(X_row(o, r)[c]) : 0.0f;
     }
+#pragma unroll
+    for (int i = 0; i < CNT_ROWS / 4; ++i) cnt += (v[i] < bound && v[i] != 0.0f) ? 1u : 0u;
+  }
   if (cnt) atomicAdd(o.out + 2 * (size_t)o.cols + c, cnt);
 }
 
@@ -1081,57 +1121,74 @@ __device__ __forceinline__ uint32_t reduce_quad(const GemmF16Args &p, int64_t e,
   const int N = p.N;
   r = (int)(e / nq);
   c = (int)(e - (int64_t)r * nq) * 4;
-  const uint32_t ar = p.amax[r];
-  if (ar >= NONFINITE) return 0;
+  // every load of the quad issued before the first test: the slabs, the
+  // row's statistics and the four columns' (one 16-B load each when the
+  // blocks allow; a column past N reads as non-finite, i.e. not stored)
   const float *q = p.part + (int64_t)r * np4 + c;
   float4 v = *reinterpret_cast<const float4 *>(q);
-  for (int k = 1; k < p.ksplit; ++k) {
-    const float4 w = *reinterpret_cast<const float4 *>(q + k * plane);
-    v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
-  }
-  const float sv[4] = {v.x, v.y, v.z, v.w};
-  // the check's thresholds (0: no check) of the four columns; the counts
-  // are 0 unless a group is spread, so one test skips it all
-  float thr[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  const uint32_t cr = p.acnt[r];
-  uint32_t cc[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) cc[i] = c + i < N ? p.bcnt[c + i] : 0u;
-  const bool any = (cr | cc[0] | cc[1] | cc[2] | cc[3]) != 0;
-  if (any) {
-    const int er = scale_exp(ar);
+  float4 w = p.ksplit > 1 ? *reinterpret_cast<const float4 *>(q + plane) : v;
+  const uint32_t ar = p.amax[r], cr = p.acnt[r];
+  uint32_t bm[4], cc[4];
+  if (p.bvec) {
+    const uint4 x = *reinterpret_cast<const uint4 *>(p.bmax + c);
+    const uint4 y = *reinterpret_cast<const uint4 *>(p.bcnt + c);
+    bm[0] = x.x; bm[1] = x.y; bm[2] = x.z; bm[3] = x.w;
+    cc[0] = y.x; cc[1] = y.y; cc[2] = y.z; cc[3] = y.w;
+  } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if (c + i >= N) continue;
-      const uint32_t bc = p.bmax[c + i];
-      if (bc >= NONFINITE || (cr | cc[i]) == 0) continue;
-      thr[i] = __builtin_amdgcn_ldexpf(
-          kcnn::f16x3::spread_weight(cr) + kcnn::f16x3::spread_weight(cc[i]),
-          -(er + scale_exp(bc)));
+      bm[i] = c + i < N ? p.bmax[c + i] : NONFINITE;
+      cc[i] = c + i < N ? p.bcnt[c + i] : 0u;
     }
   }
+  if (p.ksplit > 1) {
+    v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    for (int k = 2; k < p.ksplit; ++k) {
+      w = *reinterpret_cast<const float4 *>(q + k * plane);
+      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    }
+  }
+  if (ar >= NONFINITE) return 0;
+  const float sv[4] = {v.x, v.y, v.z, v.w};
+#ifdef KCNN_EXPERIMENTS  // A/B: KCNN_RED_DEBUG & 1 drops the spread check
+  const bool any = !(p.dbg & 1) && (cr | cc[0] | cc[1] | cc[2] | cc[3]) != 0;
+#else
+  // the counts are 0 unless a group is spread, so one test skips the check
+  const bool any = (cr | cc[0] | cc[1] | cc[2] | cc[3]) != 0;
+#endif
   float *o = p.C + (int64_t)r * p.ldc + c;
-  const bool fin = c + 4 <= N && max(max(p.bmax[c], p.bmax[c + 1]),
-                                     max(p.bmax[c + 2], p.bmax[c + 3])) < NONFINITE;
+  const bool fin = max(max(bm[0], bm[1]), max(bm[2], bm[3])) < NONFINITE;
   if (!any && fin && ((p.ldc & 3) | ((uintptr_t)p.C & 15)) == 0) {
     if (store) {  // one 16-B store (the same values)
       float4 ov = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
       if (p.beta != 0.0f) ov = *reinterpret_cast<const float4 *>(o);
       const float oi[4] = {ov.x, ov.y, ov.z, ov.w};
-      float w[4];
+      float wv[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        w[i] = p.beta == 0.0f ? p.alpha * sv[i] : p.alpha * sv[i] + p.beta * oi[i];
-        if (p.bias) w[i] += p.bias[c + i];
+        wv[i] = p.beta == 0.0f ? p.alpha * sv[i] : p.alpha * sv[i] + p.beta * oi[i];
+        if (p.bias) wv[i] += p.bias[c + i];
       }
-      *reinterpret_cast<float4 *>(o) = make_float4(w[0], w[1], w[2], w[3]);
+      *reinterpret_cast<float4 *>(o) = make_float4(wv[0], wv[1], wv[2], wv[3]);
     }
     return 0;
+  }
+  // the check's thresholds (0: no check) of the four columns
+  float thr[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (any) {
+    const int er = scale_exp(ar);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (bm[i] >= NONFINITE || (cr | cc[i]) == 0) continue;
+      thr[i] = __builtin_amdgcn_ldexpf(
+          kcnn::f16x3::spread_weight(cr) + kcnn::f16x3::spread_weight(cc[i]),
+          -(er + scale_exp(bm[i])));
+    }
   }
   uint32_t rej = 0;  // bit i: column c + i is rejected
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    if (c + i >= N || p.bmax[c + i] >= NONFINITE) continue;
+    if (bm[i] >= NONFINITE) continue;  // (and columns past N)
     if (thr[i] != 0.0f && !(fabsf(sv[i]) >= thr[i])) {
       rej |= 1u << i;
       continue;
@@ -1305,6 +1362,9 @@ static int gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alph
   a.acnt = amax + 2 * (size_t)M;
   a.bmin = bmax + N;
   a.bcnt = bmax + 2 * (size_t)N;
+  a.bvec = N % 4 == 0 && (uintptr_t)a.bmax % 16 == 0 && (uintptr_t)a.bcnt % 16 == 0;
+  static const int red_dbg = KCNN_KNOB("KCNN_RED_DEBUG", 0);
+  a.dbg = red_dbg;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.alpha = alpha; a.beta = beta;
   a.tiles_m = (M + BM - 1) / BM;

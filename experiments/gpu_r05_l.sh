@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 9
 O=gpurun_out/${TAG:-r05l}; mkdir -p $O; export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_pool_stats.py tests/test_gpu_gemm.py tests/test_gpu_nnet.py tests/test_gpu_fwd_f16.py tests/test_gpu_fullsize.py -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest.txt 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_pool_stats.py tests/test_gpu_components.py tests/test_gpu_gemm.py tests/test_gpu_nnet.py tests/test_gpu_fwd_f16.py tests/test_gpu_fullsize.py -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest.txt 2>&1
 rc=$?; echo "pytest rc $rc"; grep -E "FAILED|ERROR|differs" $O/pytest.txt | head -20; tail -1 $O/pytest.txt
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit 3
 for i in 1 2 3; do for lib in r04 new; do

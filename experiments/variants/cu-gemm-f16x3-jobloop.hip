@@ -78,7 +78,7 @@ constexpr int ROWB = BK * 2;                  // bytes per LDS row of one plane
 constexpr int A_PLANE = BM * ROWB;            // 16 KB
 constexpr int B_PLANE = BN * ROWB;            // 8 KB
 constexpr int BUF = 2 * (A_PLANE + B_PLANE);  // 48 KB
-constexpr int LDS_BYTES = 2 * BUF + (BM + BN) * 8;  // + sexp, sw
+constexpr int LDS_BYTES = 2 * BUF + 2 * (BM + BN) * 8;  // + two sets of sexp, sw
 
 struct GemmF16Args {
   const float *A, *B;
@@ -668,138 +668,189 @@ template <int AM, int BMODE, bool RAG>
 __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
   constexpr bool A_KC = AM == LK, B_KC = BMODE == LK;
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  int *sexp = reinterpret_cast<int *>(lds + 2 * BUF);
-  float *sw = reinterpret_cast<float *>(sexp + BM + BN);
-  const int tid = threadIdx.x;
+  // two sets of the tile's scales (sexp [BM + BN] ints, then sw [BM + BN]
+  // floats): a persistent block fills the next job's while its current job
+  // still needs its own for the epilogue
+  int *sexp_s[2];
+  float *sw_s[2];
+  sexp_s[0] = reinterpret_cast<int *>(lds + 2 * BUF);
+  sw_s[0] = reinterpret_cast<float *>(sexp_s[0] + BM + BN);
+  sexp_s[1] = reinterpret_cast<int *>(sw_s[0] + BM + BN);
+  sw_s[1] = reinterpret_cast<float *>(sexp_s[1] + BM + BN);
   const float m1 = kcnn::f16x3::opaque_m1();
-  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
+  // jobs (tile, split) in XCD chunks: the consecutive jobs that share an A
+  // panel run on one XCD (its L2).  The blocks of XCD x (b & 7 == x) take
+  // its chunk's jobs round robin: one each when the grid has a block per
+  // job, several in a persistent grid (the next job's first loads are then
+  // issued before the current job's epilogue)
   const int nb = gridDim.x, b = blockIdx.x;
-  const int xcd = b & 7, q = nb >> 3, rr = nb & 7;
-  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
-  const int split = lid % p.ksplit;
-  const int rest = lid / p.ksplit;
-  const int tn = rest % p.tiles_n, tm = rest / p.tiles_n;
-  const int row0 = tm * BM, col0 = tn * BN;
-  const int kbeg = split * p.kps;
-  const int kend = min(p.K, kbeg + p.kps);
-  const int T = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  const int klast = kend - kbeg - (T - 1) * BK;
+  const int nj = p.tiles_m * p.tiles_n * p.ksplit;
+  const int xcd = b & 7, q = nj >> 3, rr = nj & 7;
+  const int xbeg = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
+  const int xend = xbeg + q + (xcd < rr ? 1 : 0);
+  const int nbx = (nb >> 3) + ((nb & 7) > xcd ? 1 : 0);  // blocks on this XCD
+  int lid = xbeg + (b >> 3);
+  if (lid >= xend) return;  // (uniform: a persistent grid larger than a chunk)
 
-  const int flags = tile_scales(p, sexp, sw, row0, col0, tid);
-  const float *baseA = A_KC ? p.A + (int64_t)row0 * p.lda : p.A + (int64_t)kbeg * p.lda + row0;
-  const float *baseB = B_KC ? p.B + (int64_t)col0 * p.ldb : p.B + (int64_t)kbeg * p.ldb + col0;
-  const int vra = p.M - row0, vrb = p.N - col0;
-  const int64_t endA = A_KC ? ((int64_t)(vra - 1) * p.lda + p.K) * 4
-                            : ((int64_t)(p.K - 1 - kbeg) * p.lda + vra) * 4;
-  const int64_t endB = B_KC ? ((int64_t)(vrb - 1) * p.ldb + p.K) * 4
-                            : ((int64_t)(p.K - 1 - kbeg) * p.ldb + vrb) * 4;
-  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)baseA, (short)0, (int)(endA < 0x7fffffff ? endA : 0x7fffffff), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)baseB, (short)0, (int)(endB < 0x7fffffff ? endB : 0x7fffffff), 0x00020000);
-  auto kk = [&](int t, bool kc) { return (kc ? kbeg : 0) + min(t, T - 1) * BK; };
+  struct Job {
+    int split, row0, col0, kbeg, T, klast, vra, vrb;
+    __amdgpu_buffer_rsrc_t rsA, rsB;
+  };
+  auto setup = [&](int id) {
+    Job J;
+    J.split = id % p.ksplit;
+    const int rest = id / p.ksplit;
+    const int tn = rest % p.tiles_n, tm = rest / p.tiles_n;
+    J.row0 = tm * BM;
+    J.col0 = tn * BN;
+    J.kbeg = J.split * p.kps;
+    const int kend = min(p.K, J.kbeg + p.kps);
+    J.T = kend > J.kbeg ? (kend - J.kbeg + BK - 1) / BK : 0;
+    J.klast = kend - J.kbeg - (J.T - 1) * BK;
+    const float *baseA =
+        A_KC ? p.A + (int64_t)J.row0 * p.lda : p.A + (int64_t)J.kbeg * p.lda + J.row0;
+    const float *baseB =
+        B_KC ? p.B + (int64_t)J.col0 * p.ldb : p.B + (int64_t)J.kbeg * p.ldb + J.col0;
+    J.vra = p.M - J.row0;
+    J.vrb = p.N - J.col0;
+    const int64_t endA = A_KC ? ((int64_t)(J.vra - 1) * p.lda + p.K) * 4
+                              : ((int64_t)(p.K - 1 - J.kbeg) * p.lda + J.vra) * 4;
+    const int64_t endB = B_KC ? ((int64_t)(J.vrb - 1) * p.ldb + p.K) * 4
+                              : ((int64_t)(p.K - 1 - J.kbeg) * p.ldb + J.vrb) * 4;
+    J.rsA = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)baseA, (short)0, (int)(endA < 0x7fffffff ? endA : 0x7fffffff), 0x00020000);
+    J.rsB = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)baseB, (short)0, (int)(endB < 0x7fffffff ? endB : 0x7fffffff), 0x00020000);
+    return J;
+  };
 
   using LA = Loader<BM, AM>;
   using LB = Loader<BN, BMODE>;
-  LA la[2];
-  LB lb[2];
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int g = 0; g < 16; ++g) acc[i][j][g] = 0.0f;
-  la[0].init_exp(sexp, tid);
-  la[1].init_exp(sexp, tid);
-  lb[0].init_exp(sexp + BM, tid);
-  lb[1].init_exp(sexp + BM, tid);
-
-  const int ar = wm * 64, br = wn * 64;
-  f16x8 fa0[2][2], fb0[2][2], fa1[2][2], fb1[2][2];
-  // r-th fragment of half s: A fragments (i, plane) first, then B
-  auto read_frag = [&](const char *buf, int s, int r, f16x8 (&fa)[2][2], f16x8 (&fb)[2][2]) {
-    if (r < 4) {
-      const int i = r >> 1, pl = r & 1;
-      fa[i][pl] = LA::frag(buf + pl * A_PLANE, ar + 32 * i, s, lane);
-    } else {
-      const int i = (r - 4) >> 1, pl = (r - 4) & 1;
-      fb[i][pl] = LB::frag(buf + 2 * A_PLANE + pl * B_PLANE, br + 32 * i, s, lane);
-    }
-  };
-  // n-th MFMA of a half: accumulator (n / 6, (n / 3) % 2), lo.hi, hi.lo, hi.hi
-  auto mfma_n = [&](int n, const f16x8 (&fa)[2][2], const f16x8 (&fb)[2][2]) {
-    const int i = n / 6, j = (n / 3) & 1, pr = n % 3;
-    constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};
-    acc[i][j] = mfma(fa[i][PA[pr]], fb[j][PB[pr]], acc[i][j]);
-  };
-
-  if (T > 0) {
-    la[0].load(rsA, p.lda, vra, kk(0, A_KC), tid);
-    lb[0].load(rsB, p.ldb, vrb, kk(0, B_KC), tid);
-    la[0].template store<A_PLANE, RAG>(lds, tid, T == 1 ? klast : BK, m1);
-    lb[0].template store<B_PLANE, RAG>(lds + 2 * A_PLANE, tid, T == 1 ? klast : BK, m1);
-    __builtin_amdgcn_sched_barrier(0);
-    la[1].load(rsA, p.lda, vra, kk(1, A_KC), tid);
-    lb[1].load(rsB, p.ldb, vrb, kk(1, B_KC), tid);
-    __builtin_amdgcn_sched_barrier(0);
-    la[0].load(rsA, p.lda, vra, kk(2, A_KC), tid);
-    lb[0].load(rsB, p.ldb, vrb, kk(2, B_KC), tid);
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 8; ++r) read_frag(lds, 0, r, fa0, fb0);
-
-    // step t: tile t+1 is in set (t+1) & 1 (split in phase A), which then
-    // takes tile t+3 (phase B; a step past T issues its clamped loads too)
-    // (more_c: std::true_type where the step is known not to be the last,
-    // so its split and next-fragment reads carry no branch; std::false_type
-    // for the last step, which has neither)
-    auto step = [&](int t, LA &lan, LB &lbn, auto more_c) {
-      const char *buf = lds + (t & 1) * BUF;
-      char *nbuf = lds + ((t + 1) & 1) * BUF;
-      constexpr bool more = decltype(more_c)::value;
-      const int kv = t + 2 == T ? klast : BK;
-      uint32_t ph[4], pl[4];
-      // phase A
-#pragma unroll
-      for (int n = 0; n < 12; ++n) {
-        mfma_n(n, fa0, fb0);
-        if (more) {
-          if (n < LA::NPIECE)
-            lan.template piece<A_PLANE, RAG>(nbuf, tid, n, kv, ph, pl, m1);
-          else if (n - LA::NPIECE < LB::NPIECE)
-            lbn.template piece<B_PLANE, RAG>(nbuf + 2 * A_PLANE, tid, n - LA::NPIECE, kv, ph, pl, m1);
-        }
-        if (n >= 2 && n < 10) read_frag(buf, 1, n - 2, fa1, fb1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      __syncthreads();
-      // phase B
-#pragma unroll
-      for (int n = 0; n < 12; ++n) {
-        mfma_n(n, fa1, fb1);
-        if (n == 1) lan.load(rsA, p.lda, vra, kk(t + 3, A_KC), tid);
-        if (n == 3) lbn.load(rsB, p.ldb, vrb, kk(t + 3, B_KC), tid);
-        if (more && n >= 2 && n < 10) read_frag(nbuf, 0, n - 2, fa0, fb0);
-        __builtin_amdgcn_sched_barrier(0);
+  Job J = setup(lid);
+  int set = 0;
+  for (;;) {
+    // the thread id made opaque per job: the per-thread addresses are
+    // recomputed in each job instead of hoisted out of the job loop (held,
+    // they overflow the register file)
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63;
+    LA la[2];
+    LB lb[2];
+    f32x16 acc[2][2];
+    const int ar = wm * 64, br = wn * 64;
+    f16x8 fa0[2][2], fb0[2][2], fa1[2][2], fb1[2][2];
+    // r-th fragment of half s: A fragments (i, plane) first, then B
+    auto read_frag = [&](const char *buf, int s, int r, f16x8 (&fa)[2][2], f16x8 (&fb)[2][2]) {
+      if (r < 4) {
+        const int i = r >> 1, pl = r & 1;
+        fa[i][pl] = LA::frag(buf + pl * A_PLANE, ar + 32 * i, s, lane);
+      } else {
+        const int i = (r - 4) >> 1, pl = (r - 4) & 1;
+        fb[i][pl] = LB::frag(buf + 2 * A_PLANE + pl * B_PLANE, br + 32 * i, s, lane);
       }
     };
-    int t = 0;
-    // every step of the loop has a successor; the last one or two after it
-    for (; t + 2 < T; t += 2) {
-      step(t, la[1], lb[1], std::true_type{});
-      step(t + 1, la[0], lb[0], std::true_type{});
-    }
-    if (t + 1 < T) {
-      step(t, la[1], lb[1], std::true_type{});
-      step(t + 1, la[0], lb[0], std::false_type{});
-    } else {
-      step(t, la[1], lb[1], std::false_type{});
-    }
-  }
+    // n-th MFMA of a half: accumulator (n / 6, (n / 3) % 2), lo.hi, hi.lo, hi.hi
+    auto mfma_n = [&](int n, const f16x8 (&fa)[2][2], const f16x8 (&fb)[2][2]) {
+      const int i = n / 6, j = (n / 3) & 1, pr = n % 3;
+      constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};
+      acc[i][j] = mfma(fa[i][PA[pr]], fb[j][PB[pr]], acc[i][j]);
+    };
+    // a job's scales into set `set`, its loaders' exponents, and its first two
+    // K tiles' loads
+    auto begin_job = [&](const Job &J, int set) {
+      const int fl = tile_scales(p, sexp_s[set], sw_s[set], J.row0, J.col0, tid);
+      la[0].init_exp(sexp_s[set], tid);
+      la[1].init_exp(sexp_s[set], tid);
+      lb[0].init_exp(sexp_s[set] + BM, tid);
+      lb[1].init_exp(sexp_s[set] + BM, tid);
+      if (J.T > 0) {
+        la[0].load(J.rsA, p.lda, J.vra, A_KC ? J.kbeg : 0, tid);
+        lb[0].load(J.rsB, p.ldb, J.vrb, B_KC ? J.kbeg : 0, tid);
+        __builtin_amdgcn_sched_barrier(0);
+        la[1].load(J.rsA, p.lda, J.vra, (A_KC ? J.kbeg : 0) + min(1, J.T - 1) * BK, tid);
+        lb[1].load(J.rsB, p.ldb, J.vrb, (B_KC ? J.kbeg : 0) + min(1, J.T - 1) * BK, tid);
+      }
+      return fl;
+    };
 
-  tile_epilogue<A_KC, B_KC>(p, sexp, sw, acc, split, row0, col0, flags, tid);
+    const int flags = begin_job(J, set);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) acc[i][j][g] = 0.0f;
+    const int T = J.T, klast = J.klast;
+    auto kk = [&](int t, bool kc) { return (kc ? J.kbeg : 0) + min(t, T - 1) * BK; };
+    if (T > 0) {
+      la[0].template store<A_PLANE, RAG>(lds, tid, T == 1 ? klast : BK, m1);
+      lb[0].template store<B_PLANE, RAG>(lds + 2 * A_PLANE, tid, T == 1 ? klast : BK, m1);
+      __builtin_amdgcn_sched_barrier(0);
+      la[0].load(J.rsA, p.lda, J.vra, kk(2, A_KC), tid);
+      lb[0].load(J.rsB, p.ldb, J.vrb, kk(2, B_KC), tid);
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) read_frag(lds, 0, r, fa0, fb0);
+
+      // step t: tile t+1 is in set (t+1) & 1 (split in phase A), which then
+      // takes tile t+3 (phase B; a step past T issues its clamped loads too)
+      // (more_c: std::true_type where the step is known not to be the last,
+      // so its split and next-fragment reads carry no branch; std::false_type
+      // for the last step, which has neither)
+      auto step = [&](int t, LA &lan, LB &lbn, auto more_c) {
+        const char *buf = lds + (t & 1) * BUF;
+        char *nbuf = lds + ((t + 1) & 1) * BUF;
+        constexpr bool more = decltype(more_c)::value;
+        const int kv = t + 2 == T ? klast : BK;
+        uint32_t ph[4], pl[4];
+        // phase A
+#pragma unroll
+        for (int n = 0; n < 12; ++n) {
+          mfma_n(n, fa0, fb0);
+          if (more) {
+            if (n < LA::NPIECE)
+              lan.template piece<A_PLANE, RAG>(nbuf, tid, n, kv, ph, pl, m1);
+            else if (n - LA::NPIECE < LB::NPIECE)
+              lbn.template piece<B_PLANE, RAG>(nbuf + 2 * A_PLANE, tid, n - LA::NPIECE, kv, ph,
+                                               pl, m1);
+          }
+          if (n >= 2 && n < 10) read_frag(buf, 1, n - 2, fa1, fb1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();
+        // phase B
+#pragma unroll
+        for (int n = 0; n < 12; ++n) {
+          mfma_n(n, fa1, fb1);
+          if (more && n == 1) lan.load(J.rsA, p.lda, J.vra, kk(t + 3, A_KC), tid);
+          if (more && n == 3) lbn.load(J.rsB, p.ldb, J.vrb, kk(t + 3, B_KC), tid);
+          if (more && n >= 2 && n < 10) read_frag(nbuf, 0, n - 2, fa0, fb0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+      int t = 0;
+      // every step of the loop has a successor; the last one or two after it
+      for (; t + 2 < T; t += 2) {
+        step(t, la[1], lb[1], std::true_type{});
+        step(t + 1, la[0], lb[0], std::true_type{});
+      }
+      if (t + 1 < T) {
+        step(t, la[1], lb[1], std::true_type{});
+        step(t + 1, la[0], lb[0], std::false_type{});
+      } else {
+        step(t, la[1], lb[1], std::false_type{});
+      }
+    }
+    tile_epilogue<A_KC, B_KC>(p, sexp_s[set], sw_s[set], acc, J.split, J.row0, J.col0, flags,
+                              tid);
+    lid += nbx;
+    if (lid >= xend) break;  // uniform
+    set ^= 1;
+    J = setup(lid);
+  }
 }
 
 // Max |x| and min nonzero |x| per row or per column of a pitched fp32 matrix,
@@ -1340,7 +1391,11 @@ void launch_t(const GemmF16Args &a, unsigned blocks, hipStream_t st) {
     }();
     (void)fattr;
     if (fast) {
-      hipLaunchKernelGGL((gemm_f16x3_fast_kernel<AM, BMODE, RAG>), dim3(blocks), dim3(NT),
+      // KCNN_F16X3_PERSIST (experiment build) = n > 0: a persistent grid of
+      // 256 n blocks, each taking several jobs of its XCD's chunk
+      static const int pers = KCNN_KNOB("KCNN_F16X3_PERSIST", 0);
+      const unsigned fb = pers > 0 ? std::min<unsigned>(blocks, 256u * (unsigned)pers) : blocks;
+      hipLaunchKernelGGL((gemm_f16x3_fast_kernel<AM, BMODE, RAG>), dim3(fb), dim3(NT),
                          LDS_BYTES, st, a);
       return;
     }

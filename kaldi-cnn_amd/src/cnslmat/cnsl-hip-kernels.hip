@@ -14,6 +14,7 @@
 #include <cstdlib>
 
 #include "hip-util.h"
+#include "momentum-step.h"
 
 using kcnn::FastDiv;
 
@@ -297,12 +298,11 @@ struct MomentumUpdate {
   float *W; MatrixDim wd; float *prev; MatrixDim pd; const float *grad;
   MatrixDim gd; float momentum, a_wd, a_g;
   __device__ void operator()(int64_t i, int j) const {
-    float p = prev[i * pd.stride + j] * momentum;   // Scale(momentum_)
-    const float w = W[i * wd.stride + j];
-    p = a_wd * w + p;                               // AddMat(-lr*wd, W)
-    p = a_g * grad[i * gd.stride + j] + p;          // AddMat(lr, grad)
+    // momentum-step.h: the same code as the gradient GEMM's fused store
+    float p = prev[i * pd.stride + j], w = W[i * wd.stride + j];
+    kcnn::momentum_step(grad[i * gd.stride + j], p, w, momentum, a_wd, a_g);
     prev[i * pd.stride + j] = p;
-    W[i * wd.stride + j] = 1.0f * p + w;            // AddMat(1.0, prev)
+    W[i * wd.stride + j] = w;
   }
 };
 

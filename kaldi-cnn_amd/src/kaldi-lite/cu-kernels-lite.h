@@ -63,6 +63,15 @@ int kl_gemm_f16x3_bias(int transA, int transB, int M, int N, int K, float alpha,
                        const float *A, int lda, const float *B, int ldb, float beta, float *C,
                        int ldc, const uint32_t *amax_given, const uint32_t *bmax_given,
                        const float *bias, void *ws, size_t ws_bytes, kcnn_stream_t stream);
+/* kl_gemm_f16x3_given(alpha 1, beta 0) of a weight gradient applied as the
+   momentum update in the GEMM's own store (cnslmat/momentum-step.h): W and
+   prev (M x N, 16-B aligned rows) get prev = momentum prev + a_wd W + a_g g,
+   W += prev; the bits of the gradient buffer + hipF_momentum_update */
+int kl_gemm_f16x3_momentum(int transA, int transB, int M, int N, int K, const float *A,
+                           int lda, const float *B, int ldb, const uint32_t *amax_given,
+                           const uint32_t *bmax_given, float *W, int ldw, float *prev, int ldp,
+                           float momentum, float a_wd, float a_g, void *ws, size_t ws_bytes,
+                           kcnn_stream_t stream);
 /* the same product from operands already split into bf16 planes h, m, l
    (plane p of X at X + p * ps elements); kl_split_planes makes them */
 int kl_split_planes(const float *src, int rows, int cols, int ld, uint16_t *dst, int ldp,

@@ -305,6 +305,44 @@ bool CuMatrixBase<Real>::GemmF16x3(Real alpha, const CuMatrixBase<Real> &A,
 }
 
 template <typename Real>
+bool CuMatrixBase<Real>::AddMatMatMomentum(const CuMatrixBase<Real> &A,
+                                           MatrixTransposeType transA,
+                                           const CuMatrixBase<Real> &B,
+                                           MatrixTransposeType transB, CuMatrixBase<Real> *prev,
+                                           Real momentum, Real a_wd, Real a_g) {
+  const MatrixIndexT m = num_rows_, n = num_cols_;
+  const MatrixIndexT k = transA == kNoTrans ? A.NumCols() : A.NumRows();
+  CuDevice &dev0 = CuDevice::Instantiate();
+  auto aligned = [](const CuMatrixBase<Real> &X) {
+    return X.Stride() % 4 == 0 && reinterpret_cast<uintptr_t>(X.Data()) % 16 == 0;
+  };
+  if (dev0.GemmMode() != 2 || m == 0 || n == 0 || k == 0 || !aligned(A) || !aligned(B) ||
+      !aligned(*this) || !aligned(*prev))
+    return false;
+  KALDI_ASSERT((transA == kNoTrans ? A.NumRows() : A.NumCols()) == m &&
+               (transB == kNoTrans ? B.NumCols() : B.NumRows()) == n &&
+               (transB == kNoTrans ? B.NumRows() : B.NumCols()) == k &&
+               prev->NumRows() == m && prev->NumCols() == n);
+  CuProfileScope prof("AddMatMat");
+  const CuGemmStatsHint *ha = CuGemmStatsHint::Find(A.Data(), A.NumRows(), A.NumCols(),
+                                                    A.Stride());
+  const CuGemmStatsHint *hb = CuGemmStatsHint::Find(B.Data(), B.NumRows(), B.NumCols(),
+                                                    B.Stride());
+  const uint32_t *ag = ha ? (transA == kNoTrans ? ha->rowmax : ha->colmax) : nullptr;
+  const uint32_t *bg = hb ? (transB == kNoTrans ? hb->colmax : hb->rowmax) : nullptr;
+  const size_t wsf = kl_gemm_f16x3_full_workspace_bytes(m, n, k);
+  void *wf = dev0.Malloc(wsf);
+  const int rc = kl_gemm_f16x3_momentum(transA == kTrans, transB == kTrans, m, n, k, A.Data(),
+                                        A.Stride(), B.Data(), B.Stride(), ag, bg, data_, stride_,
+                                        prev->Data(), prev->Stride(), momentum, a_wd, a_g, wf,
+                                        wsf, S());
+  dev0.Free(wf);
+  if (rc == (int)hipErrorNotSupported) return false;
+  CNSL_SAFE_CALL(rc);
+  return true;
+}
+
+template <typename Real>
 void CuMatrixBase<Real>::AddMatMatBias(Real alpha, const CuMatrixBase<Real> &A,
                                        MatrixTransposeType transA, const CuMatrixBase<Real> &B,
                                        MatrixTransposeType transB,

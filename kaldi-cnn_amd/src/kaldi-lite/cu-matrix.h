@@ -120,6 +120,14 @@ class CuMatrixBase {
   void AddMatMatBias(Real alpha, const CuMatrixBase<Real> &A, MatrixTransposeType transA,
                      const CuMatrixBase<Real> &B, MatrixTransposeType transB,
                      const CuVectorBase<Real> &bias);
+  /// this = W: the momentum update with the gradient op(A) op(B) applied in
+  /// the f16x3 GEMM's store (kl_gemm_f16x3_momentum; prev = momentum prev +
+  /// a_wd W + a_g g, W += prev), without a gradient buffer.  False when the
+  /// engine is not f16x3 or an operand is not 16-B aligned: nothing is
+  /// changed then and the caller takes the gradient buffer path.
+  bool AddMatMatMomentum(const CuMatrixBase<Real> &A, MatrixTransposeType transA,
+                         const CuMatrixBase<Real> &B, MatrixTransposeType transB,
+                         CuMatrixBase<Real> *prev, Real momentum, Real a_wd, Real a_g);
   /// every row = v
   void CopyRowsFromVec(const CuVectorBase<Real> &v);
   void CopyRowsFromVec(const VectorBase<Real> &v);  // host vector

@@ -1189,6 +1189,28 @@ void FullyConnectedComponent::UpdateSimple(const CuMatrixBase<BaseFloat> &in_val
     linear_params_.AddMat(1.0, prev_grad_, kNoTrans);
     return;
   }
+  // f16x3 engine: the weight gradient applied as the momentum update in the
+  // GEMM's own store (no gradient buffer: 2 x 47.6 MB of c2's traffic), the
+  // bias row as in ApplyGradient; the same bits as ComputeGradient +
+  // ApplyGradient (momentum-step.h), the path the data-parallel step keeps
+  {
+    const double learning_rate = learning_rate_ / (double)num_sample;  // :1136
+    const BaseFloat a_wd = (BaseFloat)(-1 * learning_rate * weight_decay_);
+    const BaseFloat a_g = (BaseFloat)learning_rate;
+    CuProfileScope prof("FullyConnectedComponent::ComputeGradient");
+    if (linear_params_.AddMatMatMomentum(out_deriv, kTrans, in_value, kNoTrans, &prev_grad_,
+                                         momentum_, a_wd, a_g)) {
+      Scratch gbs(sizeof(BaseFloat) * (size_t)OutputDim());
+      CuSubVector<BaseFloat> gb(gbs.f(), OutputDim());
+      gb.AddRowSumMat(1.0, out_deriv, 0.0);
+      // (hipF_momentum_update with no weight rows: its bias row alone)
+      CNSL_SAFE_CALL(hipF_momentum_update(
+          linear_params_.Data(), Dense(0, OutputDim()), prev_grad_.Data(),
+          Dense(0, OutputDim()), gbs.f(), Dense(0, OutputDim()), momentum_, a_wd, a_g,
+          bias_params_.Data(), gbs.f(), OutputDim(), S()));
+      return;
+    }
+  }
   Scratch grad(sizeof(BaseFloat) * (size_t)NumGradientParams());
   ComputeGradient(in_value, out_deriv, grad.f());
   ApplyGradient(grad.f(), num_sample);

@@ -306,12 +306,16 @@ def test_fc_bias_in_gemm_store(kc, I, Od, N):
     np.testing.assert_array_equal(y, host(c))
 
 
-@pytest.mark.parametrize("I,Od,N", [(512, 256, 2048), (300, 70, 33), (1000, 130, 4100)])
+@pytest.mark.parametrize("I,Od,N", [(512, 256, 2048), (300, 70, 33), (1000, 130, 4100),
+                                    (11616, 1024, 4096)])
 def test_fc_update_equals_gradient_then_apply(kc, I, Od, N):
     """The update inside Backprop (UpdateSimple, nnet-component-nnet0.cc:1133-1150)
     must give the bits of ComputeGradient + ApplyGradient, the split the DP
-    step uses.  The first and last shapes split the gradient GEMM's K
-    (N >= 2048 frames), the second does not."""
+    step uses.  Under f16x3 UpdateSimple applies the momentum update in the
+    gradient GEMM's own store (kl_gemm_f16x3_momentum); the other path writes
+    the gradient and runs hipF_momentum_update.  The first, third and c2
+    shapes split the gradient GEMM's K (N >= 2048 frames), the second does
+    not (its tile epilogue applies the update)."""
     line = (f"FullyConnectedComponent input-dim={I} output-dim={Od} learning-rate=0.02 "
             f"param-stddev=0.01 bias-stddev=1 weight-decay=0.0002 momentum=0.9")
     r = rng(9)

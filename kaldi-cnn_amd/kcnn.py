@@ -58,7 +58,8 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         L.kcnn_last_error.restype = ctypes.c_char_p
         L.kcnn_version.restype = ctypes.c_char_p
-        L.kcnn_device_malloc_calls.restype = ctypes.c_ulonglong
+        if hasattr(L, "kcnn_device_malloc_calls"):  # (absent from pre-r05 builds)
+            L.kcnn_device_malloc_calls.restype = ctypes.c_ulonglong
         for name in ("kcnn_component_new_from_string", "kcnn_component_read",
                      "kcnn_component_copy"):
             getattr(L, name).restype = ctypes.c_void_p

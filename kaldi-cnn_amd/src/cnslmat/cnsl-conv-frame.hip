@@ -353,16 +353,31 @@ __device__ __forceinline__ void frame_row_max(uint32_t *rslot, uint32_t v, uint3
 // the same scale; 0x7f... for Inf; an all-zero column gets the subnormal
 // bound, harmless).  colmax zeroed by the forward; blockIdx.y takes 32
 // workgroups' rows, atomic max across those chunks.
+// A thread takes four columns (one dword of bytes per row; npool % 4 == 0,
+// else one column), its 32 rows' loads in flight together.
 constexpr int COLMAX_ROWS = 32;
 __global__ __launch_bounds__(256) void pool_colmax_kernel(const uint8_t *__restrict__ pcol,
                                                            int nblk, int npool,
                                                            uint32_t *__restrict__ colmax) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
+  const bool quad = npool % 4 == 0;
+  const int c = (blockIdx.x * 256 + threadIdx.x) * (quad ? 4 : 1);
   if (c >= npool) return;
   const int b0 = blockIdx.y * COLMAX_ROWS, b1 = min(nblk, b0 + COLMAX_ROWS);
-  uint32_t m = 0;
-  for (int b = b0; b < b1; b++) m = max(m, (uint32_t)pcol[(int64_t)b * npool + c]);
-  atomicMax(colmax + c, (m << 23) | 0x7fffffu);
+  uint32_t w[COLMAX_ROWS];
+#pragma unroll
+  for (int i = 0; i < COLMAX_ROWS; i++) {
+    const int b = b0 + i;
+    const uint8_t *q = pcol + (int64_t)b * npool + c;
+    w[i] = b >= b1 ? 0u : quad ? *reinterpret_cast<const uint32_t *>(q) : (uint32_t)*q;
+  }
+  uint32_t m[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int i = 0; i < COLMAX_ROWS; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) m[j] = max(m[j], (w[i] >> (8 * j)) & 0xffu);
+#pragma unroll
+  for (int j = 0; j < 4; j++)
+    if (j == 0 || quad) atomicMax(colmax + c + j, (m[j] << 23) | 0x7fffffu);
 }
 
 // The pooled output's small elements (f16-split.h) after pool_colmax_kernel,
@@ -2328,8 +2343,9 @@ int kcnn_conv_fwd_frame_pool(const ConvGeom &g, const float *X, int xs,
 #undef KCNN_FWD_POOL_T
   if (pcol) {
     const int npool = g.G / pc * g.P;
+    const int ncq = npool % 4 == 0 ? npool / 4 : npool;  // pool_colmax_kernel's threads
     hipLaunchKernelGGL(pool_colmax_kernel,
-                       dim3((npool + 255) / 256, (grid + COLMAX_ROWS - 1) / COLMAX_ROWS),
+                       dim3((ncq + 255) / 256, (grid + COLMAX_ROWS - 1) / COLMAX_ROWS),
                        dim3(256), 0, st, reinterpret_cast<const uint8_t *>(pcol), (int)grid,
                        npool, stats->colmax);
     const int vec = ps % 4 == 0 && (uintptr_t)pool % 16 == 0;

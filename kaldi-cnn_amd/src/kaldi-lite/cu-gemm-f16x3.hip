@@ -328,6 +328,16 @@ struct Loader {
 // column; bit 1: one of them is spread (both for the whole block).
 __device__ __forceinline__ int tile_scales(const GemmF16Args &p, int *sexp, float *sw, int row0,
                                            int col0, int tid) {
+#ifdef KCNN_EXPERIMENTS  // KCNN_GEMM_DEBUG & 4: no statistics loads (scale 0; timing only)
+  if (p.dbg & 64) {
+    for (int i = tid; i < BM + BN; i += NT) {
+      sexp[i] = 0;
+      sw[i] = 0.0f;
+    }
+    __syncthreads();
+    return 0;
+  }
+#endif
   int skip = 0, spr = 0;
   for (int i = tid; i < BM + BN; i += NT) {
     int s = 0;
@@ -449,7 +459,8 @@ __device__ __forceinline__ void fix_rejected(const GemmF16Args &p, bool a_kc, bo
 template <bool A_KC, bool B_KC>
 __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *sexp,
                                               const float *sw, const f32x16 (&acc)[2][2],
-                                              int split, int row0, int col0, int flags, int tid) {
+                                              int split, int row0, int col0, int flags, int tid,
+                                              char *lds) {
   const int lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
   const int half2 = lane >> 5;
   const bool partial = p.ksplit > 1;
@@ -463,6 +474,80 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
   float *slab = partial ? p.part + (int64_t)split * p.M * np4 : p.C;
   const int ldo = partial ? np4 : p.ldc;
   uint64_t rej = 0;  // bit (2 i + j) * 16 + g: that element is rejected
+  auto fix = [&]() {
+    fix_rejected(p, A_KC, B_KC, rej, lane, [&](int l, int n, int &row, int &col) {
+      const int i = n >> 5, j = (n >> 4) & 1, g = n & 15;
+      row = row0 + wm * 64 + i * 32 + (g & 3) + 8 * (g >> 2) + 4 * (l >> 5);
+      col = col0 + wn * 64 + j * 32 + (l & 31);
+    });
+  };
+  // A whole tile without Inf / NaN rows or columns (block-uniform): each
+  // wave's 64 x 64 block through LDS in two 32-row halves (the main loop's
+  // plane buffers, free after a barrier), then 16-B stores of whole rows:
+  // a quarter of the store instructions of the per-register stores below
+  // (c2's data gradient: 400 -> 388 us at K 1024).  An element the check
+  // rejects is staged and stored like the rest, then recomputed and stored
+  // again by its own wave (fix_rejected: the same wave, so in order).
+  const bool staged = row0 + BM <= p.M && col0 + BN <= p.N && !skip && !p.mom.W &&
+                      (partial || ((ldo & 3) | ((uintptr_t)slab & 15)) == 0)
+#ifdef KCNN_EXPERIMENTS  // KCNN_GEMM_DEBUG & 8: the per-register stores only
+                      && !(p.dbg & 128)
+#endif
+      ;
+  if (staged) {
+    __syncthreads();  // every wave past its last read of the plane buffers
+    constexpr int SR = 68;  // staging row pitch (floats): 16-B rows, rows 4 apart on other banks
+    float *st = reinterpret_cast<float *>(lds) + wave * 32 * SR;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int cl = wn * 64 + j * 32 + (lane & 31);
+        const int ec = sexp[BM + cl];
+        const float wc = check ? sw[BM + cl] : 0.0f;
+        const bool bcheck =
+            check && (__ballot(wc != 0.0f || sw[wm * 64 + i * 32 + (lane & 31)] != 0.0f) != 0);
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const int rr = (g & 3) + 8 * (g >> 2) + 4 * half2;
+          const int rl = wm * 64 + i * 32 + rr;
+          if (bcheck) {
+            const float thr = wc + sw[rl];
+            if (thr != 0.0f && !(fabsf(acc[i][j][g]) >= thr))
+              rej |= (uint64_t)1 << ((2 * i + j) * 16 + g);
+          }
+          st[rr * SR + j * 32 + (lane & 31)] =
+              __builtin_amdgcn_ldexpf(acc[i][j][g], -(sexp[rl] + ec));
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int f = lane + 64 * k, rr = f >> 4, c4 = f & 15;
+        const float4 v = *reinterpret_cast<const float4 *>(st + rr * SR + 4 * c4);
+        const int row = row0 + wm * 64 + i * 32 + rr, col = col0 + wn * 64 + 4 * c4;
+        float4 *o = reinterpret_cast<float4 *>(slab + (int64_t)row * ldo + col);
+        if (partial) {
+          *o = v;
+          continue;
+        }
+        float4 w = make_float4(p.alpha * v.x, p.alpha * v.y, p.alpha * v.z, p.alpha * v.w);
+        if (p.beta != 0.0f) {
+          const float4 c = *o;
+          w = make_float4(p.alpha * v.x + p.beta * c.x, p.alpha * v.y + p.beta * c.y,
+                          p.alpha * v.z + p.beta * c.z, p.alpha * v.w + p.beta * c.w);
+        }
+        if (p.bias) {
+          w.x += p.bias[col];
+          w.y += p.bias[col + 1];
+          w.z += p.bias[col + 2];
+          w.w += p.bias[col + 3];
+        }
+        *o = w;
+      }
+    }
+    if (check) fix();
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -490,16 +575,19 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
           }
         }
         const float v = __builtin_amdgcn_ldexpf(acc[i][j][g], -(er + ec));
+#ifdef KCNN_EXPERIMENTS  // KCNN_GEMM_DEBUG & 1: no stores, & 2: nontemporal stores
+        if (p.dbg & 16) continue;
+        if (p.dbg & 32) {
+          float *o = partial ? slab + (int64_t)row * ldo + col : p.C + (int64_t)row * p.ldc + col;
+          __builtin_nontemporal_store(partial ? v : store_value(p, v, o, col), o);
+          continue;
+        }
+#endif
         if (partial) slab[(int64_t)row * ldo + col] = v;
         else emit(p, row, col, v);
       }
     }
-  if (check)
-    fix_rejected(p, A_KC, B_KC, rej, lane, [&](int l, int n, int &row, int &col) {
-      const int i = n >> 5, j = (n >> 4) & 1, g = n & 15;
-      row = row0 + wm * 64 + i * 32 + (g & 3) + 8 * (g >> 2) + 4 * (l >> 5);
-      col = col0 + wn * 64 + j * 32 + (l & 31);
-    });
+  if (check) fix();
   if (skip && split == 0) {
     for (int e = tid; e < BM * BN; e += NT) {
       const int rl = e / BN, cl = e - rl * BN;
@@ -643,7 +731,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
     }
   }
 
-  tile_epilogue<A_KC, B_KC>(p, sexp, sw, acc, split, row0, col0, flags, tid);
+  tile_epilogue<A_KC, B_KC>(p, sexp, sw, acc, split, row0, col0, flags, tid, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -686,7 +774,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
   const int T = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   const int klast = kend - kbeg - (T - 1) * BK;
 
-  const int flags = tile_scales(p, sexp, sw, row0, col0, tid);
   const float *baseA = A_KC ? p.A + (int64_t)row0 * p.lda : p.A + (int64_t)kbeg * p.lda + row0;
   const float *baseB = B_KC ? p.B + (int64_t)col0 * p.ldb : p.B + (int64_t)kbeg * p.ldb + col0;
   const int vra = p.M - row0, vrb = p.N - col0;
@@ -711,10 +798,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int g = 0; g < 16; ++g) acc[i][j][g] = 0.0f;
-  la[0].init_exp(sexp, tid);
-  la[1].init_exp(sexp, tid);
-  lb[0].init_exp(sexp + BM, tid);
-  lb[1].init_exp(sexp + BM, tid);
 
   const int ar = wm * 64, br = wn * 64;
   f16x8 fa0[2][2], fb0[2][2], fa1[2][2], fb1[2][2];
@@ -735,14 +818,25 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
     acc[i][j] = mfma(fa[i][PA[pr]], fb[j][PB[pr]], acc[i][j]);
   };
 
+  // the first two K tiles' loads go out before the tile's scales are read
+  // (the split needs both; the scales' loads and barriers then pass under
+  // the tiles' latency: c2's data gradient 400 -> 381 us at K 1024 without
+  // the scales at all)
   if (T > 0) {
     la[0].load(rsA, p.lda, vra, kk(0, A_KC), tid);
     lb[0].load(rsB, p.ldb, vrb, kk(0, B_KC), tid);
-    la[0].template store<A_PLANE, RAG>(lds, tid, T == 1 ? klast : BK, m1);
-    lb[0].template store<B_PLANE, RAG>(lds + 2 * A_PLANE, tid, T == 1 ? klast : BK, m1);
-    __builtin_amdgcn_sched_barrier(0);
     la[1].load(rsA, p.lda, vra, kk(1, A_KC), tid);
     lb[1].load(rsB, p.ldb, vrb, kk(1, B_KC), tid);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  const int flags = tile_scales(p, sexp, sw, row0, col0, tid);
+  la[0].init_exp(sexp, tid);
+  la[1].init_exp(sexp, tid);
+  lb[0].init_exp(sexp + BM, tid);
+  lb[1].init_exp(sexp + BM, tid);
+  if (T > 0) {
+    la[0].template store<A_PLANE, RAG>(lds, tid, T == 1 ? klast : BK, m1);
+    lb[0].template store<B_PLANE, RAG>(lds + 2 * A_PLANE, tid, T == 1 ? klast : BK, m1);
     __builtin_amdgcn_sched_barrier(0);
     la[0].load(rsA, p.lda, vra, kk(2, A_KC), tid);
     lb[0].load(rsB, p.ldb, vrb, kk(2, B_KC), tid);
@@ -799,7 +893,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
     }
   }
 
-  tile_epilogue<A_KC, B_KC>(p, sexp, sw, acc, split, row0, col0, flags, tid);
+  tile_epilogue<A_KC, B_KC>(p, sexp, sw, acc, split, row0, col0, flags, tid, lds);
 }
 
 // Max |x| and min nonzero |x| per row or per column of a pitched fp32 matrix,
@@ -1423,7 +1517,8 @@ static int gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alph
   a.bcnt = bmax + 2 * (size_t)N;
   a.bvec = N % 4 == 0 && (uintptr_t)a.bmax % 16 == 0 && (uintptr_t)a.bcnt % 16 == 0;
   static const int red_dbg = KCNN_KNOB("KCNN_RED_DEBUG", 0);
-  a.dbg = red_dbg;
+  static const int gemm_dbg = KCNN_KNOB("KCNN_GEMM_DEBUG", 0);
+  a.dbg = red_dbg | gemm_dbg << 4;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.alpha = alpha; a.beta = beta;
   a.tiles_m = (M + BM - 1) / BM;

@@ -749,18 +749,18 @@ def main():
                 # ceiling is the bf16 dense peak over the products per fp32
                 # product (6 for the bf16x6 implicit GEMM / weight gradient /
                 # pooled backward that carry most of these layers' flop)
-                eng_peak = PEAK_BF16_MFMA_TFLOPS / 6
+                eng_peak = ENGINE_PEAK_TFLOPS["bf16x6"]
                 result["roofline"] = {
                     "kernel": "conv layers (every ConvolutionComponent scope)", "bound": "mfma",
                     "achieved": round(conv_flop / conv_ms / 1e9, 2),
-                    "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(conv_flop / conv_ms / 1e9 / PEAK_FP32_MFMA_TFLOPS, 4),
+                    "peak": round(eng_peak, 1), "unit": "TFLOP/s",
+                    "frac": round(conv_flop / conv_ms / 1e9 / eng_peak, 4),
                     "traffic": None, "algorithmic_flop_per_step": conv_flop,
-                    "engine_peak": round(eng_peak, 1),
-                    "frac_of_engine_peak": round(conv_flop / conv_ms / 1e9 / eng_peak, 4),
-                    "note": "peak = fp32 dense MFMA (the dtype's); the layers compute fp32 "
-                            "products on the bf16/f16 matrix cores (split operands), so frac "
-                            "can pass 1; engine_peak = bf16 dense peak / 6 products"}
+                    "engine": "bf16x6",
+                    "note": "peak = the engine's fp32-equivalent ceiling: the layers compute "
+                            "fp32 products on the bf16 matrix cores from 3-way split operands, "
+                            "six products each (bf16 dense peak / 6); the fp32 MFMA peak "
+                            f"({PEAK_FP32_MFMA_TFLOPS} TFLOP/s) is not the bound of these kernels"}
             if dp:
                 result["dp"] = dp
             if not args.no_cpu_baseline and world == 1:

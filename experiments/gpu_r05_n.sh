@@ -14,6 +14,11 @@ for i in 1 2; do for lib in r04 new; do
   python -c "
 import json;d=json.load(open('$O/ab_${lib}_$i.json'));print('$lib', d['value'], d['ms_per_step'])"
 done; done
+if [ -n "$NNET" ]; then
+  timeout -k 10 300 python bench.py --config nnet --no-cpu-baseline --json-out $O/nnet.json > $O/nnet.log 2>&1 || exit 5
+  python -c "
+import json;d=json.load(open('$O/nnet.json'));print('nnet', d['value'], d['ms_per_step'])"
+fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof.log 2>&1 || exit 6
 python scripts/kstats.py "$(find $O/prof -name "*kernel_stats.csv" | head -1)" 45 20
 if [ -n "$KSWEEP" ]; then

@@ -107,13 +107,14 @@ def main():
               "| kernel | FETCH_SIZE (KB) | WRITE_SIZE (KB) | HBM bytes / launch |",
               "|---|---:|---:|---:|"]
     for k in sorted(set(fetch) | set(write)):
+        # every kernel in the table (the FC GEMMs' bytes included); the
+        # hot-path roles also go to pmc_traffic.json for bench.py's roofline
         key = kernel_key(k)
-        if key is None:
-            continue
         f_kb, w_kb = fetch.get(k, 0.0), write.get(k, 0.0)
         byts = 2 * f_kb * 1024 + w_kb * 1024
-        traffic.setdefault(key, {"kernel": short(k), "hbm_bytes_per_launch": 0.0})
-        traffic[key]["hbm_bytes_per_launch"] += byts
+        if key is not None:
+            traffic.setdefault(key, {"kernel": short(k), "hbm_bytes_per_launch": 0.0})
+            traffic[key]["hbm_bytes_per_launch"] += byts
         lines.append(f"| `{short(k)}` | {f_kb:.0f} | {w_kb:.0f} | {byts:.3e} |")
     with open(os.path.join(a.out, f"{a.tag}_kernel_stats.md"), "w") as fh:
         fh.write("\n".join(lines) + "\n")

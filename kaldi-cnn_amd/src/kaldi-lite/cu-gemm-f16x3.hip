@@ -84,6 +84,8 @@ struct GemmF16Args {
   const float *A, *B;
   float *C;                      // the output
   float *part;                   // ksplit > 1: the partial slabs [ksplit][M][N]
+  uint32_t *rflag;               // ksplit > 1: per 64 quads of C, 1 when the reduce left
+                                 // its rejections to gemm_f16x3_fixup_kernel
   const uint32_t *amax, *bmax;   // max |x| bits per row of op(A), per column of op(B)
   const uint32_t *amin, *bmin;   // min nonzero |x| bits (0: none), the same groups
   const uint32_t *acnt, *bcnt;   // spread groups: their elements below 2^-3 after the scale
@@ -1250,11 +1252,12 @@ int stats_launch(const StatOp &a, const StatOp &b, hipStream_t st) {
 // past N are not stored); elements of an Inf / NaN row or column are the
 // epilogue's (split 0).  The spread check of tile_epilogue on the summed
 // value (unscaled: the threshold times 2^-(s_row + s_col)); a rejected
-// element is not stored but listed in LDS, and after the block's elements
-// the block's waves recompute the listed ones (wave_dot).  A block with more
-// rejections than the list holds stores none of the list and instead re-runs
-// its elements, recomputing every rejected one in a wave-uniform loop.
-constexpr int REJ_CAP = 256;
+// element is not stored.  A wave with at most REJ_LOCAL of them recomputes
+// them itself (wave_dot); one with more flags its 64 quads (rflag) for
+// gemm_f16x3_fixup_kernel, which spreads such groups over the whole GPU: a
+// spread row rejects hundreds of elements of one row, and one wave's
+// wave_dots in series took milliseconds (nnet.config's weight gradients).
+constexpr int REJ_LOCAL = 4;
 __device__ __forceinline__ uint32_t reduce_quad(const GemmF16Args &p, int64_t e, int nq, int np4,
                                                 int64_t plane, int &r, int &c, bool store) {
   const int N = p.N;
@@ -1354,50 +1357,133 @@ __device__ __forceinline__ uint32_t reduce_quad(const GemmF16Args &p, int64_t e,
 
 __global__ __launch_bounds__(256) void gemm_f16x3_reduce_kernel(GemmF16Args p, int a_kc,
                                                                 int b_kc) {
-  __shared__ int rej_r[REJ_CAP], rej_c[REJ_CAP];
-  __shared__ int rej_n;
   const int np4 = (p.N + 3) & ~3, nq = np4 >> 2;
   const int64_t total = (int64_t)p.M * nq;
   const int64_t plane = (int64_t)p.M * np4;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (threadIdx.x == 0) rej_n = 0;
-  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  // e0 = the wave's first quad, a multiple of 64 below total: lane 0 is
+  // active in every pass, and every group of 64 quads gets its flag written
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     int r, c;
-    uint32_t rej = reduce_quad(p, e, nq, np4, plane, r, c, true);
-    while (rej) {  // rare
-      const int i = __builtin_ctz(rej);
-      rej &= rej - 1;
-      const int slot = atomicAdd(&rej_n, 1);
-      if (slot < REJ_CAP) {
-        rej_r[slot] = r;
-        rej_c[slot] = c + i;
-      }
-    }
-  }
-  __syncthreads();
-  const int n = rej_n;  // block-uniform
-  if (n == 0) return;
-  if (n <= REJ_CAP) {
-    for (int j = wave; j < n; j += 4) {
-      const int row = rej_r[j], col = rej_c[j];
-      const float v = wave_dot(p, a_kc != 0, b_kc != 0, row, col, lane);
-      if (lane == 0) emit(p, row, col, v);
-    }
-    return;
-  }
-  // the list overflowed (none of it stored): find every rejected element
-  // again (the kept ones are stored already) and recompute it by its wave
-  for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < total;
-       base += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = base + threadIdx.x;
-    int r = 0, c = 0;
-    const uint32_t rej = e < total ? reduce_quad(p, e, nq, np4, plane, r, c, false) : 0u;
+    const uint32_t rej = reduce_quad(p, e, nq, np4, plane, r, c, true);
+    // the wave's rejections (ballots: only the active lanes)
+    const int n = __builtin_popcountll(__ballot(rej & 1)) + __builtin_popcountll(__ballot(rej & 2)) +
+                  __builtin_popcountll(__ballot(rej & 4)) + __builtin_popcountll(__ballot(rej & 8));
+    const bool defer = n > REJ_LOCAL;
+    if (lane == 0) p.rflag[e >> 6] = defer ? 1u : 0u;
+    if (n == 0 || defer) continue;
     fix_rejected(p, a_kc != 0, b_kc != 0, rej, lane, [&](int l, int bit, int &row, int &col) {
       row = __builtin_amdgcn_readlane(r, l);
       col = __builtin_amdgcn_readlane(c, l) + bit;
     });
+  }
+}
+
+// The flagged groups of 64 quads (gemm_f16x3_reduce_kernel), one per block
+// at a time: slot s = t G + b for thread t of block b (G blocks), so the
+// consecutive groups of one spread row go to different blocks.  A group's
+// rejections are found again (reduce_quad, not stored) and recomputed in fp32:
+//  - op(B) row-contiguous with 16-B rows (`rows`): every lane its quad's four sums, the
+//    block's four waves each over a quarter of K (16-B loads of op(B)'s rows,
+//    coalesced over the lanes; the lanes of one C row share op(A)'s element),
+//    the quarters added in wave order, the rejected elements stored;
+//  - otherwise: wave_dot per rejected element, the quads dealt to
+//    the waves by lane & 3.
+// Deterministic: the group's results do not depend on the block or order.
+constexpr int FIX_DEPTH = 16;
+__global__ __launch_bounds__(256) void gemm_f16x3_fixup_kernel(GemmF16Args p, int a_kc,
+                                                               int b_kc, int rows) {
+  __shared__ int list[256];
+  __shared__ int nlist;
+  __shared__ float4 quarter[4][64];
+  const int np4 = (p.N + 3) & ~3, nq = np4 >> 2;
+  const int64_t total = (int64_t)p.M * nq;
+  const int64_t plane = (int64_t)p.M * np4;
+  const int64_t nslots = (total + 63) >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int64_t base = 0; base < nslots; base += (int64_t)gridDim.x * blockDim.x) {
+    if (threadIdx.x == 0) nlist = 0;
+    __syncthreads();
+    const int64_t slot = base + (int64_t)threadIdx.x * gridDim.x + blockIdx.x;
+    if (slot < nslots && p.rflag[slot] != 0) list[atomicAdd(&nlist, 1)] = (int)threadIdx.x;
+    __syncthreads();
+    const int n = nlist;
+    for (int j = 0; j < n; ++j) {
+      const int64_t e0 = (base + (int64_t)list[j] * gridDim.x + blockIdx.x) << 6;
+      const int64_t e = e0 + lane;
+      const bool valid = e < total;
+      int r = 0, c = 0;
+      const uint32_t rej = valid ? reduce_quad(p, e, nq, np4, plane, r, c, false) : 0u;
+      if (!rows) {
+        const uint64_t mine = (lane & 3) == wave ? rej : 0u;
+        fix_rejected(p, a_kc != 0, b_kc != 0, mine, lane, [&](int l, int bit, int &row, int &col) {
+          row = __builtin_amdgcn_readlane(r, l);
+          col = __builtin_amdgcn_readlane(c, l) + bit;
+        });
+        __syncthreads();
+        continue;
+      }
+      // this wave's quarter of K for the lane's quad (r, c .. c + 3)
+      const int kq = (p.K + 3) >> 2;
+      const int k0 = wave * kq, k1 = min(p.K, k0 + kq);
+      const int64_t sa = a_kc ? 1 : p.lda;
+      const float *qa = a_kc ? p.A + (int64_t)r * p.lda + k0 : p.A + (int64_t)k0 * p.lda + r;
+      const float *qb = p.B + (int64_t)k0 * p.ldb + c;
+      float4 acc[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      int k = k0;
+#pragma unroll 1
+      for (; k + FIX_DEPTH <= k1; k += FIX_DEPTH) {
+        float x[FIX_DEPTH];
+        float4 y[FIX_DEPTH];
+#pragma unroll
+        for (int i = 0; i < FIX_DEPTH; ++i) {
+          x[i] = qa[i * sa];
+          y[i] = *reinterpret_cast<const float4 *>(qb + (int64_t)i * p.ldb);
+        }
+#pragma unroll
+        for (int i = 0; i < FIX_DEPTH; ++i) {
+          float4 &t = acc[i & 3];
+          t.x = fmaf(x[i], y[i].x, t.x);
+          t.y = fmaf(x[i], y[i].y, t.y);
+          t.z = fmaf(x[i], y[i].z, t.z);
+          t.w = fmaf(x[i], y[i].w, t.w);
+        }
+        qa += FIX_DEPTH * sa;
+        qb += (int64_t)FIX_DEPTH * p.ldb;
+      }
+#pragma unroll 1
+      for (; k < k1; ++k) {
+        const float x = *qa;
+        const float4 y = *reinterpret_cast<const float4 *>(qb);
+        acc[0].x = fmaf(x, y.x, acc[0].x);
+        acc[0].y = fmaf(x, y.y, acc[0].y);
+        acc[0].z = fmaf(x, y.z, acc[0].z);
+        acc[0].w = fmaf(x, y.w, acc[0].w);
+        qa += sa;
+        qb += p.ldb;
+      }
+      float4 q;
+      q.x = (acc[0].x + acc[1].x) + (acc[2].x + acc[3].x);
+      q.y = (acc[0].y + acc[1].y) + (acc[2].y + acc[3].y);
+      q.z = (acc[0].z + acc[1].z) + (acc[2].z + acc[3].z);
+      q.w = (acc[0].w + acc[1].w) + (acc[2].w + acc[3].w);
+      quarter[wave][lane] = q;
+      __syncthreads();
+      if (wave == 0 && rej) {
+        const float4 q0 = quarter[0][lane], q1 = quarter[1][lane], q2 = quarter[2][lane],
+                     q3 = quarter[3][lane];
+        const float v[4] = {((q0.x + q1.x) + q2.x) + q3.x, ((q0.y + q1.y) + q2.y) + q3.y,
+                            ((q0.z + q1.z) + q2.z) + q3.z, ((q0.w + q1.w) + q2.w) + q3.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (rej >> i & 1) emit(p, r, c + i, v[i]);
+      }
+      __syncthreads();
+    }
+    __syncthreads();
   }
 }
 
@@ -1461,10 +1547,18 @@ void launch(int am, int bm, const GemmF16Args &a, unsigned blocks, hipStream_t s
 }
 
 size_t align16(size_t b) { return (b + 15) & ~(size_t)15; }
+// the split-K workspace: the slabs, then the reduce's flags (one word per
+// 64 quads of C)
+size_t slab_bytes(int s, int M, int N) {
+  return align16(sizeof(float) * (size_t)s * M * ((N + 3) & ~3));
+}
+size_t flag_bytes(int M, int N) {
+  return align16(sizeof(uint32_t) * (((size_t)M * ((N + 3) / 4) + 63) / 64));
+}
 size_t partial_bytes(int M, int N, int K) {
   const int64_t tiles = (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const int s = choose_ksplit(tiles, K);
-  return s > 1 ? align16(sizeof(float) * (size_t)s * M * ((N + 3) & ~3)) : 0;
+  return s > 1 ? slab_bytes(s, M, N) + flag_bytes(M, N) : 0;
 }
 
 }  // namespace
@@ -1525,9 +1619,12 @@ static int gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alph
   a.tiles_n = (N + BN - 1) / BN;
   const int64_t tiles = (int64_t)a.tiles_m * a.tiles_n;
   int s = choose_ksplit(tiles, K);
-  const size_t need = s > 1 ? sizeof(float) * (size_t)s * M * ((N + 3) & ~3) : 0;
+  const size_t need = s > 1 ? slab_bytes(s, M, N) + flag_bytes(M, N) : 0;
   if (need > ws_bytes || !ws) s = 1;
-  if (s > 1) a.part = static_cast<float *>(ws);
+  if (s > 1) {
+    a.part = static_cast<float *>(ws);
+    a.rflag = reinterpret_cast<uint32_t *>(static_cast<char *>(ws) + slab_bytes(s, M, N));
+  }
   a.ksplit = s;
   a.kps = ((K + s - 1) / s + BK - 1) / BK * BK;
   const int64_t nb = tiles * s;
@@ -1553,6 +1650,14 @@ static int gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alph
   if (rc || s == 1) return rc;
   hipLaunchKernelGGL(gemm_f16x3_reduce_kernel, dim3(kcnn::grid_for((int64_t)M * ((N + 3) / 4))),
                      dim3(256), 0, st, a, a_kc ? 1 : 0, b_kc ? 1 : 0);
+  rc = kcnn::launch_status();
+  if (rc) return rc;
+  // op(B) row-contiguous: the fixup's 16-B loads along its rows
+  const int rows = !b_kc && ldb % 4 == 0 && (uintptr_t)B % 16 == 0 && N % 4 == 0;
+  const int64_t slots = ((int64_t)M * ((N + 3) / 4) + 63) / 64;
+  hipLaunchKernelGGL(gemm_f16x3_fixup_kernel,
+                     dim3((unsigned)std::min<int64_t>(1024, (slots + 15) / 16)), dim3(256), 0, st,
+                     a, a_kc ? 1 : 0, b_kc ? 1 : 0, rows);
   return kcnn::launch_status();
 }
 extern "C" int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alpha,

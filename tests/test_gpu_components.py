@@ -306,21 +306,33 @@ def test_fc_bias_in_gemm_store(kc, I, Od, N):
     np.testing.assert_array_equal(y, host(c))
 
 
-@pytest.mark.parametrize("I,Od,N", [(512, 256, 2048), (300, 70, 33), (1000, 130, 4100),
-                                    (11616, 1024, 4096)])
-def test_fc_update_equals_gradient_then_apply(kc, I, Od, N):
+@pytest.mark.parametrize("I,Od,N,spread", [(512, 256, 2048, False), (300, 70, 33, False),
+                                           (1000, 130, 4100, False), (11616, 1024, 4096, False),
+                                           (512, 256, 2048, True), (11616, 1024, 4096, True)])
+def test_fc_update_equals_gradient_then_apply(kc, I, Od, N, spread):
     """The update inside Backprop (UpdateSimple, nnet-component-nnet0.cc:1133-1150)
     must give the bits of ComputeGradient + ApplyGradient, the split the DP
     step uses.  Under f16x3 UpdateSimple applies the momentum update in the
     gradient GEMM's own store (kl_gemm_f16x3_momentum); the other path writes
     the gradient and runs hipF_momentum_update.  The first, third and c2
     shapes split the gradient GEMM's K (N >= 2048 frames), the second does
-    not (its tile epilogue applies the update)."""
+    not (its tile epilogue applies the update).  `spread`: two output units'
+    derivatives are N(0,1) * 2^-28 but for one frame whose input is 0, so
+    every element of those two gradient rows fails the store's check and is
+    recomputed (split K: by gemm_f16x3_fixup_kernel), with the update applied
+    there."""
     line = (f"FullyConnectedComponent input-dim={I} output-dim={Od} learning-rate=0.02 "
             f"param-stddev=0.01 bias-stddev=1 weight-decay=0.0002 momentum=0.9")
     r = rng(9)
     params = [randn(r, (Od, I), 0.05), randn(r, (Od,), 0.5), randn(r, (Od, I), 0.01)]
-    x, dy = dev(randn(r, (N, I))), dev(randn(r, (N, Od), 0.1))
+    xh, dyh = randn(r, (N, I)), randn(r, (N, Od), 0.1)
+    if spread:
+        k0 = N // 3
+        for j0 in (3, Od - 2):
+            dyh[:, j0] = randn(r, (N,), 2.0 ** -28)
+            dyh[k0, j0] = 1.0
+        xh[k0, :] = 0.0
+    x, dy = dev(xh), dev(dyh)
     out = []
     for fused in (True, False):
         comp = kc.Component.NewFromString(line)

@@ -326,8 +326,10 @@ struct Loader {
 
 // The scale exponents of the tile's rows and columns into sexp, and each
 // one's spread weight into sw (f16-split.h spread_weight: 0 unless the group
-// is spread).  Returns bit 0: one of them is an Inf / NaN row or
-// column; bit 1: one of them is spread (both for the whole block).
+// is spread; -inf for an all-zero group, whose products are exactly 0: the
+// threshold sum is then -inf, i.e. no check).  Returns bit 0: one of them is
+// an Inf / NaN row or column; bit 1: one of them is spread (both for the
+// whole block).
 __device__ __forceinline__ int tile_scales(const GemmF16Args &p, int *sexp, float *sw, int row0,
                                            int col0, int tid) {
 #ifdef KCNN_EXPERIMENTS  // KCNN_GEMM_DEBUG & 4: no statistics loads (scale 0; timing only)
@@ -346,17 +348,19 @@ __device__ __forceinline__ int tile_scales(const GemmF16Args &p, int *sexp, floa
     float w = 0.0f;
     if (i < BM) {
       if (row0 + i < p.M) {
-        s = scale_exp(p.amax[row0 + i]);
-        w = kcnn::f16x3::spread_weight(p.acnt[row0 + i]);
+        const uint32_t m = p.amax[row0 + i];
+        s = scale_exp(m);
+        w = m == 0 ? -__builtin_inff() : kcnn::f16x3::spread_weight(p.acnt[row0 + i]);
       }
     } else if (col0 + i - BM < p.N) {
-      s = scale_exp(p.bmax[col0 + i - BM]);
-      w = kcnn::f16x3::spread_weight(p.bcnt[col0 + i - BM]);
+      const uint32_t m = p.bmax[col0 + i - BM];
+      s = scale_exp(m);
+      w = m == 0 ? -__builtin_inff() : kcnn::f16x3::spread_weight(p.bcnt[col0 + i - BM]);
     }
     sexp[i] = s;
     sw[i] = w;
     skip |= s == SKIP;
-    spr |= w != 0.0f;
+    spr |= w > 0.0f;
   }
   const int any_skip = __syncthreads_or(skip) != 0;
   return any_skip | (__syncthreads_or(spr) != 0 ? 2 : 0);
@@ -508,7 +512,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
         const int ec = sexp[BM + cl];
         const float wc = check ? sw[BM + cl] : 0.0f;
         const bool bcheck =
-            check && (__ballot(wc != 0.0f || sw[wm * 64 + i * 32 + (lane & 31)] != 0.0f) != 0);
+            check && (__ballot(wc > 0.0f || sw[wm * 64 + i * 32 + (lane & 31)] > 0.0f) != 0);
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
           const int rr = (g & 3) + 8 * (g >> 2) + 4 * half2;
@@ -562,7 +566,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
       // this 32 x 32 block's check: one of its columns or rows is spread
       // (wave-uniform; most blocks skip it)
       const bool bcheck =
-          check && (__ballot(wc != 0.0f || sw[wm * 64 + i * 32 + (lane & 31)] != 0.0f) != 0);
+          check && (__ballot(wc > 0.0f || sw[wm * 64 + i * 32 + (lane & 31)] > 0.0f) != 0);
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int rl = wm * 64 + i * 32 + (g & 3) + 8 * (g >> 2) + 4 * half2;
@@ -1293,10 +1297,11 @@ __device__ __forceinline__ uint32_t reduce_quad(const GemmF16Args &p, int64_t e,
   if (ar >= NONFINITE) return 0;
   const float sv[4] = {v.x, v.y, v.z, v.w};
 #ifdef KCNN_EXPERIMENTS  // A/B: KCNN_RED_DEBUG & 1 drops the spread check
-  const bool any = !(p.dbg & 1) && (cr | cc[0] | cc[1] | cc[2] | cc[3]) != 0;
+  const bool any = !(p.dbg & 1) && (cr | cc[0] | cc[1] | cc[2] | cc[3]) != 0 && ar != 0;
 #else
   // the counts are 0 unless a group is spread, so one test skips the check
-  const bool any = (cr | cc[0] | cc[1] | cc[2] | cc[3]) != 0;
+  // (an all-zero row: its products are exactly 0, no check)
+  const bool any = (cr | cc[0] | cc[1] | cc[2] | cc[3]) != 0 && ar != 0;
 #endif
   float *o = p.C + (int64_t)r * p.ldc + c;
   const bool fin = max(max(bm[0], bm[1]), max(bm[2], bm[3])) < NONFINITE;
@@ -1336,7 +1341,8 @@ __device__ __forceinline__ uint32_t reduce_quad(const GemmF16Args &p, int64_t e,
     const int er = scale_exp(ar);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if (bm[i] >= NONFINITE || (cr | cc[i]) == 0) continue;
+      // (an all-zero column: exact, no check)
+      if (bm[i] >= NONFINITE || bm[i] == 0 || (cr | cc[i]) == 0) continue;
       thr[i] = __builtin_amdgcn_ldexpf(
           kcnn::f16x3::spread_weight(cr) + kcnn::f16x3::spread_weight(cc[i]),
           -(er + scale_exp(bm[i])));

@@ -49,6 +49,7 @@
 // (double-buffered, 2 x 48 KB), one barrier per step.  Thin outputs split K
 // over workgroups into partial slabs, which gemm_f16x3_reduce_kernel sums in
 // a fixed order.
+#include <atomic>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -85,7 +86,9 @@ struct GemmF16Args {
   float *C;                      // the output
   float *part;                   // ksplit > 1: the partial slabs [ksplit][M][N]
   uint32_t *rflag;               // ksplit > 1: per 64 quads of C, 1 when the reduce left
-                                 // its rejections to gemm_f16x3_fixup_kernel
+                                 // its rejections to gemm_f16x3_fixup_kernel; after
+                                 // them one word, gen when any group was flagged
+  uint32_t gen;                  // this call's number (host counter, never 0)
   const uint32_t *amax, *bmax;   // max |x| bits per row of op(A), per column of op(B)
   const uint32_t *amin, *bmin;   // min nonzero |x| bits (0: none), the same groups
   const uint32_t *acnt, *bcnt;   // spread groups: their elements below 2^-3 after the scale
@@ -1377,7 +1380,10 @@ __global__ __launch_bounds__(256) void gemm_f16x3_reduce_kernel(GemmF16Args p, i
     const int n = __builtin_popcountll(__ballot(rej & 1)) + __builtin_popcountll(__ballot(rej & 2)) +
                   __builtin_popcountll(__ballot(rej & 4)) + __builtin_popcountll(__ballot(rej & 8));
     const bool defer = n > REJ_LOCAL;
-    if (lane == 0) p.rflag[e >> 6] = defer ? 1u : 0u;
+    if (lane == 0) {
+      p.rflag[e >> 6] = defer ? 1u : 0u;
+      if (defer) p.rflag[(total + 63) >> 6] = p.gen;
+    }
     if (n == 0 || defer) continue;
     fix_rejected(p, a_kc != 0, b_kc != 0, rej, lane, [&](int l, int bit, int &row, int &col) {
       row = __builtin_amdgcn_readlane(r, l);
@@ -1398,6 +1404,11 @@ __global__ __launch_bounds__(256) void gemm_f16x3_reduce_kernel(GemmF16Args p, i
 //    the waves by lane & 3.
 // Deterministic: the group's results do not depend on the block or order.
 constexpr int FIX_DEPTH = 16;
+// the fixup's grid: a flagged call's groups take the workgroups in turn
+// (c2's weight-gradient shape with 32 spread rows, 1452 groups: +925 us at
+// 128 workgroups, experiments/fixup_storm.py); an unflagged call exits at the
+// first load, and the launch costs the same 4.4 us at 128 or 1024
+constexpr int FIX_GRID = 1024;
 __global__ __launch_bounds__(256) void gemm_f16x3_fixup_kernel(GemmF16Args p, int a_kc,
                                                                int b_kc, int rows) {
   __shared__ int list[256];
@@ -1408,6 +1419,9 @@ __global__ __launch_bounds__(256) void gemm_f16x3_fixup_kernel(GemmF16Args p, in
   const int64_t plane = (int64_t)p.M * np4;
   const int64_t nslots = (total + 63) >> 6;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // nothing flagged in this call (the word is another call's number, or
+  // anything the workspace held: a stale match only costs the scan below)
+  if (p.rflag[nslots] != p.gen) return;
   for (int64_t base = 0; base < nslots; base += (int64_t)gridDim.x * blockDim.x) {
     if (threadIdx.x == 0) nlist = 0;
     __syncthreads();
@@ -1559,7 +1573,7 @@ size_t slab_bytes(int s, int M, int N) {
   return align16(sizeof(float) * (size_t)s * M * ((N + 3) & ~3));
 }
 size_t flag_bytes(int M, int N) {
-  return align16(sizeof(uint32_t) * (((size_t)M * ((N + 3) / 4) + 63) / 64));
+  return align16(sizeof(uint32_t) * (((size_t)M * ((N + 3) / 4) + 63) / 64 + 1));
 }
 size_t partial_bytes(int M, int N, int K) {
   const int64_t tiles = (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
@@ -1630,6 +1644,9 @@ static int gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alph
   if (s > 1) {
     a.part = static_cast<float *>(ws);
     a.rflag = reinterpret_cast<uint32_t *>(static_cast<char *>(ws) + slab_bytes(s, M, N));
+    static std::atomic<uint32_t> calls{0};
+    a.gen = ++calls;
+    if (a.gen == 0) a.gen = ++calls;
   }
   a.ksplit = s;
   a.kps = ((K + s - 1) / s + BK - 1) / BK * BK;
@@ -1662,7 +1679,7 @@ static int gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alph
   const int rows = !b_kc && ldb % 4 == 0 && (uintptr_t)B % 16 == 0 && N % 4 == 0;
   const int64_t slots = ((int64_t)M * ((N + 3) / 4) + 63) / 64;
   hipLaunchKernelGGL(gemm_f16x3_fixup_kernel,
-                     dim3((unsigned)std::min<int64_t>(1024, (slots + 15) / 16)), dim3(256), 0, st,
+                     dim3((unsigned)std::min<int64_t>(FIX_GRID, (slots + 15) / 16)), dim3(256), 0, st,
                      a, a_kc ? 1 : 0, b_kc ? 1 : 0, rows);
   return kcnn::launch_status();
 }

@@ -308,7 +308,7 @@ struct MomentumUpdate {
 
 struct BiasUpdate {
   float *b; const float *gb; float a_g;
-  __device__ void operator()(int64_t, int j) const { b[j] = a_g * gb[j] + b[j]; }
+  __device__ void operator()(int64_t, int j) const { b[j] = __builtin_fmaf(a_g, gb[j], b[j]); }
 };
 
 // Both in one launch: rows [0, rows) of W as MomentumUpdate, the extra row

@@ -97,7 +97,12 @@ __global__ __launch_bounds__(256) void kl_colsum_final(
 #pragma unroll
     for (int u = 0; u < 8; u++) s += t[u];
   }
-  v[j] = beta == 0.0f ? alpha * s : beta * v[j] + alpha * s;
+  // beta 1: one rounding, the bits of BiasUpdate's fma(a_g, gb, b)
+  // (cnsl-hip-kernels.hip), so a bias row updated here equals one updated
+  // from a stored column sum
+  v[j] = beta == 0.0f   ? alpha * s
+         : beta == 1.0f ? __builtin_fmaf(alpha, s, v[j])
+                        : beta * v[j] + alpha * s;
 }
 
 // C = sum_s P_s + beta C  (split-K partials [S][m][n], fixed order).

@@ -1200,14 +1200,9 @@ void FullyConnectedComponent::UpdateSimple(const CuMatrixBase<BaseFloat> &in_val
     CuProfileScope prof("FullyConnectedComponent::ComputeGradient");
     if (linear_params_.AddMatMatMomentum(out_deriv, kTrans, in_value, kNoTrans, &prev_grad_,
                                          momentum_, a_wd, a_g)) {
-      Scratch gbs(sizeof(BaseFloat) * (size_t)OutputDim());
-      CuSubVector<BaseFloat> gb(gbs.f(), OutputDim());
-      gb.AddRowSumMat(1.0, out_deriv, 0.0);
-      // (hipF_momentum_update with no weight rows: its bias row alone)
-      CNSL_SAFE_CALL(hipF_momentum_update(
-          linear_params_.Data(), Dense(0, OutputDim()), prev_grad_.Data(),
-          Dense(0, OutputDim()), gbs.f(), Dense(0, OutputDim()), momentum_, a_wd, a_g,
-          bias_params_.Data(), gbs.f(), OutputDim(), S()));
+      // the bias row b = a_g colsum(dY) + b in the column sum's final pass
+      // (one rounding: ApplyGradient's BiasUpdate bits, no gradient vector)
+      bias_params_.AddRowSumMat(a_g, out_deriv, 1.0);
       return;
     }
   }

@@ -24,10 +24,16 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 
+#include <vector>
+
 #include "conv-geom.h"
+#include "f16-split.h"
 #include "x6-util.h"
+#include "../kaldi-lite/cu-device.h"
+#include "../kaldi-lite/cu-kernels-lite.h"
 
 using namespace kcnn;
 
@@ -50,6 +56,15 @@ __device__ __forceinline__ void put8(char *img, int pl_bytes, int off, const flo
   *reinterpret_cast<uint4 *>(img + 2 * pl_bytes + off) = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
+// eight fp32 under the scale 2^e -> one 16-B chunk of each f16 plane (f16x3)
+__device__ __forceinline__ void put8h(char *img, int pl_bytes, int off, const float *v, int e,
+                                      float m1) {
+  f16x3::f16x8 hh, ll;
+  f16x3::split8h(v, e, hh, ll, m1);
+  *reinterpret_cast<f16x3::f16x8 *>(img + off) = hh;
+  *reinterpret_cast<f16x3::f16x8 *>(img + pl_bytes + off) = ll;
+}
+
 // The Maxpool that follows the convolution, pooled in the epilogue (POOL >
 // 0): a window of 2 consecutive map positions (ph x pw = 2 x 1 with oh even,
 // or 1 x 2 with oh = 1: positions p, p + 1 with p even, the columns m, m + 1
@@ -64,13 +79,34 @@ struct PoolOut {
   int ms;
 };
 
-template <int BG, bool PADDED, bool STG, bool TAB, int POOL>
+// The f16x3 form (F16, igemm_x6 family value 2; f16-split.h): two f16 planes
+// per operand under a power-of-two scale per group, three products per pair.
+// The groups: A's rows are W's columns (one filter over every k), B's columns
+// take the scale of their frame (every tap of an im2col column reads one
+// frame of X, so a frame's max covers them).  Statistics blocks [max, min,
+// cnt] (kl_absmax_cols of W, kl_absmax_rows of X: f16-split.h spread /
+// spread_weight).  A tile with an Inf / NaN group, or an element the store
+// check (the GEMM's tile_epilogue rule: |acc| >= the two groups' spread
+// weights) cannot clear, is flagged and stores nothing; the bf16x6 form of
+// the same kernel then runs with redo = the flags and recomputes exactly the
+// flagged tiles (their results are then bf16x6's, its contract: DESIGN 3).
+struct F16Aux {
+  const uint32_t *wst;   // [max G][min G][cnt G] of W's columns
+  const uint32_t *xst;   // [max R][min R][cnt R] of X's rows (frames)
+  unsigned *tflag;       // F16: per tile (logical id), 1 = recompute
+  const unsigned *redo;  // bf16x6 form: non-null = only the flagged tiles
+};
+constexpr int kAuxBytes = 384 * 8;  // F16: scale exponents and weights of a tile's groups
+
+template <int BG, bool PADDED, bool STG, bool TAB, int POOL, bool F16>
 __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
     ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ Kw, int ks,
-    const float *__restrict__ bias, float *__restrict__ out, int os, int relu, PoolOut po) {
+    const float *__restrict__ bias, float *__restrict__ out, int os, int relu, PoolOut po,
+    F16Aux fx) {
   constexpr int BN = 384 - BG;
   constexpr int APT = BG * BK / NT, BPT = BN * BK / NT;  // values per thread per step
-  constexpr int PLA = BG * ROWB, PLB = BN * ROWB, BUF = 3 * (PLA + PLB);
+  constexpr int NPL = F16 ? 2 : 3;                       // planes per operand
+  constexpr int PLA = BG * ROWB, PLB = BN * ROWB, BUF = NPL * (PLA + PLB);
   constexpr int WN = BN / 64;                            // waves along m
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -87,6 +123,9 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
   const int g0 = (lid % tiles_g) * BG;
   const int64_t m0 = (int64_t)(lid / tiles_g) * BN;
   const int T = (g.Kdim + BK - 1) / BK;
+  if constexpr (!F16) {
+    if (fx.redo && fx.redo[lid] == 0) return;  // (uniform) the f16x3 result stands
+  }
 
   // A = W^T: thread row g0 + a_row, k = kt*32 + a_kc*APT + j (a_kc uniform)
   const int a_row = tid % BG;
@@ -130,6 +169,47 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
   const int KT = T * BK;
   unsigned *ktab = reinterpret_cast<unsigned *>(lds + 2 * BUF);
   unsigned char *ttab = reinterpret_cast<unsigned char *>(ktab + (TAB ? KT : 0));
+
+  // F16: the tile's group scales (sexp) and check weights (sw): entries
+  // [0, BG) its rows g, [BG, 384) its columns m; groups past G / M: scale 0,
+  // weight -inf (never checked).  A tile with an Inf / NaN group is flagged.
+  int *sexp = reinterpret_cast<int *>(lds + 2 * BUF + (TAB ? KT * 4 + (PADDED ? KT : 0) : 0));
+  float *sw = reinterpret_cast<float *>(sexp + 384);
+  int ea = 0, eb = 0;
+  if constexpr (F16) {
+    bool bad = false;
+    if (tid < 384) {
+      uint32_t mx = 0, cnt = 0;
+      bool in = false;
+      if (tid < BG) {
+        const int gg = g0 + tid;
+        if (gg < g.G) {
+          in = true;
+          mx = fx.wst[gg];
+          cnt = fx.wst[2 * (size_t)g.G + gg];
+        }
+      } else {
+        const int64_t mm = m0 + (tid - BG);
+        if (mm < g.M) {
+          uint32_t n, p;
+          g.div_P.divmod((uint32_t)mm, n, p);
+          in = true;
+          mx = fx.xst[n];
+          cnt = fx.xst[2 * (size_t)g.R + n];
+        }
+      }
+      const int e = in ? f16x3::scale_exp(mx) : 0;
+      bad = e == f16x3::SKIP;
+      sexp[tid] = bad ? 0 : e;
+      sw[tid] = in && mx != 0 ? f16x3::spread_weight(cnt) : -__builtin_inff();
+    }
+    if (__syncthreads_or(bad)) {
+      if (tid == 0) fx.tflag[lid] = 1u;
+      return;
+    }
+    ea = sexp[a_row];
+    eb = sexp[BG + b_row];
+  }
   if constexpr (TAB) {
     for (int k = tid; k < KT; k += NT) {
       uint32_t c = 0, r = 0, kx = 0, ky = 0;
@@ -205,13 +285,23 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
       }
     }
   };
+  const float m1 = F16 ? f16x3::opaque_m1() : -1.0f;
   auto store = [&](char *buf) {
+    if constexpr (F16) {
 #pragma unroll
-    for (int cc = 0; cc < APT / 8; cc++)
-      put8(buf, PLA, swz(a_row, a_kc * (APT / 8) + cc), &av[8 * cc]);
+      for (int cc = 0; cc < APT / 8; cc++)
+        put8h(buf, PLA, swz(a_row, a_kc * (APT / 8) + cc), &av[8 * cc], ea, m1);
 #pragma unroll
-    for (int cc = 0; cc < BPT / 8; cc++)
-      put8(buf + 3 * PLA, PLB, swz(b_row, b_kc * (BPT / 8) + cc), &bv[8 * cc]);
+      for (int cc = 0; cc < BPT / 8; cc++)
+        put8h(buf + 2 * PLA, PLB, swz(b_row, b_kc * (BPT / 8) + cc), &bv[8 * cc], eb, m1);
+    } else {
+#pragma unroll
+      for (int cc = 0; cc < APT / 8; cc++)
+        put8(buf, PLA, swz(a_row, a_kc * (APT / 8) + cc), &av[8 * cc]);
+#pragma unroll
+      for (int cc = 0; cc < BPT / 8; cc++)
+        put8(buf + 3 * PLA, PLB, swz(b_row, b_kc * (BPT / 8) + cc), &bv[8 * cc]);
+    }
   };
 
   floatx16 acc[2][2];
@@ -229,9 +319,26 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
   const int ar = wm * 64 + l, br = wn * 64 + l;
   // one k16 half of a step: 12 fragment reads, 24 MFMAs
   auto half_step = [&](const char *bufA, int s) {
+    const int c = 2 * s + h;
+    if constexpr (F16) {  // 8 fragment reads, 12 MFMAs
+      const char *bufB = bufA + 2 * PLA;
+      f16x3::f16x8 a[2][2], bb[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int pl = 0; pl < 2; pl++) {
+          a[i][pl] = *reinterpret_cast<const f16x3::f16x8 *>(bufA + pl * PLA + swz(ar + 32 * i, c));
+          bb[i][pl] = *reinterpret_cast<const f16x3::f16x8 *>(bufB + pl * PLB + swz(br + 32 * i, c));
+        }
+#pragma unroll
+      for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+          acc[i][j] = f16x3::mfma3(a[i][0], a[i][1], bb[j][0], bb[j][1], acc[i][j]);
+      return;
+    }
     const char *bufB = bufA + 3 * PLA;
     x6::bf16x8 a[2][3], bb[2][3];
-    const int c = 2 * s + h;
 #pragma unroll
     for (int i = 0; i < 2; i++)
 #pragma unroll
@@ -260,6 +367,31 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
 
   // epilogue: accumulator r of lane (l, h) is row g0 + wm*64 + 32i +
   // mfma32_row(r), column m0 + wn*64 + 32j + l; concat layout + bias (+ReLU)
+  if constexpr (F16) {
+    // the store check (f16-split.h: a scaled sum of at least the groups'
+    // spread weights keeps its small elements' error under 2^-19 of itself),
+    // then the exact unscale; a tile with a rejection stores nothing and is
+    // recomputed by the bf16x6 form
+    bool fail = false;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const int cl = BG + wn * 64 + 32 * j + l;
+      const int ec = sexp[cl];
+      const float wc = sw[cl];
+#pragma unroll
+      for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const int rl = wm * 64 + 32 * i + mfma32_row(r, lane);
+          const float v = acc[i][j][r];
+          fail |= fabsf(v) < sw[rl] + wc;
+          acc[i][j][r] = __builtin_amdgcn_ldexpf(v, -(sexp[rl] + ec));
+        }
+    }
+    const int f = __syncthreads_or(fail);
+    if (tid == 0) fx.tflag[lid] = f ? 1u : 0u;
+    if (f) return;
+  }
   if constexpr (POOL > 0) {
     constexpr int PC = POOL == 1 ? 4 : POOL == 2 ? 1 : 2;
     const int Q = g.P >> 1;  // pooled positions per map
@@ -713,53 +845,116 @@ int stagger() {
 }
 
 constexpr int kLdsMax = 160 * 1024;
-constexpr int kImgBytes = 2 * 3 * 384 * ROWB;  // the double-buffered plane images
+constexpr int img_bytes(bool f16) { return 2 * (f16 ? 2 : 3) * 384 * ROWB; }  // double-buffered planes
 
 // LDS of the tap table for Kdim (0: it does not fit beside the images)
 int tab_bytes(const ConvGeom &g, bool padded) {
   static const int use = KCNN_KNOB("KCNN_IGX6_TAB", 1);
   const int KT = (g.Kdim + BK - 1) / BK * BK;
   const int b = KT * 4 + (padded ? KT : 0);
-  return use && kImgBytes + b <= kLdsMax ? b : 0;
+  return use && img_bytes(false) + b <= kLdsMax ? b : 0;
 }
 
-template <int BG, bool PADDED, bool STG, bool TAB, int POOL = 0>
-void launch_t(const ConvGeom &g, unsigned blocks, int lds, const float *X, int xs,
-              const float *K, int ks, const float *bias, float *out, int os, int relu,
-              hipStream_t st, PoolOut po = PoolOut{}) {
+template <int BG, bool PADDED, bool STG, bool TAB, int POOL, bool F16>
+void launch_t(const ConvGeom &g, unsigned blocks, const float *X, int xs, const float *K,
+              int ks, const float *bias, float *out, int os, int relu, hipStream_t st,
+              PoolOut po, F16Aux fx) {
+  const int lds = img_bytes(F16) + (TAB ? tab_bytes(g, PADDED) : 0) + (F16 ? kAuxBytes : 0);
   static bool attr = hipFuncSetAttribute(
-      reinterpret_cast<const void *>(&conv_igemm_x6_kernel<BG, PADDED, STG, TAB, POOL>),
+      reinterpret_cast<const void *>(&conv_igemm_x6_kernel<BG, PADDED, STG, TAB, POOL, F16>),
       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax) == hipSuccess;
   (void)attr;
-  hipLaunchKernelGGL((conv_igemm_x6_kernel<BG, PADDED, STG, TAB, POOL>), dim3(blocks),
-                     dim3(NT), lds, st, g, X, xs, K, ks, bias, out, os, relu, po);
+  hipLaunchKernelGGL((conv_igemm_x6_kernel<BG, PADDED, STG, TAB, POOL, F16>), dim3(blocks),
+                     dim3(NT), lds, st, g, X, xs, K, ks, bias, out, os, relu, po, fx);
+}
+// the bf16x6 form (redo: only the tiles the f16x3 form flagged), or the
+// f16x3 form then the bf16x6 redo of its flagged tiles
+template <int BG, bool PADDED, bool TAB, int POOL>
+void launch_pair(const ConvGeom &g, unsigned blocks, const float *X, int xs, const float *K,
+                 int ks, const float *bias, float *out, int os, int relu, hipStream_t st,
+                 PoolOut po, F16Aux fx) {
+  if (fx.tflag) {
+    launch_t<BG, PADDED, false, TAB, POOL, true>(g, blocks, X, xs, K, ks, bias, out, os, relu,
+                                                 st, po, fx);
+    fx.redo = fx.tflag;
+  }
+  launch_t<BG, PADDED, false, TAB, POOL, false>(g, blocks, X, xs, K, ks, bias, out, os, relu,
+                                                st, po, fx);
 }
 // pooled epilogue (POOL > 0): no stagger (the host declines it)
 template <int BG, bool PADDED, int POOL>
 void launch_pool(const ConvGeom &g, unsigned blocks, const float *X, int xs, const float *K,
-                 int ks, const float *bias, float *out, int os, PoolOut po, hipStream_t st) {
-  const int tb = tab_bytes(g, PADDED);
-  const int lds = kImgBytes + tb;
-  if (tb) launch_t<BG, PADDED, false, true, POOL>(g, blocks, lds, X, xs, K, ks, bias, out, os, 0, st, po);
-  else launch_t<BG, PADDED, false, false, POOL>(g, blocks, lds, X, xs, K, ks, bias, out, os, 0, st, po);
+                 int ks, const float *bias, float *out, int os, PoolOut po, F16Aux fx,
+                 hipStream_t st) {
+  if (tab_bytes(g, PADDED))
+    launch_pair<BG, PADDED, true, POOL>(g, blocks, X, xs, K, ks, bias, out, os, 0, st, po, fx);
+  else
+    launch_pair<BG, PADDED, false, POOL>(g, blocks, X, xs, K, ks, bias, out, os, 0, st, po, fx);
 }
 template <int BG, bool PADDED>
 void launch(const ConvGeom &g, unsigned blocks, const float *X, int xs, const float *K, int ks,
-            const float *bias, float *out, int os, int relu, hipStream_t st) {
-  const int tb = tab_bytes(g, PADDED);
-  const int lds = kImgBytes + tb;
-  if (tb) {
-    if (stagger()) launch_t<BG, PADDED, true, true>(g, blocks, lds, X, xs, K, ks, bias, out, os, relu, st);
-    else launch_t<BG, PADDED, false, true>(g, blocks, lds, X, xs, K, ks, bias, out, os, relu, st);
-  } else {
-    if (stagger()) launch_t<BG, PADDED, true, false>(g, blocks, lds, X, xs, K, ks, bias, out, os, relu, st);
-    else launch_t<BG, PADDED, false, false>(g, blocks, lds, X, xs, K, ks, bias, out, os, relu, st);
+            const float *bias, float *out, int os, int relu, F16Aux fx, hipStream_t st) {
+  const bool tb = tab_bytes(g, PADDED) != 0;
+  if (stagger() && !fx.tflag) {
+    if (tb) launch_t<BG, PADDED, true, true, 0, false>(g, blocks, X, xs, K, ks, bias, out, os, relu, st, PoolOut{}, fx);
+    else launch_t<BG, PADDED, true, false, 0, false>(g, blocks, X, xs, K, ks, bias, out, os, relu, st, PoolOut{}, fx);
+    return;
   }
+  if (tb) launch_pair<BG, PADDED, true, 0>(g, blocks, X, xs, K, ks, bias, out, os, relu, st, PoolOut{}, fx);
+  else launch_pair<BG, PADDED, false, 0>(g, blocks, X, xs, K, ks, bias, out, os, relu, st, PoolOut{}, fx);
+}
+
+// The f16x3 form's statistics and tile flags (igemm_x6 family 2) in per-call
+// scratch from the device allocator (kaldi-lite/cu-device.h CuScratch: the
+// block is reused only by work ordered after this call's kernels): W's column
+// and X's row statistics (f16-split.h), one flag per tile.  Returns 0, or
+// the error of a statistics launch.
+struct F16Setup {
+  kaldi::CuScratch ws;
+  F16Aux fx{};
+  int rc = 0;
+  F16Setup(bool on, const ConvGeom &g, const float *X, int xs, const float *K, int ks,
+           unsigned blocks, hipStream_t st)
+      : ws(on ? words(g, blocks) * 4 : 0) {
+    if (!on) return;
+    uint32_t *w = static_cast<uint32_t *>(ws.p);
+    uint32_t *wst = w, *xst = wst + 3 * (size_t)g.G, *tflag = xst + 3 * (size_t)g.R,
+             *part = tflag + blocks;
+    rc = kl_absmax_rows_cols(X, g.R, g.HW * g.C, xs, xst, K, g.Kdim, g.G, ks, wst, part,
+                             reinterpret_cast<kcnn_stream_t>(st));
+    fx.wst = wst;
+    fx.xst = xst;
+    fx.tflag = tflag;
+  }
+  static size_t words(const ConvGeom &g, unsigned blocks) {
+    return 3 * (size_t)g.G + 3 * (size_t)g.R + blocks + kl_absmax_cols_words(g.Kdim, g.G);
+  }
+};
+// f16x3 for the long kernels (c5's Kdim 768 / 2304); shorter ones (nnet.config's
+// 384 / 512) keep bf16x6: their few K steps do not repay the statistics pass
+// over X (measured: nnet.config's convolutions 2.06 -> 2.20 ms per step)
+bool use_f16(const ConvGeom &g) {
+  static const int kmin = KCNN_KNOB("KCNN_IGF16_KMIN", 768);
+  return family(kFamIgemmX6) == 2 && g.R > 0 && g.Kdim >= kmin;
+}
+// experiment build: KCNN_IGF16_DEBUG=1 prints each call's flagged tiles
+void report_flags(const F16Aux &fx, unsigned nb, const ConvGeom &g, hipStream_t st) {
+  static const int dbg = KCNN_KNOB("KCNN_IGF16_DEBUG", 0);
+  if (!dbg || !fx.tflag) return;
+  std::vector<unsigned> f(nb);
+  if (hipMemcpyAsync(f.data(), fx.tflag, nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return;
+  unsigned n = 0;
+  for (unsigned v : f) n += v != 0;
+  fprintf(stderr, "igemm f16x3: G %d Kdim %d M %lld: %u of %u tiles recomputed\n", g.G, g.Kdim,
+          (long long)g.M, n, nb);
 }
 
 }  // namespace
 
-// Conv2D(concat) + bias (+ ReLU) on the bf16 MFMAs; -1 (nothing launched)
+// Conv2D(concat) + bias (+ ReLU) on the f16 (family igemm_x6 = 2, with the
+// bf16x6 form for flagged tiles) or bf16 (1) MFMAs; -1 (nothing launched)
 // for shapes outside its addressing limits.  KCNN_IGEMM_X6=0 disables it
 // (the fp32-MFMA conv_igemm2_kernel then runs).
 // Blocks of kcnn_conv_igemm_x6 for g, 0 when the shape is outside its limits.
@@ -782,14 +977,18 @@ int kcnn_conv_igemm_x6(const ConvGeom &g, const float *X, int xs, const float *K
                        const float *bias, float *out, int os, int relu, hipStream_t st) {
   const unsigned nb = igemm_x6_blocks(g, xs, ks);
   if (nb == 0) return -1;
+  const bool f16 = use_f16(g);
+  F16Setup fs(f16, g, X, xs, K, ks, nb, st);
+  if (fs.rc) return fs.rc;
   const bool padded = g.pad_h > 0 || g.pad_w > 0;
   if (g.G <= 128) {
-    if (padded) launch<128, true>(g, nb, X, xs, K, ks, bias, out, os, relu, st);
-    else launch<128, false>(g, nb, X, xs, K, ks, bias, out, os, relu, st);
+    if (padded) launch<128, true>(g, nb, X, xs, K, ks, bias, out, os, relu, fs.fx, st);
+    else launch<128, false>(g, nb, X, xs, K, ks, bias, out, os, relu, fs.fx, st);
   } else {
-    if (padded) launch<256, true>(g, nb, X, xs, K, ks, bias, out, os, relu, st);
-    else launch<256, false>(g, nb, X, xs, K, ks, bias, out, os, relu, st);
+    if (padded) launch<256, true>(g, nb, X, xs, K, ks, bias, out, os, relu, fs.fx, st);
+    else launch<256, false>(g, nb, X, xs, K, ks, bias, out, os, relu, fs.fx, st);
   }
+  report_flags(fs.fx, nb, g, st);
   return (int)hipGetLastError();
 }
 
@@ -807,13 +1006,16 @@ int kcnn_conv_igemm_x6_pool(const ConvGeom &g, const float *X, int xs, const flo
   if (!win || !(pc == 1 || pc == 2 || pc == 4) || g.G % pc != 0 || stagger()) return -1;
   const unsigned nb = igemm_x6_blocks(g, xs, ks);
   if (nb == 0) return -1;
+  const bool f16 = use_f16(g);
+  F16Setup fs(f16, g, X, xs, K, ks, nb, st);
+  if (fs.rc) return fs.rc;
   const PoolOut po{pool, ps, mask, ms};
   const bool padded = g.pad_h > 0 || g.pad_w > 0;
 #define KCNN_IGP(BG_, PAD_)                                                                 \
   do {                                                                                      \
-    if (pc == 4) launch_pool<BG_, PAD_, 1>(g, nb, X, xs, K, ks, bias, out, os, po, st);     \
-    else if (pc == 1) launch_pool<BG_, PAD_, 2>(g, nb, X, xs, K, ks, bias, out, os, po, st); \
-    else launch_pool<BG_, PAD_, 3>(g, nb, X, xs, K, ks, bias, out, os, po, st);             \
+    if (pc == 4) launch_pool<BG_, PAD_, 1>(g, nb, X, xs, K, ks, bias, out, os, po, fs.fx, st);     \
+    else if (pc == 1) launch_pool<BG_, PAD_, 2>(g, nb, X, xs, K, ks, bias, out, os, po, fs.fx, st); \
+    else launch_pool<BG_, PAD_, 3>(g, nb, X, xs, K, ks, bias, out, os, po, fs.fx, st);             \
   } while (0)
   if (g.G <= 128) {
     if (padded) KCNN_IGP(128, true);
@@ -823,6 +1025,7 @@ int kcnn_conv_igemm_x6_pool(const ConvGeom &g, const float *X, int xs, const flo
     else KCNN_IGP(256, false);
   }
 #undef KCNN_IGP
+  report_flags(fs.fx, nb, g, st);
   return (int)hipGetLastError();
 }
 

@@ -1601,6 +1601,21 @@ extern "C" int kl_absmax_cols(const float *X, int rows, int cols, int ld, uint32
                       kcnn::as_stream(stream));
 }
 
+// kl_absmax_rows of R (rows x cols, pitch ld) and kl_absmax_cols of Q
+// (qrows x qcols, pitch ldq; part: kl_absmax_cols_words) in one statistics
+// launch (and Q's finalize / count passes): the f16x3 implicit GEMM's frame
+// and filter statistics (cnsl-conv-igemm-x6.hip)
+extern "C" int kl_absmax_rows_cols(const float *R, int rows, int cols, int ld, uint32_t *rmax,
+                                   const float *Q, int qrows, int qcols, int ldq, uint32_t *cmax,
+                                   uint32_t *part, kcnn_stream_t stream) {
+  if (rows < 0 || cols < 0 || ld < cols || !rmax || qrows < 0 || qcols < 0 || ldq < qcols ||
+      !cmax)
+    return (int)hipErrorInvalidValue;
+  if (qrows > 0 && qcols > 0 && !part) return (int)hipErrorInvalidValue;
+  return stats_launch(stat_op(Q, qrows, qcols, ldq, 1, cmax, part),
+                      stat_op(R, rows, cols, ld, 0, rmax, nullptr), kcnn::as_stream(stream));
+}
+
 // C[M x N] = alpha * op(A) op(B) + beta * C with the operands' max |x| given:
 // amax[i] for row i of op(A), bmax[j] for column j of op(B) (bit patterns of
 // max |x|, kl_absmax_rows / kl_absmax_cols).  Needs 16-B aligned

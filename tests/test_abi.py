@@ -96,7 +96,7 @@ def test_product_library_reads_only_documented_switches():
 
 def test_kernel_family_selectors():
     _lib()
-    defaults = {"fwd_x6": 2, "bwd_x6": 1, "igemm_x6": 1, "wgrad_x6": 2, "gemm": 2}
+    defaults = {"fwd_x6": 2, "bwd_x6": 1, "igemm_x6": 2, "wgrad_x6": 2, "gemm": 2}
     for name, d in defaults.items():
         if not os.environ.get("KCNN_" + name.upper()):
             assert kcnn.get_kernel_family(name) == d, name

@@ -1,6 +1,7 @@
 """The kernel-family selectors (kcnn.set_kernel_family, include/kcnn.h;
 kaldi-lite/kcnn-knobs.h) against the oracle: every family switched to its
-fp32-MFMA implementation (and the weight gradient's 128-wide bf16x6 kernel)
+fp32-MFMA implementation (and the weight gradient's 128-wide bf16x6 kernel,
+the implicit GEMM's bf16x6 form beside its f16x3 default)
 must meet the same parity bar as the default kernels (and the forward's
 bf16x6 form beside its f16x3 default), on shapes that reach each family (c2, c5 layers, nnet.config layer 1, the FC GEMM)."""
 import numpy as np
@@ -18,6 +19,7 @@ FAMILY_SHAPES = {
     ("fwd_x6", 1): [(40, 11, 3, 8, 1, 128, 0, 0), (9, 5, 1, 2, 2, 64, 0, 0)],
     ("bwd_x6", 0): [(40, 11, 3, 8, 1, 128, 0, 0), (40, 11, 3, 8, 1, 256, 0, 0)],
     ("igemm_x6", 0): [(8, 9, 256, 3, 3, 256, 1, 1), (40, 21, 1, 40, 4, 128, 0, 0)],
+    ("igemm_x6", 1): [(8, 9, 256, 3, 3, 256, 1, 1), (40, 21, 1, 40, 4, 128, 0, 0)],
     ("wgrad_x6", 0): [(8, 9, 256, 3, 3, 256, 1, 1), (4, 9, 64, 4, 3, 256, 0, 0)],
     ("wgrad_x6", 1): [(8, 9, 256, 3, 3, 256, 1, 1), (11, 11, 64, 4, 3, 256, 0, 0)],
 }

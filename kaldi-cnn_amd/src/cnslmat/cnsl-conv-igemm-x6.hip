@@ -27,7 +27,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
-#include <vector>
+#include <algorithm>
 
 #include "conv-geom.h"
 #include "f16-split.h"
@@ -65,6 +65,45 @@ __device__ __forceinline__ void put8h(char *img, int pl_bytes, int off, const fl
   *reinterpret_cast<f16x3::f16x8 *>(img + pl_bytes + off) = ll;
 }
 
+// One output element (filter gg, column mm = (frame, position)) by a whole
+// wave as an fp32 dot product over k in a fixed lane order (lane sums of k =
+// lane + 64 i, then a butterfly: every lane ends with the same bits), the
+// fixup kernel's element.  Taps outside a padded map are 0.
+__device__ __forceinline__ float conv_dot(const ConvGeom &g, const float *__restrict__ X, int xs,
+                                          const float *__restrict__ Kw, int ks, int gg, int64_t mm,
+                                          int lane) {
+  uint32_t n, p, px, py;
+  g.div_P.divmod((uint32_t)mm, n, p);
+  g.div_oh.divmod(p, px, py);
+  const float *xf = X + (int64_t)n * xs;
+  float s = 0.0f;
+  constexpr int B = 8;  // loads in flight per lane
+  for (int k0 = lane; k0 < g.Kdim; k0 += 64 * B) {
+    float a[B], x[B];
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+      const int k = k0 + 64 * b;
+      a[b] = 0.0f;
+      x[b] = 0.0f;
+      if (k < g.Kdim) {
+        uint32_t c, r, kx, ky;
+        g.div_khkw.divmod((uint32_t)k, c, r);
+        g.div_kh.divmod(r, kx, ky);
+        const int xx = (int)px + (int)kx - g.pad_w, yy = (int)py + (int)ky - g.pad_h;
+        if ((unsigned)xx < (unsigned)g.W && (unsigned)yy < (unsigned)g.H) {
+          a[b] = Kw[(int64_t)k * ks + gg];
+          x[b] = xf[(int64_t)c * g.HW + xx * g.H + yy];
+        }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < B; b++) s = fmaf(a[b], x[b], s);
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+  return s;
+}
+
 // The Maxpool that follows the convolution, pooled in the epilogue (POOL >
 // 0): a window of 2 consecutive map positions (ph x pw = 2 x 1 with oh even,
 // or 1 x 2 with oh = 1: positions p, p + 1 with p even, the columns m, m + 1
@@ -87,14 +126,22 @@ struct PoolOut {
 // cnt] (kl_absmax_cols of W, kl_absmax_rows of X: f16-split.h spread /
 // spread_weight).  A tile with an Inf / NaN group, or an element the store
 // check (the GEMM's tile_epilogue rule: |acc| >= the two groups' spread
-// weights) cannot clear, is flagged and stores nothing; the bf16x6 form of
-// the same kernel then runs with redo = the flags and recomputes exactly the
-// flagged tiles (their results are then bf16x6's, its contract: DESIGN 3).
+// weights) cannot clear, is recomputed in fp32 (conv_dot: a fixed-order dot
+// product, IEEE Inf / NaN like the reference's sgemm):
+//  - a rejected element is stored (or pooled) as computed and listed with
+//    its pool window's values (elist: EW words per entry);
+//    conv_igemm_efix_kernel recomputes it and stores it, or re-pools the
+//    window, over the epilogue's result;
+//  - a tile with an Inf / NaN group, or with a wave of more than REJ_MAX
+//    rejections (a pathological spread), stores nothing and lists its id;
+//    conv_igemm_fixup_kernel computes every element of it.
+constexpr int REJ_MAX = 8;  // listed rejections per wave (more: the whole tile)
+constexpr int EW = 12;      // words per element entry: g, m, mask, 8 window values
 struct F16Aux {
   const uint32_t *wst;   // [max G][min G][cnt G] of W's columns
   const uint32_t *xst;   // [max R][min R][cnt R] of X's rows (frames)
-  unsigned *tflag;       // F16: per tile (logical id), 1 = recompute
-  const unsigned *redo;  // bf16x6 form: non-null = only the flagged tiles
+  unsigned *list;        // [tile count, element count, tile ids (one per tile)]
+  unsigned *elist;       // element entries (8 waves x REJ_MAX per tile)
 };
 constexpr int kAuxBytes = 384 * 8;  // F16: scale exponents and weights of a tile's groups
 
@@ -123,9 +170,6 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
   const int g0 = (lid % tiles_g) * BG;
   const int64_t m0 = (int64_t)(lid / tiles_g) * BN;
   const int T = (g.Kdim + BK - 1) / BK;
-  if constexpr (!F16) {
-    if (fx.redo && fx.redo[lid] == 0) return;  // (uniform) the f16x3 result stands
-  }
 
   // A = W^T: thread row g0 + a_row, k = kt*32 + a_kc*APT + j (a_kc uniform)
   const int a_row = tid % BG;
@@ -204,7 +248,7 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
       sw[tid] = in && mx != 0 ? f16x3::spread_weight(cnt) : -__builtin_inff();
     }
     if (__syncthreads_or(bad)) {
-      if (tid == 0) fx.tflag[lid] = 1u;
+      if (tid == 0) fx.list[2 + atomicAdd(fx.list, 1u)] = (unsigned)lid;
       return;
     }
     ea = sexp[a_row];
@@ -367,12 +411,11 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
 
   // epilogue: accumulator r of lane (l, h) is row g0 + wm*64 + 32i +
   // mfma32_row(r), column m0 + wn*64 + 32j + l; concat layout + bias (+ReLU)
+  uint64_t rej = 0;  // F16: rejected elements, bit 16 (2i + j) + r
   if constexpr (F16) {
     // the store check (f16-split.h: a scaled sum of at least the groups'
     // spread weights keeps its small elements' error under 2^-19 of itself),
-    // then the exact unscale; a tile with a rejection stores nothing and is
-    // recomputed by the bf16x6 form
-    bool fail = false;
+    // then the exact unscale
 #pragma unroll
     for (int j = 0; j < 2; j++) {
       const int cl = BG + wn * 64 + 32 * j + l;
@@ -384,13 +427,17 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
         for (int r = 0; r < 16; r++) {
           const int rl = wm * 64 + 32 * i + mfma32_row(r, lane);
           const float v = acc[i][j][r];
-          fail |= fabsf(v) < sw[rl] + wc;
+          if (fabsf(v) < sw[rl] + wc) rej |= 1ull << (16 * (2 * i + j) + r);
           acc[i][j][r] = __builtin_amdgcn_ldexpf(v, -(sexp[rl] + ec));
         }
     }
-    const int f = __syncthreads_or(fail);
-    if (tid == 0) fx.tflag[lid] = f ? 1u : 0u;
-    if (f) return;
+    int nrej = __builtin_popcountll(rej);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) nrej += __shfl_xor(nrej, d);
+    if (__syncthreads_or(nrej > REJ_MAX)) {
+      if (tid == 0) fx.list[2 + atomicAdd(fx.list, 1u)] = (unsigned)lid;
+      return;
+    }
   }
   if constexpr (POOL > 0) {
     constexpr int PC = POOL == 1 ? 4 : POOL == 2 ? 1 : 2;
@@ -442,6 +489,25 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
             po.pool[(int64_t)on * po.ps + q] = mx;
             po.mask[(int64_t)on * po.ms + q] = (unsigned short)mk;
           }
+          if constexpr (F16) {  // a window holding a rejected element: listed
+            const unsigned rm = (unsigned)(rej >> (16 * (2 * i + j) + r0)) & ((1u << PC) - 1u);
+            const unsigned rp = (unsigned)__shfl_xor((int)rm, 1);
+            if (d == 0 && mv && gv && (rm | rp)) {
+              unsigned bits = 0;
+#pragma unroll
+              for (int c = 0; c < PC; c++)
+                bits |= ((rm >> c) & 1u) << (2 * c) | ((rp >> c) & 1u) << (2 * c + 1);
+              unsigned *e = fx.elist + (size_t)EW * atomicAdd(fx.list + 1, 1u);
+              e[0] = (unsigned)gg0;
+              e[1] = (unsigned)mm;
+              e[2] = bits;
+#pragma unroll
+              for (int c = 0; c < PC; c++) {
+                e[3 + 2 * c] = __float_as_uint(v[c]);
+                e[4 + 2 * c] = __float_as_uint(w[c]);
+              }
+            }
+          }
         }
     }
     return;
@@ -464,6 +530,167 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
         if (relu) v = v < 0.0f ? 0.0f : v;  // RectifiedLinear: ApplyFloor(0)
         orow[(int64_t)gg * g.P] = v;
       }
+  }
+  if constexpr (F16) {
+    while (rej) {  // (rare) this lane's rejected elements, listed
+      const int b = __builtin_ctzll(rej);
+      rej &= rej - 1;
+      const int i = b >> 5, j = (b >> 4) & 1, r = b & 15;
+      const int gg = g0 + wm * 64 + 32 * i + mfma32_row(r, lane);
+      const int64_t mm = m0 + wn * 64 + 32 * j + l;
+      if (gg >= g.G || mm >= g.M) continue;
+      unsigned *e = fx.elist + (size_t)EW * atomicAdd(fx.list + 1, 1u);
+      e[0] = (unsigned)gg;
+      e[1] = (unsigned)mm;
+      e[2] = 1u;
+    }
+  }
+}
+
+// The listed tiles of the f16x3 form in fp32 (F16Aux): work item it = (the
+// list's tile it / 256, chunk it % 256), a chunk being 8 rows g x 16
+// columns m of a BG x BN tile (BG = 256: 32 x 8 chunks; 128: 16 x 16), so
+// it holds whole pool windows (PC | 8 consecutive filters, column pairs m, m
+// + 1 with m even).  Each of the 4 waves computes 32 of its elements
+// (conv_dot) into LDS, then they are stored (+ bias, ReLU) or pooled with
+// the epilogue's order and compares.  A grid of at most 256 blocks walks
+// the items; with an empty list every block leaves at once.
+template <int BG, int POOL>
+__global__ __launch_bounds__(256) void conv_igemm_fixup_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ Kw, int ks,
+    const float *__restrict__ bias, float *__restrict__ out, int os, int relu, PoolOut po,
+    const unsigned *__restrict__ list) {
+  constexpr int BN = 384 - BG, CC = BN / 16;  // column chunks per tile
+  __shared__ float val[8][17];
+  const unsigned nitems = list[0] * 256u;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_g = (g.G + BG - 1) / BG;
+  for (unsigned it = blockIdx.x; it < nitems; it += gridDim.x) {
+    const int lid = (int)list[2 + it / 256], ch = (int)(it % 256);
+    const int g0 = (lid % tiles_g) * BG + (ch / CC) * 8;
+    const int64_t m0 = (int64_t)(lid / tiles_g) * BN + (int64_t)(ch % CC) * 16;
+    for (int e = wave; e < 128; e += 4) {
+      const int gg = g0 + (e >> 4);
+      const int64_t mm = m0 + (e & 15);
+      float v = 0.0f;
+      if (gg < g.G && mm < g.M) v = conv_dot(g, X, xs, Kw, ks, gg, mm, lane);
+      if (lane == 0) val[e >> 4][e & 15] = v;
+    }
+    __syncthreads();
+    if constexpr (POOL > 0) {
+      constexpr int PC = POOL == 1 ? 4 : POOL == 2 ? 1 : 2;
+      const int Q = g.P >> 1;
+      if (tid < 64) {  // window (8 / PC filter groups) x (8 column pairs)
+        const int wg = tid >> 3, wp = tid & 7;
+        const int gg0 = g0 + wg * PC;
+        const int64_t mm = m0 + 2 * wp;
+        if (wg < 8 / PC && gg0 < g.G && mm < g.M) {
+          uint32_t on, op;
+          g.div_P.divmod((uint32_t)mm, on, op);
+          float e0[PC], e1[PC];
+#pragma unroll
+          for (int c = 0; c < PC; c++) {
+            e0[c] = val[wg * PC + c][2 * wp];
+            e1[c] = val[wg * PC + c][2 * wp + 1];
+            if (bias) {
+              e0[c] = e0[c] + bias[gg0 + c];
+              e1[c] = e1[c] + bias[gg0 + c];
+            }
+            if (out) {
+              out[(int64_t)on * os + (int64_t)(gg0 + c) * g.P + op] = e0[c];
+              out[(int64_t)on * os + (int64_t)(gg0 + c) * g.P + op + 1] = e1[c];
+            }
+          }
+          float mx = -1e20f;
+#pragma unroll
+          for (int c = 0; c < PC; c++) {
+            if (mx < e0[c]) mx = e0[c];
+            if (mx < e1[c]) mx = e1[c];
+          }
+          unsigned mk = 0;
+#pragma unroll
+          for (int c = 0; c < PC; c++) {
+            mk |= (e0[c] == mx ? 1u : 0u) << (2 * c);
+            mk |= (e1[c] == mx ? 1u : 0u) << (2 * c + 1);
+          }
+          const int64_t q = (int64_t)(gg0 / PC) * Q + (op >> 1);
+          po.pool[(int64_t)on * po.ps + q] = mx;
+          po.mask[(int64_t)on * po.ms + q] = (unsigned short)mk;
+        }
+      }
+    } else if (tid < 128) {
+      const int gg = g0 + (tid >> 4);
+      const int64_t mm = m0 + (tid & 15);
+      if (gg < g.G && mm < g.M) {
+        uint32_t on, op;
+        g.div_P.divmod((uint32_t)mm, on, op);
+        float v = val[tid >> 4][tid & 15];
+        if (bias) v = v + bias[gg];
+        if (relu) v = v < 0.0f ? 0.0f : v;
+        out[(int64_t)on * os + (int64_t)gg * g.P + op] = v;
+      }
+    }
+    __syncthreads();  // val is rewritten by the next item
+  }
+}
+
+// The listed elements of the f16x3 form (F16Aux elist), one entry per wave:
+// the rejected element recomputed (conv_dot) and stored (+ bias, ReLU), or,
+// for the pooled epilogue, the window's rejected elements recomputed (+ bias)
+// and the window pooled again with the epilogue's order and compares.
+template <int POOL>
+__global__ __launch_bounds__(256) void conv_igemm_efix_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ Kw, int ks,
+    const float *__restrict__ bias, float *__restrict__ out, int os, int relu, PoolOut po,
+    const unsigned *__restrict__ list, const unsigned *__restrict__ elist) {
+  const unsigned n = list[1];
+  const int lane = threadIdx.x & 63;
+  const unsigned w0 = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  for (unsigned en = w0; en < n; en += nw) {
+    const unsigned *e = elist + (size_t)EW * en;
+    const int gg0 = (int)e[0];
+    const int64_t mm = (int64_t)e[1];
+    const unsigned bits = e[2];
+    uint32_t on, op;
+    g.div_P.divmod((uint32_t)mm, on, op);
+    if constexpr (POOL > 0) {
+      constexpr int PC = POOL == 1 ? 4 : POOL == 2 ? 1 : 2;
+      const int Q = g.P >> 1;
+      float v[2 * PC];
+#pragma unroll
+      for (int b = 0; b < 2 * PC; b++) {
+        v[b] = __uint_as_float(e[3 + b]);
+        if ((bits >> b) & 1u) {  // wave-uniform
+          const int gg = gg0 + (b >> 1);
+          float x = conv_dot(g, X, xs, Kw, ks, gg, mm + (b & 1), lane);
+          if (bias) x = x + bias[gg];
+          v[b] = x;
+          if (out && lane == 0) out[(int64_t)on * os + (int64_t)gg * g.P + op + (b & 1)] = x;
+        }
+      }
+      float mx = -1e20f;
+#pragma unroll
+      for (int c = 0; c < PC; c++) {
+        if (mx < v[2 * c]) mx = v[2 * c];
+        if (mx < v[2 * c + 1]) mx = v[2 * c + 1];
+      }
+      unsigned mk = 0;
+#pragma unroll
+      for (int c = 0; c < PC; c++) {
+        mk |= (v[2 * c] == mx ? 1u : 0u) << (2 * c);
+        mk |= (v[2 * c + 1] == mx ? 1u : 0u) << (2 * c + 1);
+      }
+      if (lane == 0) {
+        const int64_t q = (int64_t)(gg0 / PC) * Q + (op >> 1);
+        po.pool[(int64_t)on * po.ps + q] = mx;
+        po.mask[(int64_t)on * po.ms + q] = (unsigned short)mk;
+      }
+    } else {
+      float x = conv_dot(g, X, xs, Kw, ks, gg0, mm, lane);
+      if (bias) x = x + bias[gg0];
+      if (relu) x = x < 0.0f ? 0.0f : x;
+      if (lane == 0) out[(int64_t)on * os + (int64_t)gg0 * g.P + op] = x;
+    }
   }
 }
 
@@ -867,19 +1094,24 @@ void launch_t(const ConvGeom &g, unsigned blocks, const float *X, int xs, const 
   hipLaunchKernelGGL((conv_igemm_x6_kernel<BG, PADDED, STG, TAB, POOL, F16>), dim3(blocks),
                      dim3(NT), lds, st, g, X, xs, K, ks, bias, out, os, relu, po, fx);
 }
-// the bf16x6 form (redo: only the tiles the f16x3 form flagged), or the
-// f16x3 form then the bf16x6 redo of its flagged tiles
+// the bf16x6 form, or the f16x3 form and the fp32 fixup of its listed tiles
 template <int BG, bool PADDED, bool TAB, int POOL>
 void launch_pair(const ConvGeom &g, unsigned blocks, const float *X, int xs, const float *K,
                  int ks, const float *bias, float *out, int os, int relu, hipStream_t st,
                  PoolOut po, F16Aux fx) {
-  if (fx.tflag) {
-    launch_t<BG, PADDED, false, TAB, POOL, true>(g, blocks, X, xs, K, ks, bias, out, os, relu,
-                                                 st, po, fx);
-    fx.redo = fx.tflag;
+  if (!fx.list) {
+    launch_t<BG, PADDED, false, TAB, POOL, false>(g, blocks, X, xs, K, ks, bias, out, os, relu,
+                                                  st, po, fx);
+    return;
   }
-  launch_t<BG, PADDED, false, TAB, POOL, false>(g, blocks, X, xs, K, ks, bias, out, os, relu,
-                                                st, po, fx);
+  launch_t<BG, PADDED, false, TAB, POOL, true>(g, blocks, X, xs, K, ks, bias, out, os, relu,
+                                               st, po, fx);
+  hipLaunchKernelGGL((conv_igemm_fixup_kernel<BG, POOL>), dim3(std::min(blocks, 256u)),
+                     dim3(256), 0, st, g, X, xs, K, ks, bias, out, os, relu, po,
+                     (const unsigned *)fx.list);
+  hipLaunchKernelGGL((conv_igemm_efix_kernel<POOL>), dim3(64), dim3(256), 0, st, g, X, xs, K,
+                     ks, bias, out, os, relu, po, (const unsigned *)fx.list,
+                     (const unsigned *)fx.elist);
 }
 // pooled epilogue (POOL > 0): no stagger (the host declines it)
 template <int BG, bool PADDED, int POOL>
@@ -895,7 +1127,7 @@ template <int BG, bool PADDED>
 void launch(const ConvGeom &g, unsigned blocks, const float *X, int xs, const float *K, int ks,
             const float *bias, float *out, int os, int relu, F16Aux fx, hipStream_t st) {
   const bool tb = tab_bytes(g, PADDED) != 0;
-  if (stagger() && !fx.tflag) {
+  if (stagger() && !fx.list) {
     if (tb) launch_t<BG, PADDED, true, true, 0, false>(g, blocks, X, xs, K, ks, bias, out, os, relu, st, PoolOut{}, fx);
     else launch_t<BG, PADDED, true, false, 0, false>(g, blocks, X, xs, K, ks, bias, out, os, relu, st, PoolOut{}, fx);
     return;
@@ -918,37 +1150,44 @@ struct F16Setup {
       : ws(on ? words(g, blocks) * 4 : 0) {
     if (!on) return;
     uint32_t *w = static_cast<uint32_t *>(ws.p);
-    uint32_t *wst = w, *xst = wst + 3 * (size_t)g.G, *tflag = xst + 3 * (size_t)g.R,
-             *part = tflag + blocks;
-    rc = kl_absmax_rows_cols(X, g.R, g.HW * g.C, xs, xst, K, g.Kdim, g.G, ks, wst, part,
+    uint32_t *wst = w, *xst = wst + 3 * (size_t)g.G, *list = xst + 3 * (size_t)g.R,
+             *elist = list + 2 + blocks, *part = elist + elist_words(blocks);
+    rc = kl_absmax_rows_cols(X, g.R, g.HW * g.C, xs, xst, K, g.Kdim, g.G, ks, wst, part, list,
                              reinterpret_cast<kcnn_stream_t>(st));
     fx.wst = wst;
     fx.xst = xst;
-    fx.tflag = tflag;
+    fx.list = list;
+    fx.elist = elist;
   }
+  static size_t elist_words(unsigned blocks) { return (size_t)blocks * 8 * REJ_MAX * EW; }
   static size_t words(const ConvGeom &g, unsigned blocks) {
-    return 3 * (size_t)g.G + 3 * (size_t)g.R + blocks + kl_absmax_cols_words(g.Kdim, g.G);
+    return 3 * (size_t)g.G + 3 * (size_t)g.R + 2 + blocks + elist_words(blocks) +
+           kl_absmax_cols_words(g.Kdim, g.G);
   }
 };
-// f16x3 for the long kernels (c5's Kdim 768 / 2304); shorter ones (nnet.config's
-// 384 / 512) keep bf16x6: their few K steps do not repay the statistics pass
-// over X (measured: nnet.config's convolutions 2.06 -> 2.20 ms per step)
+// f16x3 for the large long-kernel convolutions (2 M G Kdim >= 2^34 flop and
+// Kdim >= 512: c5's C2 / C3 forward and C3 data gradient); the others keep
+// bf16x6.  nnet.config's layers (<= 8.6 Gflop): the statistics pass over X
+// and the few tiles do not repay it (its convolutions 2.06 -> 2.20 ms per
+// step with f16x3); c5's 1x1 data gradients (Kdim 256, 906 MB of output):
+// 8 K steps per tile, epilogue-bound (430 -> 800 us with f16x3)
+// (family value 3: f16x3 for every shape, the tests' setting)
 bool use_f16(const ConvGeom &g) {
-  static const int kmin = KCNN_KNOB("KCNN_IGF16_KMIN", 768);
-  return family(kFamIgemmX6) == 2 && g.R > 0 && g.Kdim >= kmin;
+  static const int lg = KCNN_KNOB("KCNN_IGF16_LOG2FLOP", 34);
+  const int f = family(kFamIgemmX6);
+  return g.R > 0 && (f == 3 || (f == 2 && g.Kdim >= 512 &&
+                                 2.0 * (double)g.M * g.G * g.Kdim >= (double)(1ull << lg)));
 }
-// experiment build: KCNN_IGF16_DEBUG=1 prints each call's flagged tiles
+// experiment build: KCNN_IGF16_DEBUG=1 prints each call's recomputed tiles
 void report_flags(const F16Aux &fx, unsigned nb, const ConvGeom &g, hipStream_t st) {
   static const int dbg = KCNN_KNOB("KCNN_IGF16_DEBUG", 0);
-  if (!dbg || !fx.tflag) return;
-  std::vector<unsigned> f(nb);
-  if (hipMemcpyAsync(f.data(), fx.tflag, nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+  if (!dbg || !fx.list) return;
+  unsigned n[2] = {0, 0};
+  if (hipMemcpyAsync(n, fx.list, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return;
-  unsigned n = 0;
-  for (unsigned v : f) n += v != 0;
-  fprintf(stderr, "igemm f16x3: G %d Kdim %d M %lld: %u of %u tiles recomputed\n", g.G, g.Kdim,
-          (long long)g.M, n, nb);
+  fprintf(stderr, "igemm f16x3: G %d Kdim %d M %lld: %u of %u tiles, %u elements recomputed\n",
+          g.G, g.Kdim, (long long)g.M, n[0], nb, n[1]);
 }
 
 }  // namespace
@@ -989,6 +1228,8 @@ int kcnn_conv_igemm_x6(const ConvGeom &g, const float *X, int xs, const float *K
     else launch<256, false>(g, nb, X, xs, K, ks, bias, out, os, relu, fs.fx, st);
   }
   report_flags(fs.fx, nb, g, st);
+  if (!f16 && KCNN_KNOB("KCNN_IGF16_DEBUG", 0))
+    fprintf(stderr, "igemm bf16x6: G %d Kdim %d M %lld relu %d\n", g.G, g.Kdim, (long long)g.M, relu);
   return (int)hipGetLastError();
 }
 

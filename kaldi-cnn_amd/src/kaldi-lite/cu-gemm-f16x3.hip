@@ -939,6 +939,7 @@ struct StatOp {
   int rpb;         // mode 0: rows per block (4: a wave each; 1: a block)
   int cb, rbk, rb; // mode 1: column blocks, row chunks, rows per chunk
   int fblocks;     // mode 1: blocks of stats_finalize_kernel
+  uint32_t *clear; // nullable: two words stats_kernel sets to 0 (a consumer's counters)
 };
 __device__ __forceinline__ const float *X_row(const StatOp &o, int r) {
   return o.X + (int64_t)r * o.ld;
@@ -1107,6 +1108,7 @@ __device__ __forceinline__ void stats_cols(const StatOp &o, int blk) {
 
 __global__ __launch_bounds__(256) void stats_kernel(StatOp a, StatOp b) {
   __shared__ uint32_t red[12];
+  if (a.clear && blockIdx.x == 0 && threadIdx.x < 2) a.clear[threadIdx.x] = 0u;
   const bool isa = (int)blockIdx.x < a.blocks;  // uniform
   const StatOp &o = isa ? a : b;
   const int blk = isa ? blockIdx.x : blockIdx.x - a.blocks;
@@ -1604,16 +1606,23 @@ extern "C" int kl_absmax_cols(const float *X, int rows, int cols, int ld, uint32
 // kl_absmax_rows of R (rows x cols, pitch ld) and kl_absmax_cols of Q
 // (qrows x qcols, pitch ldq; part: kl_absmax_cols_words) in one statistics
 // launch (and Q's finalize / count passes): the f16x3 implicit GEMM's frame
-// and filter statistics (cnsl-conv-igemm-x6.hip)
+// and filter statistics (cnsl-conv-igemm-x6.hip); clear (nullable): two
+// words set to 0 by the same launch (that kernel's list counters)
 extern "C" int kl_absmax_rows_cols(const float *R, int rows, int cols, int ld, uint32_t *rmax,
                                    const float *Q, int qrows, int qcols, int ldq, uint32_t *cmax,
-                                   uint32_t *part, kcnn_stream_t stream) {
+                                   uint32_t *part, uint32_t *clear, kcnn_stream_t stream) {
   if (rows < 0 || cols < 0 || ld < cols || !rmax || qrows < 0 || qcols < 0 || ldq < qcols ||
       !cmax)
     return (int)hipErrorInvalidValue;
   if (qrows > 0 && qcols > 0 && !part) return (int)hipErrorInvalidValue;
-  return stats_launch(stat_op(Q, qrows, qcols, ldq, 1, cmax, part),
-                      stat_op(R, rows, cols, ld, 0, rmax, nullptr), kcnn::as_stream(stream));
+  StatOp q = stat_op(Q, qrows, qcols, ldq, 1, cmax, part);
+  q.clear = clear;
+  const StatOp r = stat_op(R, rows, cols, ld, 0, rmax, nullptr);
+  if (clear && q.blocks + r.blocks == 0) {  // no statistics launch to clear it
+    const hipError_t e = hipMemsetAsync(clear, 0, 8, kcnn::as_stream(stream));
+    if (e != hipSuccess) return (int)e;
+  }
+  return stats_launch(q, r, kcnn::as_stream(stream));
 }
 
 // C[M x N] = alpha * op(A) op(B) + beta * C with the operands' max |x| given:

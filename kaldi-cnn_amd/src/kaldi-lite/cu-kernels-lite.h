@@ -43,10 +43,11 @@ size_t kl_absmax_cols_words(int rows, int cols);
 int kl_absmax_cols(const float *X, int rows, int cols, int ld, uint32_t *cmax, uint32_t *part,
                    kcnn_stream_t st);
 /* kl_absmax_rows of R and kl_absmax_cols of Q (part: kl_absmax_cols_words
-   of Q's shape) in one statistics launch */
+   of Q's shape) in one statistics launch, which also sets clear[0] and
+   clear[1] to 0 (nullable) */
 int kl_absmax_rows_cols(const float *R, int rows, int cols, int ld, uint32_t *rmax,
                         const float *Q, int qrows, int qcols, int ldq, uint32_t *cmax,
-                        uint32_t *part, kcnn_stream_t stream);
+                        uint32_t *part, uint32_t *clear, kcnn_stream_t stream);
 size_t kl_gemm_f16x3_workspace_bytes(int M, int N, int K);
 int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alpha,
                      const float *A, int lda, const float *B, int ldb, float beta, float *C,

@@ -1,18 +1,19 @@
-"""The f16x3 implicit GEMM (cnsl-conv-igemm-x6.hip, igemm_x6 family 2, the
-default for the long-kernel convolutions: c5 C2-C4 forward and data
-gradient, nnet.config's convolutions).
+"""The f16x3 implicit GEMM (cnsl-conv-igemm-x6.hip; igemm_x6 family 2, the
+default, takes it for convolutions of at least 2^34 flop -- c5's C2 / C3
+forward and data gradients -- and family 3, set here, for every shape).
 
 Scale groups (f16-split.h): one per filter (a column of W over every k) and
 one per frame of the input (every im2col column reads one frame).  A tile
 whose groups hold Inf / NaN, or one of whose products the store check cannot
-clear (a spread group's small elements carrying the sum), is recomputed by
-the bf16x6 form of the same kernel, so:
+clear (a spread group's small elements carrying the sum), is recomputed as
+fp32 dot products by conv_igemm_fixup_kernel, so:
   * ordinary data meets the parity bar (1e-5 * S elementwise,
     1e-5 normwise) against the oracle;
   * a group spread over 2^24 ... 2^32 whose largest element meets zeros
     still meets the elementwise bar (the f16x3 products alone miss it by
     up to 50x: VERDICT r04 item 1's model);
-  * frames with Inf / NaN give the bf16x6 kernel's bits.
+  * frames with Inf / NaN give the reference's IEEE pattern (the listed
+    tiles are recomputed as fp32 dot products).
 Reference: CuMatrixBase::Conv2D (src/cnslmat/conv2D.cc:43-201) and
 ConvolutionComponent::Propagate / Backprop (src/nnet0/nnet-component-nnet0.cc:
 423-446, 461-544).
@@ -21,7 +22,8 @@ import numpy as np
 import pytest
 
 from _util import assert_bound, assert_same, dev, host, randn, rng, triple
-from test_gpu_components import make_pair
+from test_gpu_components import conv_line, make_pair
+from test_gpu_fwd_f16 import check_pattern, nonfinite_inputs
 
 pytestmark = pytest.mark.gpu
 
@@ -44,7 +46,7 @@ def fam(kc):
 @pytest.mark.parametrize("cfg", [C5_C2, C5_C3, C5_C4, NNET_L2],
                          ids=["c5_C2", "c5_C3", "c5_C4", "G128"])
 def test_igemm_f16_parity(kc, fam, cfg):
-    fam(2)
+    fam(3)
     H, W, C, kh, kw, G, ph, pw = cfg
     comp, oc = make_pair(kc, cfg, seed=7 + C)
     r = rng(3 + G)
@@ -67,7 +69,7 @@ def test_igemm_intra_group_range(kc, fam, group, spread):
     N(0,1) * 2^-spread, X's channel 0 is 0; "frame": X's channel 0 is 1 (the
     frame's largest values), the other channels N(0,1) * 2^-spread, W's
     channel-0 taps 0."""
-    fam(2)
+    fam(3)
     H, W, C, kh, kw, G, ph, pw = C5_C3
     comp, oc = make_pair(kc, C5_C3, seed=43)
     r = rng(44 + spread)
@@ -92,35 +94,78 @@ def test_igemm_intra_group_range(kc, fam, group, spread):
     assert_bound(host(comp.Propagate(dev(x))), y_t, y_s, what=f"{group} spread 2^{spread}")
 
 
-def test_igemm_nonfinite_frames_take_bf16x6(kc, fam):
-    """Frames holding Inf / NaN have no scale: their tiles are recomputed by
-    the bf16x6 form, so those frames' outputs are bitwise the bf16x6 kernel's
-    (family 1), and the other frames stay within the bar."""
-    H, W, C, kh, kw, G, ph, pw = C5_C3
-    comp, oc = make_pair(kc, C5_C3, seed=5)
+@pytest.mark.parametrize("cfg", [C5_C3, C5_C2], ids=["c5_C3", "c5_C2"])
+def test_igemm_nonfinite_frames(kc, fam, cfg):
+    """Frames holding Inf / NaN have no scale: their tiles are recomputed as
+    fp32 dot products (conv_igemm_fixup_kernel), which gives the reference's
+    IEEE pattern (+Inf, -Inf, NaN) where its result is not finite and the bar
+    elsewhere; the Conv -> Maxpool fusion (c5 C3 -> P2) goes through the same
+    fixup's pooling."""
+    fam(3)
+    H, W, C, kh, kw, G, ph, pw = cfg
+    comp, oc = make_pair(kc, cfg, seed=5)
     r = rng(9)
-    N = 12
-    x = randn(r, (N, H * W * C))
-    x[3, 100] = np.inf
-    x[7, 5000] = np.nan
-    xd = dev(x)
-    fam(1)
-    y1 = host(comp.Propagate(xd))
-    fam(2)
-    y2 = host(comp.Propagate(xd))
-    for n in (3, 7):
-        assert_same(y2[n], y1[n], f"frame {n}")
-    ok = [n for n in range(N) if n not in (3, 7)]
-    _, y_t, y_s = triple(lambda: oc.propagate(x[ok]))
-    assert_bound(y2[ok], y_t, y_s, what="finite frames")
+    x = nonfinite_inputs(r, 8, H * W * C)
+    y_ref, y_t, y_s = triple(lambda: oc.propagate(x))
+    check_pattern(host(comp.Propagate(dev(x))), y_ref, y_t, y_s, "igemm f16x3 non-finite")
+
+
+def test_igemm_nonfinite_pooled(kc, fam):
+    """c5's C3 with its P2 pool in the implicit GEMM's epilogue (and the
+    fixup's pooling) against the unfused pair on non-finite frames: bitwise."""
+    fam(3)
+    H, W, C, kh, kw, G, ph, pw = C5_C3
+    oh, ow = H + 2 * ph - kh + 1, W + 2 * pw - kw + 1
+    cfg = "\n".join([conv_line(*C5_C3),
+                     f"MaxpoolComponent in-height={oh} in-width={ow} in-channel={G} "
+                     f"pool-height-dim=2 pool-width-dim=1 pool-channel-dim=4"])
+    x = dev(nonfinite_inputs(rng(10), 8, H * W * C))
+    outs = []
+    for fuse in (True, False):
+        kc.set_fusion(fuse)
+        try:
+            net = kc.Nnet(cfg)
+            conv = net.components[0]
+            conv.SetParam(kc.PARAM_LINEAR, dev(randn(rng(11), (kh * kw * C, G), 0.05)))
+            conv.SetParam(kc.PARAM_BIAS, dev(randn(rng(12), (G,), 0.5)))
+            net.Propagate(x)
+            outs.append(host(net.Output()))
+        finally:
+            kc.set_fusion(True)
+    assert_same(outs[0], outs[1], "fused vs unfused")
 
 
 def test_igemm_f16_repeat_bitwise(kc, fam):
-    """Repeated calls on one input give the same bits (tile flags, redo)."""
-    fam(2)
+    """Repeated calls on one input give the same bits (tile list, fixup)."""
+    fam(3)
     comp, _ = make_pair(kc, C5_C3, seed=11)
     H, W, C = C5_C3[:3]
     x = dev(randn(rng(12), (301, H * W * C)))
     y0 = host(comp.Propagate(x))
     for rep in range(4):
         assert_same(host(comp.Propagate(x)), y0, f"repeat {rep}")
+
+
+@pytest.mark.parametrize("kind", ["huge_x", "huge_dy", "tiny_x", "tiny_dy"])
+def test_igemm_f16_fp32_range(kc, fam, kind):
+    """The edges of fp32 (test_gpu_x6_range's operands: values up to 3.4e38,
+    or scaled by 2^-120) through the f16x3 forward and data gradient at the
+    full bar: the scales put every group into f16's range, and the frames
+    whose spread the check cannot clear are recomputed in fp32."""
+    from test_gpu_x6_range import scaled_inputs
+    fam(3)
+    H, W, C, kh, kw, G, ph, pw = C5_C3
+    comp, oc = make_pair(kc, C5_C3, seed=3)
+    if kind.startswith("huge"):
+        oc.W = (oc.W * 1e-3).astype(np.float32)
+        comp.SetParam(kc.PARAM_LINEAR, dev(oc.W))
+    r = rng(41)
+    N = 5
+    oh, ow = H + 2 * ph - kh + 1, W + 2 * pw - kw + 1
+    x, dy = scaled_inputs(kind, r, N, H * W * C, oh * ow * G, G)
+    if kind in ("huge_x", "tiny_x"):
+        _, y_t, y_s = triple(lambda: oc.propagate(x))
+        assert_bound(host(comp.Propagate(dev(x))), y_t, y_s, what=f"{kind} Propagate")
+    _, dx_t, dx_s = triple(lambda: oc.backprop(x, dy, update=False))
+    dx = comp.Backprop(dev(x), None, dev(dy), update=False)
+    assert_bound(host(dx), dx_t, dx_s, what=f"{kind} dX")

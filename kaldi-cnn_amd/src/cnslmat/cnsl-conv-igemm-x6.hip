@@ -1165,18 +1165,17 @@ struct F16Setup {
            kl_absmax_cols_words(g.Kdim, g.G);
   }
 };
-// f16x3 for the large long-kernel convolutions (2 M G Kdim >= 2^34 flop and
-// Kdim >= 512: c5's C2 / C3 forward and C3 data gradient); the others keep
+// f16x3 for the large convolutions (2 M G Kdim >= 2^34 flop: c5's C2 / C3
+// forward, C3 data gradient and C2's 1x1 data gradient); the others keep
 // bf16x6.  nnet.config's layers (<= 8.6 Gflop): the statistics pass over X
 // and the few tiles do not repay it (its convolutions 2.06 -> 2.20 ms per
-// step with f16x3); c5's 1x1 data gradients (Kdim 256, 906 MB of output):
-// 8 K steps per tile, epilogue-bound (430 -> 800 us with f16x3)
+// step with f16x3)
 // (family value 3: f16x3 for every shape, the tests' setting)
 bool use_f16(const ConvGeom &g) {
   static const int lg = KCNN_KNOB("KCNN_IGF16_LOG2FLOP", 34);
   const int f = family(kFamIgemmX6);
-  return g.R > 0 && (f == 3 || (f == 2 && g.Kdim >= 512 &&
-                                 2.0 * (double)g.M * g.G * g.Kdim >= (double)(1ull << lg)));
+  return g.R > 0 && (f == 3 || (f == 2 && 2.0 * (double)g.M * g.G * g.Kdim >=
+                                              (double)(1ull << lg)));
 }
 // experiment build: KCNN_IGF16_DEBUG=1 prints each call's recomputed tiles
 void report_flags(const F16Aux &fx, unsigned nb, const ConvGeom &g, hipStream_t st) {

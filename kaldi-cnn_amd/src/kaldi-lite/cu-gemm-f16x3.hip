@@ -973,10 +973,12 @@ __device__ __forceinline__ uint32_t count_small_row(const StatOp &o, const float
   return n;
 }
 
-// A row held in registers by the sweep (RV float4 per thread: up to 12288
-// floats per block row, 3072 per wave row), so that a spread row counts its
-// small elements without a second read
-constexpr int RV = 12;
+// A row held in registers by the sweep (RV float4 per thread: up to 18432
+// floats per block row, 4608 per wave row), so that a spread row counts its
+// small elements without a second read (c5's C3 input and output derivative
+// rows are 18432 floats, and the derivative's frames are all spread: a
+// second read doubled that pass, 83 us per call)
+constexpr int RV = 18;
 __device__ __forceinline__ void stats_rows(const StatOp &o, int blk, uint32_t *red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool wide = o.rpb == 1;

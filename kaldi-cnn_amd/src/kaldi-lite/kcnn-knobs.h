@@ -10,7 +10,7 @@
 //   family     env              values
 //   fwd_x6     KCNN_FWD_X6      2 f16x3 frame-resident forward, 1 bf16x6, 0 fp32 MFMA
 //   bwd_x6     KCNN_BWD_X6      1 bf16x6 fused backward, 0 fp32 MFMA
-//   igemm_x6   KCNN_IGEMM_X6    2 f16x3 implicit GEMM for convolutions of >= 2^34 flop, Kdim >= 512 (bf16x6
+//   igemm_x6   KCNN_IGEMM_X6    2 f16x3 implicit GEMM for convolutions of >= 2^34 flop (bf16x6
 //                               below), 3 f16x3 for all, 1 bf16x6, 0 fp32 MFMA
 //   wgrad_x6   KCNN_WGRAD_X6    2 wide bf16x6, 1 128-wide bf16x6, 0 fp32 MFMA
 //   gemm       KCNN_GEMM        2 f16x3 GEMM (AddMatMat), 1 bf16x6 GEMM, 0 rocBLAS sgemm

@@ -692,10 +692,28 @@ def main():
             el = float(t.item())
         return el, pr
 
+    # the parameters after the warm-up, restored before the profiled pass: the
+    # synthetic output derivative is the same every step, so the parameters
+    # drift one way and nnet.config's four FC layers overflow after a few
+    # dozen steps (Inf / NaN operands then take the f16x3 kernels' fp32 paths,
+    # and its profiled pass measured 630 ms per step); restored, both passes
+    # run from the same state (outside the timed regions)
+    snap = []
+    for comp in net.components:
+        for which in (kcnn.PARAM_LINEAR, kcnn.PARAM_BIAS, kcnn.PARAM_PREV_GRAD):
+            try:
+                snap.append((comp, which, comp.GetParam(which).clone()))
+            except Exception:  # noqa: BLE001 -- a component without that parameter
+                pass
+    torch.cuda.synchronize()
+
     # headline: profiling off (no events in the stream); then the same K steps
     # again with hipEvents around every component scope, for the per-kernel
     # times of the roofline
     elapsed, _ = timed(False)
+    for comp, which, v in snap:
+        comp.SetParam(which, v)
+    torch.cuda.synchronize()
     profiling_dp = True
     elapsed_prof, prof = timed(True)
     profiling_dp = False

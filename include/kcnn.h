@@ -90,7 +90,9 @@ int kcnn_set_gemm_mode(int mode);
  * products) or the fp32-input MFMA kernels (0).
  *   "fwd_x6"   frame-resident conv forward      2 (default, f16x3) / 1 / 0
  *   "bwd_x6"   fused conv backward              1 (default) / 0
- *   "igemm_x6" implicit-GEMM forward and dgrad  1 (default) / 0
+ *   "igemm_x6" implicit-GEMM forward and dgrad  2 (default: f16x3 for
+ *              convolutions of >= 2^34 flop, bf16x6 below) / 3 (f16x3 for
+ *              all) / 1 (bf16x6) / 0
  *   "wgrad_x6" long-kernel weight gradient      2 (default, wide) / 1 / 0
  *   "gemm"     AddMatMat (= kcnn_set_gemm_mode) 2 (default, f16x3) / 1 / 0
  * The environment variables KCNN_FWD_X6, KCNN_BWD_X6, KCNN_IGEMM_X6,

@@ -2,7 +2,11 @@
 // long-kernel layers (BASELINE c5 C2-C4, every conv of the reference's
 // egs/exp/nnet/nnet.config, and the flipped-kernel / 1x1 data gradients) on
 // the bf16 matrix cores, with every fp32 operand split exactly into three
-// bf16 parts and the six leading cross products kept (x6-util.h).
+// bf16 parts and the six leading cross products kept (x6-util.h), or, for
+// the large shapes (F16 below, igemm_x6 family 2 / 3), on the f16 matrix
+// cores with two f16 parts under a power-of-two scale per filter and per
+// frame and three products (f16-split.h), checked at the store and fixed up
+// in fp32 where the scale cannot hold a product to the per-element bar.
 //
 // Reference: CuMatrixBase::Conv2D (conv2D.cc:43-201) = im2col span (:105,
 // _span_row_to_convmat) + cuBLAS GEMM (:138-139) + _convmat_to_out (:181) +

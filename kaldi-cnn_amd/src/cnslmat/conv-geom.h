@@ -83,8 +83,9 @@ int kcnn_conv_bwd_x6(const kcnn::ConvGeom &g, const float *X, int xs, const floa
                      int dys, const float *K, int ks, float *dX, int dxs, float *ws_part,
                      int S, int dx_acc, hipStream_t st, const unsigned char *pmask,
                      int pms, int pc, int ph, int dbg = 0);
-// Conv2D(concat) + bias (+ ReLU when relu) as an implicit GEMM on the bf16
-// MFMAs (cnsl-conv-igemm-x6.hip); -1 when the shape is outside its limits.
+// Conv2D(concat) + bias (+ ReLU when relu) as an implicit GEMM on the f16
+// (f16x3, igemm_x6 family 2 / 3) or bf16 (bf16x6) MFMAs
+// (cnsl-conv-igemm-x6.hip); -1 when the shape is outside its limits.
 int kcnn_conv_igemm_x6(const kcnn::ConvGeom &g, const float *X, int xs, const float *K,
                        int ks, const float *bias, float *out, int os, int relu,
                        hipStream_t st);

@@ -105,6 +105,10 @@ def test_kernel_family_selectors():
         assert kcnn.get_kernel_family("wgrad_x6") == 1
         kcnn.set_kernel_family("gemm", 0)
         assert kcnn.get_kernel_family("gemm") == 0
+        kcnn.set_kernel_family("igemm_x6", 3)  # f16x3 for every shape
+        assert kcnn.get_kernel_family("igemm_x6") == 3
+        with pytest.raises(kcnn.KcnnError, match="out of range"):
+            kcnn.set_kernel_family("igemm_x6", 4)
         with pytest.raises(kcnn.KcnnError, match="out of range"):
             kcnn.set_kernel_family("bwd_x6", 2)
         with pytest.raises(kcnn.KcnnError, match="unknown"):

@@ -93,7 +93,8 @@ int kcnn_set_gemm_mode(int mode);
  *   "igemm_x6" implicit-GEMM forward and dgrad  2 (default: f16x3 for
  *              convolutions of >= 2^34 flop, bf16x6 below) / 3 (f16x3 for
  *              all) / 1 (bf16x6) / 0
- *   "wgrad_x6" long-kernel weight gradient      2 (default, wide) / 1 / 0
+ *   "wgrad_x6" long-kernel weight gradient      2 (default, wide bf16x6) / 3
+ *              (wide f16x3) / 1 (128-wide bf16x6) / 0
  *   "gemm"     AddMatMat (= kcnn_set_gemm_mode) 2 (default, f16x3) / 1 / 0
  * The environment variables KCNN_FWD_X6, KCNN_BWD_X6, KCNN_IGEMM_X6,
  * KCNN_WGRAD_X6 and KCNN_GEMM set the initial values.  Returns nonzero for

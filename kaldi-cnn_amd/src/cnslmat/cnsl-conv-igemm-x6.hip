@@ -903,16 +903,39 @@ __device__ __forceinline__ int swz32(int r, int c) {
   return r * WROW + ((c ^ ((r >> 3) & 1)) << 4);
 }
 
-template <bool PADDED>
+// The f16x3 form of the wide weight gradient (F16, wgrad_x6 family 3; not
+// the default: on c5 it measured slower than the bf16x6 form): scale groups over the whole batch -- a filter g
+// (dY's columns g*P .. g*P + P - 1 of every frame) and an input channel c (X's
+// columns c*HW .. c*HW + HW - 1 of every frame, a superset of every tap of
+// that channel) -- from wgrad_group_stats_kernel.  A split's partial of
+// (g, k) is checked like the implicit GEMM's store; a rejected one is listed
+// (elist: split, g, k) and recomputed over the split's frames in fp32
+// (conv_wgrad_efix_kernel); a block with an Inf / NaN group or a wave of
+// more than REJ_MAX rejections flags itself (flags[bid]) and the bf16x6 form
+// then recomputes exactly the flagged blocks (redo).
+struct WF16 {
+  const uint32_t *gst;   // [max G][min G][cnt G] of dY's filter groups
+  const uint32_t *cst;   // [max C][min C][cnt C] of X's channel groups
+  unsigned *flags;       // F16: per block, 1 = recompute on bf16x6
+  const unsigned *redo;  // bf16x6 form: non-null = only the flagged blocks
+  unsigned *list;        // [element count]
+  unsigned *elist;       // entries (split, g, k)
+};
+
+template <bool PADDED, bool F16>
 __global__ __launch_bounds__(NT, 1) void conv_wgrad_x6w_kernel(
     ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ dY, int dys,
-    float *__restrict__ ws, int fps, int ktiles, int nblocks) {
+    float *__restrict__ ws, int fps, int ktiles, int nblocks, WF16 wf) {
   constexpr int BG = 256, BN = 256, BT = 16;
-  constexpr int PLA = BG * WROW, PLB = BN * WROW, BUF = 3 * (PLA + PLB);
+  constexpr int NPL = F16 ? 2 : 3;
+  constexpr int PLA = BG * WROW, PLB = BN * WROW, BUF = NPL * (PLA + PLB);
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int nb8 = (nblocks + 7) >> 3;
   const int bid = (int)(blockIdx.x & 7) * nb8 + (int)(blockIdx.x >> 3);
   if (bid >= nblocks) return;  // whole workgroup: no barrier is skipped
+  if constexpr (!F16) {
+    if (wf.redo && wf.redo[bid] == 0) return;  // (uniform) the f16x3 partial stands
+  }
   const int ntiles = ktiles * ((g.G + BG - 1) / BG);
   const int split = bid / ntiles, tile = bid - split * ntiles;
   const int k0 = (tile % ktiles) * BN, g0 = (tile / ktiles) * BG;
@@ -944,6 +967,43 @@ __global__ __launch_bounds__(NT, 1) void conv_wgrad_x6w_kernel(
     if (PADDED) { tkx[j] = (int)kx - g.pad_w; tky[j] = (int)ky - g.pad_h; }
   }
   const int nsteps = (nf * g.P + BT - 1) / BT;
+
+  // F16: scale exponents / check weights of the block's 256 filters (sx[0,
+  // 256)) and 256 k columns (sx[256, 512), by their channel) in LDS past the
+  // images; a block with an Inf / NaN group is flagged for the bf16x6 form
+  int *sx = reinterpret_cast<int *>(lds + 2 * BUF);
+  float *swt = reinterpret_cast<float *>(sx + 512);
+  int ea[4] = {0, 0, 0, 0}, eb[4] = {0, 0, 0, 0};
+  if constexpr (F16) {
+    uint32_t mx = 0, cnt = 0;
+    bool in = false;
+    if (tid < 256) {
+      const int gg = g0 + tid;
+      if (gg < g.G) { in = true; mx = wf.gst[gg]; cnt = wf.gst[2 * g.G + gg]; }
+    } else {
+      const int k = k0 + tid - 256;
+      if (k < g.Kdim) {
+        uint32_t c, rr;
+        g.div_khkw.divmod((uint32_t)k, c, rr);
+        in = true;
+        mx = wf.cst[c];
+        cnt = wf.cst[2 * g.C + c];
+      }
+    }
+    const int e = in ? f16x3::scale_exp(mx) : 0;
+    const bool bad = e == f16x3::SKIP;
+    sx[tid] = bad ? 0 : e;
+    swt[tid] = in && mx != 0 ? f16x3::spread_weight(cnt) : -__builtin_inff();
+    if (__syncthreads_or(bad)) {
+      if (tid == 0) wf.flags[bid] = 1u;
+      return;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      ea[j] = sx[r + 64 * j];
+      eb[j] = sx[256 + r + 64 * j];
+    }
+  }
 
   float av[4][2], bv[4][2], bsum[4];
 #pragma unroll
@@ -981,7 +1041,29 @@ __global__ __launch_bounds__(NT, 1) void conv_wgrad_x6w_kernel(
     }
   };
   const int tc = tp >> 2, tb = (tp & 3) * 4;  // pair (2tp, 2tp+1): chunk, byte
+  const float m1 = F16 ? f16x3::opaque_m1() : -1.0f;
   auto store = [&](char *buf) {
+    if constexpr (F16) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        uint32_t hh, ll;
+        f16x3::split2h(av[j][0], av[j][1], ea[j], ea[j], hh, ll, m1);
+        const int o = swz32(r + 64 * j, tc) + tb;
+        *reinterpret_cast<uint32_t *>(buf + o) = hh;
+        *reinterpret_cast<uint32_t *>(buf + PLA + o) = ll;
+        if (do_bias) bsum[j] += av[j][0] + av[j][1];
+      }
+      char *bb = buf + 2 * PLA;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        uint32_t hh, ll;
+        f16x3::split2h(bv[j][0], bv[j][1], eb[j], eb[j], hh, ll, m1);
+        const int o = swz32(r + 64 * j, tc) + tb;
+        *reinterpret_cast<uint32_t *>(bb + o) = hh;
+        *reinterpret_cast<uint32_t *>(bb + PLB + o) = ll;
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       uint32_t hh, mm, ll;
@@ -1015,6 +1097,31 @@ __global__ __launch_bounds__(NT, 1) void conv_wgrad_x6w_kernel(
   if (nsteps > 1) load(1);
   const int arow = wm * 64 + l, brow = wn * 128 + l;
   for (int t = 0; t < nsteps; t++) {
+    if constexpr (F16) {
+      const char *bufA = lds + (t & 1) * BUF;
+      const char *bufB = bufA + 2 * PLA;
+      f16x3::f16x8 a[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int pl = 0; pl < 2; pl++)
+          a[i][pl] = *reinterpret_cast<const f16x3::f16x8 *>(bufA + pl * PLA + swz32(arow + 32 * i, h));
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        f16x3::f16x8 bb[2];
+#pragma unroll
+        for (int pl = 0; pl < 2; pl++)
+          bb[pl] = *reinterpret_cast<const f16x3::f16x8 *>(bufB + pl * PLB + swz32(brow + 32 * j, h));
+#pragma unroll
+        for (int i = 0; i < 2; i++) acc[i][j] = f16x3::mfma3(a[i][0], a[i][1], bb[0], bb[1], acc[i][j]);
+      }
+      if (t + 1 < nsteps) {
+        store(lds + ((t + 1) & 1) * BUF);
+        if (t + 2 < nsteps) load(t + 2);
+      }
+      __syncthreads();
+      continue;
+    }
     const char *bufA = lds + (t & 1) * BUF;
     const char *bufB = bufA + 3 * PLA;
     x6::bf16x8 a[2][3];
@@ -1041,6 +1148,30 @@ __global__ __launch_bounds__(NT, 1) void conv_wgrad_x6w_kernel(
 
   const int64_t E = (int64_t)g.G * g.Kdim + g.G;
   float *wsp = ws + (int64_t)split * E;
+  uint64_t rej[2] = {0, 0};  // F16: bit 16 j + q of word i
+  if constexpr (F16) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int kl = 256 + wn * 128 + 32 * j + l;
+      const int ec = sx[kl];
+      const float wc = swt[kl];
+#pragma unroll
+      for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+          const int gl = wm * 64 + 32 * i + mfma32_row(q, lane);
+          const float v = acc[i][j][q];
+          if (fabsf(v) < swt[gl] + wc) rej[i] |= 1ull << (16 * j + q);
+          acc[i][j][q] = __builtin_amdgcn_ldexpf(v, -(sx[gl] + ec));
+        }
+    }
+    int nrej = __builtin_popcountll(rej[0]) + __builtin_popcountll(rej[1]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) nrej += __shfl_xor(nrej, d);
+    const int f = __syncthreads_or(nrej > REJ_MAX);
+    if (tid == 0) wf.flags[bid] = f ? 1u : 0u;
+    if (f) return;
+  }
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const int kk = k0 + wn * 128 + 32 * j + l;
@@ -1053,6 +1184,22 @@ __global__ __launch_bounds__(NT, 1) void conv_wgrad_x6w_kernel(
         if (gg < g.G) wsp[(int64_t)gg * g.Kdim + kk] = acc[i][j][q];
       }
   }
+  if constexpr (F16) {
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+      while (rej[i]) {  // (rare) this lane's rejected partials, listed
+        const int b = __builtin_ctzll(rej[i]);
+        rej[i] &= rej[i] - 1;
+        const int j = b >> 4, q = b & 15;
+        const int gg = g0 + wm * 64 + 32 * i + mfma32_row(q, lane);
+        const int kk = k0 + wn * 128 + 32 * j + l;
+        if (gg >= g.G || kk >= g.Kdim) continue;
+        unsigned *e = wf.elist + 3 * (size_t)atomicAdd(wf.list, 1u);
+        e[0] = (unsigned)split;
+        e[1] = (unsigned)gg;
+        e[2] = (unsigned)kk;
+      }
+  }
   if (do_bias) {
     float *red = reinterpret_cast<float *>(lds);  // [256][9]
 #pragma unroll
@@ -1063,6 +1210,116 @@ __global__ __launch_bounds__(NT, 1) void conv_wgrad_x6w_kernel(
       for (int i = 0; i < 8; i++) sum += red[tid * 9 + i];
       wsp[(int64_t)g.G * g.Kdim + g0 + tid] = sum;
     }
+  }
+}
+
+// Scale-group statistics of the f16x3 weight gradient: op 0 = dY's filter
+// groups (gw = P contiguous columns per group, G groups), op 1 = X's channel
+// groups (gw = HW, C groups), every frame.  Block (group, row chunk);
+// pass 0: max |x| and min nonzero |x| (bit patterns, atomicMax / atomicMin:
+// order-independent), pass 1: for a spread group (f16-split.h) the count of
+// its nonzero elements under small_bound (integer atomics).  out: [max n]
+// [min n (0xffffffff: none)][cnt n]; wgrad_group_init_kernel sets them (and
+// the element list's counter) first.
+struct GStatOp {
+  const float *A;
+  int rows, ld, gw, n, rchunks;
+  uint32_t *out;
+};
+__global__ __launch_bounds__(256) void wgrad_group_init_kernel(GStatOp a, GStatOp b,
+                                                               unsigned *counter) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i == 0) *counter = 0u;
+  for (const GStatOp *o : {&a, &b})
+    if (i < o->n) {
+      o->out[i] = 0u;
+      o->out[o->n + i] = 0xffffffffu;
+      o->out[2 * o->n + i] = 0u;
+    }
+}
+__global__ __launch_bounds__(256) void wgrad_group_stats_kernel(GStatOp a, GStatOp b, int pass) {
+  __shared__ uint32_t red[2][4];
+  const int na = a.n * a.rchunks;
+  const bool isa = (int)blockIdx.x < na;
+  const GStatOp &o = isa ? a : b;
+  const int blk = isa ? blockIdx.x : blockIdx.x - na;
+  const int grp = blk % o.n, rc = blk / o.n;
+  const int rb = (o.rows + o.rchunks - 1) / o.rchunks;
+  const int r0 = rc * rb, r1 = min(o.rows, r0 + rb);
+  if (r0 >= r1) return;
+  const int cnt_e = (r1 - r0) * o.gw;
+  const float *base = o.A + (int64_t)r0 * o.ld + (int64_t)grp * o.gw;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (pass == 0) {
+    uint32_t m = 0, n = 0xffffffffu;
+    for (int e = threadIdx.x; e < cnt_e; e += 256) {
+      const int rr = e / o.gw, cc = e - rr * o.gw;
+      const uint32_t x = __float_as_uint(base[(int64_t)rr * o.ld + cc]) & 0x7fffffffu;
+      m = max(m, x);
+      n = min(n, x - 1u);  // 0 - 1 wraps: a zero never wins
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      m = max(m, (uint32_t)__shfl_xor((int)m, d));
+      n = min(n, (uint32_t)__shfl_xor((int)n, d));
+    }
+    if (lane == 0) { red[0][wave] = m; red[1][wave] = n; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      m = max(max(red[0][0], red[0][1]), max(red[0][2], red[0][3]));
+      n = min(min(red[1][0], red[1][1]), min(red[1][2], red[1][3]));
+      atomicMax(o.out + grp, m);
+      if (n != 0xffffffffu) atomicMin(o.out + o.n + grp, n + 1u);
+    }
+    return;
+  }
+  const uint32_t mx = o.out[grp], mn = o.out[o.n + grp];
+  if (!f16x3::spread(mx, mn == 0xffffffffu ? 0u : mn)) return;  // (uniform)
+  const float bound = f16x3::small_bound(mx);
+  uint32_t c = 0;
+  for (int e = threadIdx.x; e < cnt_e; e += 256) {
+    const int rr = e / o.gw, cc = e - rr * o.gw;
+    const float x = fabsf(base[(int64_t)rr * o.ld + cc]);
+    c += (x < bound && x != 0.0f) ? 1u : 0u;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) c += (uint32_t)__shfl_xor((int)c, d);
+  if (lane == 0 && c) atomicAdd(o.out + 2 * o.n + grp, c);
+}
+
+// A listed partial of the f16x3 weight gradient (entry: split, g, k), one
+// wave per entry: the split's sum over t = n*P + p in fp32 (lane sums of t =
+// lane + 64 i, then a butterfly), stored over the partial.
+__global__ __launch_bounds__(256) void conv_wgrad_efix_kernel(
+    ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ dY, int dys,
+    float *__restrict__ ws, int fps, const unsigned *__restrict__ list,
+    const unsigned *__restrict__ elist) {
+  const unsigned cnt = list[0];
+  const int lane = threadIdx.x & 63;
+  const unsigned w0 = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  const int64_t E = (int64_t)g.G * g.Kdim + g.G;
+  for (unsigned en = w0; en < cnt; en += nw) {
+    const unsigned *e = elist + 3 * (size_t)en;
+    const int split = (int)e[0], gg = (int)e[1], kk = (int)e[2];
+    const int nbeg = split * fps, nf = min(g.R, nbeg + fps) - nbeg;
+    uint32_t c, rr, kx, ky;
+    g.div_khkw.divmod((uint32_t)kk, c, rr);
+    g.div_kh.divmod(rr, kx, ky);
+    const int T = nf * g.P;
+    float s = 0.0f;
+    for (int t = lane; t < T; t += 64) {
+      uint32_t n, p, px, py;
+      g.div_P.divmod((uint32_t)t, n, p);
+      g.div_oh.divmod(p, px, py);
+      const int xx = (int)px + (int)kx - g.pad_w, yy = (int)py + (int)ky - g.pad_h;
+      const int64_t fr = nbeg + (int64_t)n;
+      if ((unsigned)xx < (unsigned)g.W && (unsigned)yy < (unsigned)g.H)
+        s = fmaf(dY[fr * dys + (int64_t)gg * g.P + p],
+                 X[fr * xs + (int64_t)c * g.HW + xx * g.H + yy], s);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+    if (lane == 0) ws[(int64_t)split * E + (int64_t)gg * g.Kdim + kk] = s;
   }
 }
 
@@ -1278,7 +1535,10 @@ int kcnn_conv_igemm_x6_pool(const ConvGeom &g, const float *X, int xs, const flo
 // accumulation chain stays within ~16k terms.
 // KCNN_WGRAD_X6: 0 off, 1 the 128-wide k tiles, 2 the wide (256) k tiles
 static int wgrad_x6_mode() { return family(kFamWgradX6); }
-static int wgrad_kwidth() { return wgrad_x6_mode() == 2 ? 256 : 128; }
+static int wgrad_kwidth() { return wgrad_x6_mode() >= 2 ? 256 : 128; }
+// the f16x3 form of the wide kernel: family 3 (not the default: measured
+// slower on c5, DESIGN 3 Long kernels)
+static bool wgrad_f16(const ConvGeom &) { return wgrad_x6_mode() == 3; }
 
 bool kcnn_conv_wgrad_x6_plan(const ConvGeom &g, int xs, int dys, int &S, int &fps,
                              size_t &ws_bytes) {
@@ -1320,17 +1580,47 @@ int kcnn_conv_wgrad_x6(const ConvGeom &g, const float *X, int xs, const float *d
   const dim3 grid((unsigned)(8 * ((nblocks + 7) / 8)));
   if (wgrad_kwidth() == 256) {
     constexpr int wl = 2 * 3 * 512 * WROW;
-#define KCNN_WX6W(P_)                                                                      \
-  do {                                                                                     \
-    static bool attr = hipFuncSetAttribute(                                                \
-        reinterpret_cast<const void *>(&conv_wgrad_x6w_kernel<P_>),                        \
-        hipFuncAttributeMaxDynamicSharedMemorySize, wl) == hipSuccess;                      \
-    (void)attr;                                                                            \
-    hipLaunchKernelGGL((conv_wgrad_x6w_kernel<P_>), grid, dim3(NT), wl, st, g, X, xs, dY, \
-                       dys, ws, fps, ktiles, nblocks);                                     \
+    constexpr int wl16 = 2 * 2 * 512 * WROW + 512 * 8;  // + the groups' scales / weights
+    const bool f16 = wgrad_f16(g);
+    WF16 wf{};
+    kaldi::CuScratch sc(f16 ? (3 * (size_t)(g.G + g.C) + 1 + (size_t)nblocks +
+                               3 * (size_t)nblocks * 8 * REJ_MAX) * 4
+                            : 0);
+    if (f16) {
+      uint32_t *w = static_cast<uint32_t *>(sc.p);
+      uint32_t *gst = w, *cst = gst + 3 * (size_t)g.G, *list = cst + 3 * (size_t)g.C;
+      wf.gst = gst;
+      wf.cst = cst;
+      wf.list = list;
+      wf.flags = list + 1;
+      wf.elist = wf.flags + nblocks;
+      const int rch = std::max(1, std::min(64, g.R / 64));
+      const GStatOp ga{dY, g.R, dys, g.P, g.G, rch, gst};
+      const GStatOp gc{X, g.R, xs, g.HW, g.C, rch, cst};
+      hipLaunchKernelGGL(wgrad_group_init_kernel, dim3((std::max(g.G, g.C) + 255) / 256),
+                         dim3(256), 0, st, ga, gc, list);
+      for (int pass = 0; pass < 2; pass++)
+        hipLaunchKernelGGL(wgrad_group_stats_kernel, dim3((g.G + g.C) * rch), dim3(256), 0, st,
+                           ga, gc, pass);
+    }
+#define KCNN_WX6W(P_, F_, L_)                                                               \
+  do {                                                                                      \
+    static bool attr = hipFuncSetAttribute(                                                 \
+        reinterpret_cast<const void *>(&conv_wgrad_x6w_kernel<P_, F_>),                     \
+        hipFuncAttributeMaxDynamicSharedMemorySize, L_) == hipSuccess;                       \
+    (void)attr;                                                                             \
+    hipLaunchKernelGGL((conv_wgrad_x6w_kernel<P_, F_>), grid, dim3(NT), L_, st, g, X, xs,  \
+                       dY, dys, ws, fps, ktiles, nblocks, wf);                              \
   } while (0)
-    if (padded) KCNN_WX6W(true);
-    else KCNN_WX6W(false);
+    if (f16) {
+      if (padded) KCNN_WX6W(true, true, wl16);
+      else KCNN_WX6W(false, true, wl16);
+      hipLaunchKernelGGL(conv_wgrad_efix_kernel, dim3(64), dim3(256), 0, st, g, X, xs, dY, dys,
+                         ws, fps, (const unsigned *)wf.list, (const unsigned *)wf.elist);
+      wf.redo = wf.flags;
+    }
+    if (padded) KCNN_WX6W(true, false, wl);
+    else KCNN_WX6W(false, false, wl);
 #undef KCNN_WX6W
     return (int)hipGetLastError();
   }

@@ -17,7 +17,7 @@ const FamilyInfo kFamilies[kNumFamilies] = {
     {"fwd_x6", "KCNN_FWD_X6", 2, 2},
     {"bwd_x6", "KCNN_BWD_X6", 1, 1},
     {"igemm_x6", "KCNN_IGEMM_X6", 2, 3},
-    {"wgrad_x6", "KCNN_WGRAD_X6", 2, 2},
+    {"wgrad_x6", "KCNN_WGRAD_X6", 2, 3},
     {"gemm", "KCNN_GEMM", 2, 2},
 };
 

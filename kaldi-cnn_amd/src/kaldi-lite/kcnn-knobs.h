@@ -12,7 +12,8 @@
 //   bwd_x6     KCNN_BWD_X6      1 bf16x6 fused backward, 0 fp32 MFMA
 //   igemm_x6   KCNN_IGEMM_X6    2 f16x3 implicit GEMM for convolutions of >= 2^34 flop (bf16x6
 //                               below), 3 f16x3 for all, 1 bf16x6, 0 fp32 MFMA
-//   wgrad_x6   KCNN_WGRAD_X6    2 wide bf16x6, 1 128-wide bf16x6, 0 fp32 MFMA
+//   wgrad_x6   KCNN_WGRAD_X6    2 wide bf16x6, 3 wide f16x3 (slower on c5), 1 128-wide bf16x6,
+//                               0 fp32 MFMA
 //   gemm       KCNN_GEMM        2 f16x3 GEMM (AddMatMat), 1 bf16x6 GEMM, 0 rocBLAS sgemm
 //
 // (KCNN_FUSE, KCNN_LITERAL and KCNN_PROFILE are kcnn_set_fusion,

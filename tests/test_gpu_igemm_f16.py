@@ -169,3 +169,112 @@ def test_igemm_f16_fp32_range(kc, fam, kind):
     _, dx_t, dx_s = triple(lambda: oc.backprop(x, dy, update=False))
     dx = comp.Backprop(dev(x), None, dev(dy), update=False)
     assert_bound(host(dx), dx_t, dx_s, what=f"{kind} dX")
+
+
+# ---------------------------------------------------------------------------
+# The weight gradient's f16x3 form (conv_wgrad_x6w_kernel<P, true>, wgrad_x6
+# family 3; not the default): scale groups over the whole batch (a filter of dY, an input channel
+# of X), rejected partials recomputed in fp32, flagged blocks on bf16x6.
+# Reference: ConvolutionComponent::Update's gradient (src/nnet0/
+# nnet-component-nnet0.cc:738-765).
+
+@pytest.fixture
+def wfam(kc):
+    old = kc.get_kernel_family("wgrad_x6")
+
+    def set_(v):
+        kc.set_kernel_family("wgrad_x6", v)
+    yield set_
+    kc.set_kernel_family("wgrad_x6", old)
+
+
+def _grad_check(kc, comp, oc, x, dy, what, bound=assert_bound):
+    _, (gW_t, gb_t), (gW_s, gb_s) = triple(lambda: oc.gradient(x, dy))
+    g = host(comp.ComputeGradient(dev(x), dev(dy)))
+    kd = gW_t.shape[0]
+    G = gW_t.shape[1]
+    bound(g[:kd * G].reshape(kd, G), gW_t, gW_s, what=f"{what} gW")
+    bound(g[kd * G:], gb_t, gb_s, what=f"{what} gb")
+
+
+@pytest.mark.parametrize("cfg", [C5_C3, C5_C2, C5_C4], ids=["c5_C3", "c5_C2", "c5_C4"])
+def test_wgrad_f16_parity(kc, wfam, cfg):
+    wfam(3)
+    H, W, C, kh, kw, G, ph, pw = cfg
+    comp, oc = make_pair(kc, cfg, seed=17 + C)
+    r = rng(5 + G)
+    N = 41
+    oh, ow = H + 2 * ph - kh + 1, W + 2 * pw - kw + 1
+    x = randn(r, (N, H * W * C))
+    dy = randn(r, (N, oh * ow * G))
+    _grad_check(kc, comp, oc, x, dy, "f16x3")
+
+
+@pytest.mark.parametrize("spread", [24, 32])
+@pytest.mark.parametrize("group", ["filter", "channel"])
+def test_wgrad_intra_group_range(kc, wfam, group, spread):
+    """A group's largest values meet zeros and the rest sit 2^-spread below:
+    "filter": dY's filter-0 maps are 1 on frame 0 and N(0,1) 2^-spread on the
+    other frames, X zero on frame 0; "channel": X's channel 0 is 1 on frame
+    0 and the rest of the batch N(0,1) 2^-spread, dY zero on frame 0."""
+    wfam(3)
+    H, W, C, kh, kw, G, ph, pw = C5_C3
+    oh, ow = H + 2 * ph - kh + 1, W + 2 * pw - kw + 1
+    P = oh * ow
+    comp, oc = make_pair(kc, C5_C3, seed=47)
+    r = rng(48 + spread)
+    N = 9
+    x = randn(r, (N, C, H * W))
+    dy = randn(r, (N, G, P))
+    sc = np.float32(2.0 ** -spread)
+    if group == "filter":
+        dy[1:] *= sc
+        dy[0] = 0.0
+        dy[0, 0] = 1.0
+        x[0] = 0.0
+    else:
+        x[1:] *= sc
+        x[0] = 0.0
+        x[0, 0] = 1.0
+        dy[0] = 0.0
+    _grad_check(kc, comp, oc, x.reshape(N, -1).astype(np.float32),
+                dy.reshape(N, -1).astype(np.float32), f"{group} spread 2^{spread}")
+
+
+@pytest.mark.parametrize("kind", ["huge_x", "huge_dy", "tiny_x", "tiny_dy"])
+def test_wgrad_f16_fp32_range(kc, wfam, kind):
+    """test_gpu_x6_range's operands through the f16x3 weight gradient: the
+    full bar for huge ones; tiny ones at the bf16x6 contract where a block
+    falls back to it (elementwise 1e-5 S, normwise 1e-4)."""
+    from test_gpu_x6_range import scaled_inputs
+    import _util
+    wfam(3)
+    H, W, C, kh, kw, G, ph, pw = C5_C3
+    comp, oc = make_pair(kc, C5_C3, seed=3)
+    r = rng(41)
+    N = 5
+    oh, ow = H + 2 * ph - kh + 1, W + 2 * pw - kw + 1
+    x, dy = scaled_inputs(kind, r, N, H * W * C, oh * ow * G, G)
+
+    def bound(a, t, s, rtol=1e-5, what=""):
+        _util.assert_bound(a, t, s, rtol=rtol, what=what, norm_rtol=1e-4)
+    _grad_check(kc, comp, oc, x, dy, kind, bound if kind.startswith("tiny") else assert_bound)
+
+
+def test_wgrad_f16_nonfinite_blocks(kc, wfam):
+    """A frame with Inf / NaN flags the blocks of its split; they run on the
+    bf16x6 form: the non-finite entries are those of the bf16x6 kernel."""
+    H, W, C, kh, kw, G, ph, pw = C5_C3
+    comp, _ = make_pair(kc, C5_C3, seed=9)
+    r = rng(10)
+    N = 7
+    oh, ow = H + 2 * ph - kh + 1, W + 2 * pw - kw + 1
+    x = randn(r, (N, H * W * C))
+    x[2, 77] = np.inf
+    dy = randn(r, (N, oh * ow * G))
+    outs = []
+    for fam_v in (1, 3):
+        wfam(fam_v)
+        outs.append(host(comp.ComputeGradient(dev(x), dev(dy))))
+    # family 1 is the 128-wide bf16x6 kernel: same non-finite positions
+    assert (np.isfinite(outs[0]) == np.isfinite(outs[1])).all()

@@ -46,6 +46,15 @@ namespace {
 constexpr int NT = 512, BK = 32, ROWB = BK * 2;
 constexpr unsigned kOob = 0x7ffffff0u;  // an offset past every buffer range used
 
+// the implicit GEMM's images: 16-B chunk c of row r XOR ((r >> 1) ^ (r >> 2))
+// & 3, conflict-free for both its ds_write_b128 (8 consecutive rows, banks
+// mod 32) and its ds_read_b128 fragments (lane groups {0-3, 12-15, 20-27},
+// {4-11, 16-19, 28-31}, banks mod 64; MI355X_MICROARCH.md LDS table); swz's
+// (r >> 2) & 3 put two rows of every write group on one slot (the f16x3
+// C3 forward: 27 % of its LDS cycles were bank conflicts)
+__device__ __forceinline__ int swzi(int r, int c) {
+  return r * ROWB + ((c ^ (((r >> 1) ^ (r >> 2)) & 3)) << 4);
+}
 __device__ __forceinline__ int swz(int r, int c) {
   return r * ROWB + ((c ^ ((r >> 2) & 3)) << 4);
 }
@@ -338,17 +347,17 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
     if constexpr (F16) {
 #pragma unroll
       for (int cc = 0; cc < APT / 8; cc++)
-        put8h(buf, PLA, swz(a_row, a_kc * (APT / 8) + cc), &av[8 * cc], ea, m1);
+        put8h(buf, PLA, swzi(a_row, a_kc * (APT / 8) + cc), &av[8 * cc], ea, m1);
 #pragma unroll
       for (int cc = 0; cc < BPT / 8; cc++)
-        put8h(buf + 2 * PLA, PLB, swz(b_row, b_kc * (BPT / 8) + cc), &bv[8 * cc], eb, m1);
+        put8h(buf + 2 * PLA, PLB, swzi(b_row, b_kc * (BPT / 8) + cc), &bv[8 * cc], eb, m1);
     } else {
 #pragma unroll
       for (int cc = 0; cc < APT / 8; cc++)
-        put8(buf, PLA, swz(a_row, a_kc * (APT / 8) + cc), &av[8 * cc]);
+        put8(buf, PLA, swzi(a_row, a_kc * (APT / 8) + cc), &av[8 * cc]);
 #pragma unroll
       for (int cc = 0; cc < BPT / 8; cc++)
-        put8(buf + 3 * PLA, PLB, swz(b_row, b_kc * (BPT / 8) + cc), &bv[8 * cc]);
+        put8(buf + 3 * PLA, PLB, swzi(b_row, b_kc * (BPT / 8) + cc), &bv[8 * cc]);
     }
   };
 
@@ -375,8 +384,8 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
       for (int i = 0; i < 2; i++)
 #pragma unroll
         for (int pl = 0; pl < 2; pl++) {
-          a[i][pl] = *reinterpret_cast<const f16x3::f16x8 *>(bufA + pl * PLA + swz(ar + 32 * i, c));
-          bb[i][pl] = *reinterpret_cast<const f16x3::f16x8 *>(bufB + pl * PLB + swz(br + 32 * i, c));
+          a[i][pl] = *reinterpret_cast<const f16x3::f16x8 *>(bufA + pl * PLA + swzi(ar + 32 * i, c));
+          bb[i][pl] = *reinterpret_cast<const f16x3::f16x8 *>(bufB + pl * PLB + swzi(br + 32 * i, c));
         }
 #pragma unroll
       for (int i = 0; i < 2; i++)
@@ -391,8 +400,8 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
     for (int i = 0; i < 2; i++)
 #pragma unroll
       for (int pl = 0; pl < 3; pl++) {
-        a[i][pl] = *reinterpret_cast<const x6::bf16x8 *>(bufA + pl * PLA + swz(ar + 32 * i, c));
-        bb[i][pl] = *reinterpret_cast<const x6::bf16x8 *>(bufB + pl * PLB + swz(br + 32 * i, c));
+        a[i][pl] = *reinterpret_cast<const x6::bf16x8 *>(bufA + pl * PLA + swzi(ar + 32 * i, c));
+        bb[i][pl] = *reinterpret_cast<const x6::bf16x8 *>(bufB + pl * PLB + swzi(br + 32 * i, c));
       }
 #pragma unroll
     for (int i = 0; i < 2; i++)

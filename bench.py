@@ -58,6 +58,7 @@ CONV_POOL_FWD_Y_BYTES = CONV_POOL_FWD_BYTES + 4 * P * G             # 249,216
 CONV_BWD_POOLED_BYTES = 4 * (2 * H * W * C + POOL_OUT) + POOL_OUT    # 68,640
 POOL_BWD_MASK_BYTES = POOL_OUT + 4 * (POOL_OUT + P * G)               # 243,936
 FC_FLOP = 3 * 2 * POOL_OUT * FC_OUT                   # 71,368,704
+DY_RING = 8   # synthetic output derivatives cycled over the steps (4 and their negations)
 
 
 def stack_config():
@@ -149,6 +150,66 @@ def nnet_conv_flop():
                for H, W, C, kh, kw, G in NNET_CONVS)
 
 
+def conv_pass_engines(convs, frames, fam):
+    """(pass, algorithmic flop, engine) of every convolution pass of a stack,
+    by the library's dispatch rules (price each kernel against
+    the engine it runs on).  convs: (H, W, C, kh, kw, G, pad, pooled_after)
+    per layer; fam: the kernel-family values (kcnn.get_kernel_family).
+      forward: the frame-resident kernel for Kdim <= 64 (f16x3 when fwd_x6 is
+        2, unpadded, G <= 128 and Kdim <= 32 -- cnsl-conv-frame.hip
+        fwd_arith; fp32 MFMA otherwise), else the implicit GEMM: f16x3 when
+        igemm_x6 is 3, or 2 and the call is >= 2^34 flop (cnsl-conv-igemm-x6.hip
+        use_f16), bf16x6 for 1 or 2 below the rule, fp32 for 0;
+      data gradient: the one-pass frame backward for Kdim <= 31 (bf16x6 with
+        bwd_x6, fp32 without), else the implicit GEMM in its gather form
+        (flipped kernel over the HW input positions) or, when HW >= 1.25 P,
+        its scatter form (a 1x1 convolution over the P output positions),
+        with the forward's f16x3 rule on that call's flop;
+      weight gradient: the frame backward's (Kdim <= 31), else the wide
+        kernel: bf16x6 for wgrad_x6 1 / 2, f16x3 for 3, fp32 for 0.
+    Returns the list and the number of f16x3 implicit-GEMM calls."""
+    out, f16_calls = [], 0
+
+    def igemm(flop_call):
+        f = fam["igemm_x6"]
+        if f == 3 or (f == 2 and flop_call >= 2 ** 34):
+            return "f16x3"
+        return "bf16x6" if f else "fp32"
+    for i, (h, w, c, kh, kw, g, pad, _) in enumerate(convs):
+        oh, ow = h + 2 * pad - kh + 1, w + 2 * pad - kw + 1
+        P, HW, Kdim = oh * ow, h * w, kh * kw * c
+        flop = 2 * frames * P * g * Kdim
+        if Kdim <= 64:
+            eng = "f16x3" if (fam["fwd_x6"] == 2 and pad == 0 and g <= 128 and Kdim <= 32) \
+                else "bf16x6" if (fam["fwd_x6"] == 1 and pad == 0 and g <= 128 and Kdim <= 31) \
+                else "fp32"
+        else:
+            eng = igemm(flop)
+            f16_calls += eng == "f16x3"
+        out.append((f"C{i + 1} forward", flop, eng))
+        if Kdim <= 31:
+            eb = "bf16x6" if fam["bwd_x6"] else "fp32"
+            out += [(f"C{i + 1} data gradient", flop, eb), (f"C{i + 1} weight gradient", flop, eb)]
+            continue
+        npos = P if HW >= 1.25 * P else HW
+        eng = igemm(2 * frames * npos * Kdim * g)
+        f16_calls += eng == "f16x3"
+        out.append((f"C{i + 1} data gradient", flop, eng))
+        wf = fam["wgrad_x6"]
+        out.append((f"C{i + 1} weight gradient", flop,
+                    "f16x3" if wf == 3 else "bf16x6" if wf else "fp32"))
+    return out, f16_calls
+
+
+def engine_ceiling(passes):
+    """The fp32-equivalent ceiling of a mix of passes: total flop over the
+    time each pass needs at its own engine's peak (a flop-weighted harmonic
+    mean of the engines' ceilings)."""
+    tot = sum(f for _, f, _ in passes)
+    t = sum(f / ENGINE_PEAK_TFLOPS[e] for _, f, e in passes)
+    return tot / t if t else None
+
+
 # the source of each roofline kernel: a PMC byte count (profiles/
 # pmc_traffic.json) is only used while the digest of the source it was taken
 # from still matches
@@ -164,19 +225,68 @@ KERNEL_SOURCES = {
 }
 
 
+def strip_c_comments(text):
+    """C/C++ source without its comments, blank lines and trailing blanks
+    (string and character literals kept as they are)."""
+    out, i, n = [], 0, len(text)
+    while i < n:
+        c = text[i]
+        if c == "/" and text.startswith("//", i):
+            j = text.find("\n", i)
+            i = n if j < 0 else j
+        elif c == "/" and text.startswith("/*", i):
+            j = text.find("*/", i + 2)
+            i = n if j < 0 else j + 2
+            out.append(" ")
+        elif c in "\"'":
+            j = i + 1
+            while j < n and text[j] != c:
+                j += 2 if text[j] == "\\" else 1
+            out.append(text[i:j + 1])
+            i = j + 1
+        else:
+            out.append(c)
+            i += 1
+    lines = ("".join(out)).splitlines()
+    return "\n".join(l.rstrip() for l in lines if l.strip())
+
+
+def kernel_source_files(src):
+    """`src` and every repo header it includes, transitively (quoted
+    #includes resolved as the Makefile's -I../include -Isrc do)."""
+    import re
+    dirs = [os.path.join(ROOT, "kaldi-cnn_amd/src"), os.path.join(ROOT, "include")]
+    seen, todo = [], [os.path.join(ROOT, src)]
+    while todo:
+        f = todo.pop(0)
+        if f in seen:
+            continue
+        seen.append(f)
+        with open(f) as fh:
+            code = strip_c_comments(fh.read())
+        for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', code, re.M):
+            for d in [os.path.dirname(f)] + dirs:
+                cand = os.path.normpath(os.path.join(d, inc))
+                if os.path.exists(cand):
+                    todo.append(cand)
+                    break
+    return seen
+
+
 def kernel_source_digest(kernel):
-    """sha1 of the .hip file that defines `kernel` (name up to '<') and of the
-    headers under src/cnslmat it may include; None for an unknown kernel."""
-    import glob
+    """sha1 of the code (comments and blank lines stripped) of the .hip file
+    that defines `kernel` (name up to '<') and of the repo headers it
+    includes, transitively; None for an unknown kernel.  A comment-only edit
+    leaves it unchanged."""
     import hashlib
     src = KERNEL_SOURCES.get(kernel.split("<")[0].strip())
     if src is None:
         return None
     h = hashlib.sha1()
-    for f in [src] + sorted(glob.glob(os.path.join(ROOT, "kaldi-cnn_amd/src/cnslmat/*.h"))):
-        path = f if os.path.isabs(f) else os.path.join(ROOT, f)
-        with open(path, "rb") as fh:
-            h.update(fh.read())
+    for path in kernel_source_files(src):
+        with open(path) as fh:
+            h.update(os.path.relpath(path, ROOT).encode() + b"\0")
+            h.update(strip_c_comments(fh.read()).encode())
     return h.hexdigest()
 
 
@@ -609,7 +719,15 @@ def main():
     # a CuMatrix holds it (the reference's CuMatrix: cudaMallocPitch); an
     # unpadded 3454-column nnet.config derivative costs the FC GEMMs a copy
     pitch = (out_cols + 15) // 16 * 16
-    dy = torch.randn((B, pitch), generator=gen, device="cuda").mul_(1e-2)[:, :out_cols]
+    # a ring of DY_RING seeded derivatives, each followed by its negation, one
+    # per step: the same derivative every step drives the parameters one way
+    # (nnet.config's FC layers overflowed after a few dozen steps); the ring
+    # keeps every pass in the same steady state
+    dy_ring = []
+    for _ in range(DY_RING // 2):
+        base = torch.randn((B, pitch), generator=gen, device="cuda").mul_(1e-2)
+        dy_ring += [base[:, :out_cols], base.neg()[:, :out_cols]]
+    step_no = [0]
 
     grads = kcnn_dp.gradient_buffers(
         net, lambda n: torch.empty(n, device="cuda"))
@@ -625,6 +743,8 @@ def main():
     profiling_dp = False
 
     def step():
+        dy = dy_ring[step_no[0] % DY_RING]
+        step_no[0] += 1
         if not dist:
             net.Propagate(x)
             net.Backprop(dy)                     # reference semantics: update in Backprop
@@ -692,30 +812,15 @@ def main():
             el = float(t.item())
         return el, pr
 
-    # the parameters after the warm-up, restored before the profiled pass: the
-    # synthetic output derivative is the same every step, so the parameters
-    # drift one way and nnet.config's four FC layers overflow after a few
-    # dozen steps (Inf / NaN operands then take the f16x3 kernels' fp32 paths,
-    # and its profiled pass measured 630 ms per step); restored, both passes
-    # run from the same state (outside the timed regions)
-    snap = []
-    for comp in net.components:
-        for which in (kcnn.PARAM_LINEAR, kcnn.PARAM_BIAS, kcnn.PARAM_PREV_GRAD):
-            try:
-                snap.append((comp, which, comp.GetParam(which).clone()))
-            except Exception:  # noqa: BLE001 -- a component without that parameter
-                pass
-    torch.cuda.synchronize()
-
     # headline: profiling off (no events in the stream); then the same K steps
     # again with hipEvents around every component scope, for the per-kernel
     # times of the roofline
     elapsed, _ = timed(False)
-    for comp, which, v in snap:
-        comp.SetParam(which, v)
-    torch.cuda.synchronize()
     profiling_dp = True
+    kcnn.conv_fix_counts(reset=True)
     elapsed_prof, prof = timed(True)
+    fc = kcnn.conv_fix_counts()
+    f16_calls_lib = fc[0] / args.steps if fc else None  # f16x3 implicit GEMMs per step
     profiling_dp = False
     dp = dp_report(dist, grads, marks, args.steps) if dist else None
 
@@ -728,6 +833,18 @@ def main():
         scopes = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items())}
         conv_ms = sum(v for k, v in scopes.items() if k.startswith("ConvolutionComponent"))
         conv_flop = 3 * stack_flop * B  # fwd + dgrad + wgrad per frame
+        fam = {n: kcnn.get_kernel_family(n) for n in ("fwd_x6", "bwd_x6", "igemm_x6",
+                                                        "wgrad_x6")}
+        convs = ([(h, w, c, kh, kw, g, pad, False) for kind, (h, w, c, kh, kw, g, pad)
+                  in ((k, a) for k, a in C5_LAYERS if k == "conv")]
+                 if args.config == "c5" else
+                 [(h, w, c, kh, kw, g, 0, False) for h, w, c, kh, kw, g in NNET_CONVS])
+        passes, f16_pred = conv_pass_engines(convs, B, fam)
+        assert abs(sum(f for _, f, _ in passes) - conv_flop) < 1e-6 * conv_flop
+        eng_peak = engine_ceiling(passes)
+        mix = {}
+        for _, f, e in passes:
+            mix[e] = mix.get(e, 0) + f
         if args.config == "nnet":
             metric = "frames/sec fwd+bwd, reference egs/exp/nnet/nnet.config model"
             workload = ("nnet.config: Splice(40,+-10) 6x(Conv+ReLU) Maxpool(1x2x1) "
@@ -750,35 +867,37 @@ def main():
                            "parallelism": f"dp{world}"},
                 "conv": {"ms_per_step": round(conv_ms, 4),
                          "TFLOP/s": round(conv_flop / conv_ms / 1e9, 2) if conv_ms else None,
-                         # fp32 work over the bf16x6 engine's ceiling (the bf16
-                         # dense peak over its six products per fp32 product)
-                         "engine": "bf16x6 (v_mfma_f32_32x32x16_bf16, fp32 operands split 3-way, "
-                                   "6 products)",
-                         "engine_frac": round(conv_flop / conv_ms / 1e9 /
-                                              ENGINE_PEAK_TFLOPS["bf16x6"], 4) if conv_ms else None},
+                         # fp32 work over the ceiling of the engines its passes
+                         # run on (per pass, conv_pass_engines)
+                         "engine_flop_per_step": mix,
+                         "engine_ceiling_tflops": round(eng_peak, 1),
+                         "engine_frac": round(conv_flop / conv_ms / 1e9 / eng_peak, 4)
+                         if conv_ms else None,
+                         "passes": [{"pass": n, "engine": e, "gflop": round(f / 1e9, 3)}
+                                    for n, f, e in passes],
+                         "f16x3_igemm_calls_per_step": {"predicted": f16_pred,
+                                                        "library": f16_calls_lib}},
                 "scopes_ms_per_step": scopes,
             }
             if conv_ms:
                 # the convolution layers (implicit GEMM, weight gradient, frame
-                # kernels) as one MFMA-bound scope: fp32 work of fwd + dgrad +
-                # wgrad over the fp32 MFMA peak, no PMC pass of these configs
-                # frac can pass 1.0: the fp32 products run on the bf16 / f16
-                # matrix cores from split operands, whose fp32-equivalent
-                # ceiling is the bf16 dense peak over the products per fp32
-                # product (6 for the bf16x6 implicit GEMM / weight gradient /
-                # pooled backward that carry most of these layers' flop)
-                eng_peak = ENGINE_PEAK_TFLOPS["bf16x6"]
+                # kernels) as one MFMA-bound scope: the fp32 work of fwd + dgrad
+                # + wgrad over the ceiling of the engines its passes run on
+                # (f16x3: f16 dense peak / 3 products, bf16x6: bf16 dense peak /
+                # 6, fp32: the fp32 MFMA peak), flop-weighted over the passes
                 result["roofline"] = {
                     "kernel": "conv layers (every ConvolutionComponent scope)", "bound": "mfma",
                     "achieved": round(conv_flop / conv_ms / 1e9, 2),
                     "peak": round(eng_peak, 1), "unit": "TFLOP/s",
                     "frac": round(conv_flop / conv_ms / 1e9 / eng_peak, 4),
                     "traffic": None, "algorithmic_flop_per_step": conv_flop,
-                    "engine": "bf16x6",
-                    "note": "peak = the engine's fp32-equivalent ceiling: the layers compute "
-                            "fp32 products on the bf16 matrix cores from 3-way split operands, "
-                            "six products each (bf16 dense peak / 6); the fp32 MFMA peak "
-                            f"({PEAK_FP32_MFMA_TFLOPS} TFLOP/s) is not the bound of these kernels"}
+                    "engine": "mix: " + ", ".join(f"{e} {f / conv_flop:.1%}"
+                                                  for e, f in sorted(mix.items())),
+                    "note": "peak = the flop-weighted ceiling of the engines the passes run on "
+                            "(result.conv.passes); fp32 products run on the f16 / bf16 matrix "
+                            "cores from split operands (f16x3: 3 products, bf16x6: 6); the fp32 "
+                            f"MFMA peak ({PEAK_FP32_MFMA_TFLOPS} TFLOP/s) bounds only the fp32 "
+                            "passes"}
             if dp:
                 result["dp"] = dp
             if not args.no_cpu_baseline and world == 1:
@@ -915,7 +1034,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: N(0,1) fbank-shaped frames, N(0,1)*1e-2 output derivative",
+            "data": "synthetic: N(0,1) fbank-shaped frames, a ring of 4 N(0,1)*1e-2 output "
+                    "derivatives and their negations, one per step",
             # the second pass of K steps with hipEvents around each scope
             # (kernel times below come from it)
             "profiled_ms_per_step": round(elapsed_prof / args.steps * 1e3, 4),

@@ -49,6 +49,11 @@ const char *kcnn_version(void);
  * over the caching allocator's blocks stays valid while this does not move
  * (bench.py --graph). */
 unsigned long long kcnn_device_malloc_calls(void);
+/* The f16x3 implicit GEMM's cumulative counts since the last reset (a test
+ * and bench diagnostic, no reference counterpart): out[0] its calls, out[1]
+ * the tiles and out[2] the single elements its fp32 fix-up kernels
+ * recomputed; reset != 0 zeroes them.  Synchronises the device. */
+int kcnn_conv_fix_counts(unsigned long long *out, int reset);
 /* CuDevice::SelectGpuId(use_gpu, device) (upstream cu-device.h). */
 int kcnn_init(int device);
 int kcnn_set_stream(kcnn_stream_t stream);

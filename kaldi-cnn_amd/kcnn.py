@@ -146,6 +146,16 @@ def device_malloc_calls() -> int:
     return int(lib().kcnn_device_malloc_calls())
 
 
+def conv_fix_counts(reset=False):
+    """(f16x3 implicit-GEMM calls, tiles, elements recomputed by its fp32
+    fix-ups) since the last reset (kcnn_conv_fix_counts)."""
+    if not hasattr(lib(), "kcnn_conv_fix_counts"):  # (absent from pre-r06 builds)
+        return None
+    out = (ctypes.c_ulonglong * 3)()
+    check(lib().kcnn_conv_fix_counts(out, int(bool(reset))))
+    return tuple(int(v) for v in out)
+
+
 def profile_string() -> str:
     buf = ctypes.create_string_buffer(1 << 16)
     check(lib().kcnn_profile_string(buf, len(buf)))

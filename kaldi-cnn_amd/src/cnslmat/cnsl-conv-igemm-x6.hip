@@ -32,6 +32,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "conv-geom.h"
 #include "f16-split.h"
@@ -651,6 +652,11 @@ __global__ __launch_bounds__(256) void conv_igemm_fixup_kernel(
 // the rejected element recomputed (conv_dot) and stored (+ bias, ReLU), or,
 // for the pooled epilogue, the window's rejected elements recomputed (+ bias)
 // and the window pooled again with the epilogue's order and compares.
+// Cumulative fix-up counts of the f16x3 form since the last reset (listed
+// tiles, listed elements), read by kcnn_conv_fix_counts: the tests' evidence
+// that a full-size call took the fix-up paths (one atomic pair per call).
+__device__ unsigned long long g_igemm_fix_counts[2];
+
 template <int POOL>
 __global__ __launch_bounds__(256) void conv_igemm_efix_kernel(
     ConvGeom g, const float *__restrict__ X, int xs, const float *__restrict__ Kw, int ks,
@@ -658,6 +664,10 @@ __global__ __launch_bounds__(256) void conv_igemm_efix_kernel(
     const unsigned *__restrict__ list, const unsigned *__restrict__ elist) {
   const unsigned n = list[1];
   const int lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    atomicAdd(&g_igemm_fix_counts[0], (unsigned long long)list[0]);
+    atomicAdd(&g_igemm_fix_counts[1], (unsigned long long)n);
+  }
   const unsigned w0 = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
   for (unsigned en = w0; en < n; en += nw) {
     const unsigned *e = elist + (size_t)EW * en;
@@ -1364,6 +1374,8 @@ void launch_t(const ConvGeom &g, unsigned blocks, const float *X, int xs, const 
   hipLaunchKernelGGL((conv_igemm_x6_kernel<BG, PADDED, STG, TAB, POOL, F16>), dim3(blocks),
                      dim3(NT), lds, st, g, X, xs, K, ks, bias, out, os, relu, po, fx);
 }
+// f16x3 implicit-GEMM calls since the last reset (kcnn_conv_fix_counts)
+std::atomic<unsigned long long> g_igemm_f16_calls{0};
 // the bf16x6 form, or the f16x3 form and the fp32 fixup of its listed tiles
 template <int BG, bool PADDED, bool TAB, int POOL>
 void launch_pair(const ConvGeom &g, unsigned blocks, const float *X, int xs, const float *K,
@@ -1376,6 +1388,7 @@ void launch_pair(const ConvGeom &g, unsigned blocks, const float *X, int xs, con
   }
   launch_t<BG, PADDED, false, TAB, POOL, true>(g, blocks, X, xs, K, ks, bias, out, os, relu,
                                                st, po, fx);
+  g_igemm_f16_calls.fetch_add(1, std::memory_order_relaxed);
   hipLaunchKernelGGL((conv_igemm_fixup_kernel<BG, POOL>), dim3(std::min(blocks, 256u)),
                      dim3(256), 0, st, g, X, xs, K, ks, bias, out, os, relu, po,
                      (const unsigned *)fx.list);
@@ -1460,6 +1473,27 @@ void report_flags(const F16Aux &fx, unsigned nb, const ConvGeom &g, hipStream_t 
 }
 
 }  // namespace
+
+// The f16x3 implicit GEMM's cumulative counts (kcnn.h): out[0] its calls,
+// out[1] the tiles and out[2] the elements its fix-up kernels recomputed in
+// fp32; reset != 0 zeroes them afterwards.  Synchronises the device.
+extern "C" int kcnn_conv_fix_counts(unsigned long long *out, int reset) {
+  unsigned long long d[2] = {0, 0};
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpyFromSymbol(d, HIP_SYMBOL(g_igemm_fix_counts), sizeof d) != hipSuccess)
+    return 1;
+  if (out) {
+    out[0] = g_igemm_f16_calls.load();
+    out[1] = d[0];
+    out[2] = d[1];
+  }
+  if (reset) {
+    const unsigned long long z[2] = {0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_igemm_fix_counts), z, sizeof z) != hipSuccess) return 1;
+    g_igemm_f16_calls.store(0);
+  }
+  return 0;
+}
 
 // Conv2D(concat) + bias (+ ReLU) on the f16 (family igemm_x6 = 2, with the
 // bf16x6 form for flagged tiles) or bf16 (1) MFMAs; -1 (nothing launched)

@@ -432,10 +432,11 @@ __device__ __forceinline__ void emit(const GemmF16Args &p, int row, int col, flo
 }
 // The elements a lane's check rejected (bit n of `mine` its n-th candidate,
 // decode(lane, n) -> (row, col)), each recomputed by the whole wave
-// (wave_dot) and stored: a wave-uniform loop over the wave's rejections
-template <typename Decode>
+// (wave_dot) and handed to put(l, n, row, col, v) on lane 0: a wave-uniform
+// loop over the wave's rejections
+template <typename Decode, typename Put>
 __device__ __forceinline__ void fix_rejected(const GemmF16Args &p, bool a_kc, bool b_kc,
-                                             uint64_t mine, int lane, Decode decode) {
+                                             uint64_t mine, int lane, Decode decode, Put put) {
   for (;;) {
     const uint64_t who = __ballot(mine != 0);
     if (who == 0) break;
@@ -447,9 +448,15 @@ __device__ __forceinline__ void fix_rejected(const GemmF16Args &p, bool a_kc, bo
     int row, col;
     decode(l, n, row, col);
     const float v = wave_dot(p, a_kc, b_kc, row, col, lane);
-    if (lane == 0) emit(p, row, col, v);
+    if (lane == 0) put(l, n, row, col, v);
     if (lane == l) mine &= mine - 1;
   }
+}
+template <typename Decode>
+__device__ __forceinline__ void fix_rejected(const GemmF16Args &p, bool a_kc, bool b_kc,
+                                             uint64_t mine, int lane, Decode decode) {
+  fix_rejected(p, a_kc, b_kc, mine, lane, decode,
+               [&](int, int, int row, int col, float v) { emit(p, row, col, v); });
 }
 
 // The tile's results.  C/D map of 32x32x16: register g of lane l holds row
@@ -495,8 +502,10 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
   // plane buffers, free after a barrier), then 16-B stores of whole rows:
   // a quarter of the store instructions of the per-register stores below
   // (c2's data gradient: 400 -> 388 us at K 1024).  An element the check
-  // rejects is staged and stored like the rest, then recomputed and stored
-  // again by its own wave (fix_rejected: the same wave, so in order).
+  // rejects is recomputed by its wave (fix_rejected) into its staging slot
+  // before the half is stored, so alpha, beta * C and the bias are applied
+  // to it once, by the same 16-B store as its neighbours (a
+  // second store_value after the staged store read back the new C).
   const bool staged = row0 + BM <= p.M && col0 + BN <= p.N && !skip && !p.mom.W &&
                       (partial || ((ldo & 3) | ((uintptr_t)slab & 15)) == 0)
 #ifdef KCNN_EXPERIMENTS  // KCNN_GEMM_DEBUG & 8: the per-register stores only
@@ -529,6 +538,23 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
               __builtin_amdgcn_ldexpf(acc[i][j][g], -(sexp[rl] + ec));
         }
       }
+      if (check) {
+        // this half's rejections (bits 32 i .. 32 i + 31) into their slots
+        // (lane 0 writes after every lane's staging write: one wave, LDS in order)
+        const uint64_t mine = (rej >> (32 * i)) & 0xffffffffull;
+        fix_rejected(
+            p, A_KC, B_KC, mine, lane,
+            [&](int l, int n, int &row, int &col) {
+              const int j = (n >> 4) & 1, g = n & 15;
+              row = row0 + wm * 64 + i * 32 + (g & 3) + 8 * (g >> 2) + 4 * (l >> 5);
+              col = col0 + wn * 64 + j * 32 + (l & 31);
+            },
+            [&](int l, int n, int, int, float v) {
+              const int j = (n >> 4) & 1, g = n & 15;
+              const int rr = (g & 3) + 8 * (g >> 2) + 4 * (l >> 5);
+              st[rr * SR + j * 32 + (l & 31)] = v;
+            });
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int f = lane + 64 * k, rr = f >> 4, c4 = f & 15;
@@ -554,7 +580,6 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
         *o = w;
       }
     }
-    if (check) fix();
     return;
   }
 #pragma unroll

@@ -14,7 +14,10 @@ decided by the same values on both sides):
   Conv / FC update           bound on W', b', prev' (:738-777, :1133-1150)
 
 `rows` restricts the row-local checks (outputs and input derivatives) to a
-sample of rows; the parameter update, a sum over all rows, is then skipped.
+sample of rows; the parameter update, a sum over all rows, is then checked
+against a float64 gradient of the whole batch computed with torch on the
+same device (`device_gradient`: im2col by F.unfold and fp64 contractions,
+written from the layout spec) unless `update=False`.
 """
 import numpy as np
 
@@ -67,6 +70,51 @@ def oracle_layers(config, net, kc):
     return layers
 
 
+def device_gradient(oc, a, d, chunk=256):
+    """The float64 gradient of a Conv / FC layer over every row of its input
+    `a` and output derivative `d` (torch tensors, any device, row-strided
+    views allowed): ((gW, gb) rounded to fp32, (S_W, S_b) the sums of
+    |terms|), in the oracle's layouts -- conv gW[c*kh*kw + kx*kh + ky][g]
+    (cnsl-cu-kernels.cu:26-30), FC gW[out][in] (nnet-component-nnet0.cc:1141).
+    Chunked over rows so the fp64 im2col stays a few hundred MB."""
+    import torch
+    import torch.nn.functional as F
+    N = a.shape[0]
+    if isinstance(oc, O.FC):
+        gW = gS = gb = bS = 0
+        for n0 in range(0, N, 4 * chunk):
+            x = a[n0:n0 + 4 * chunk].double()
+            y = d[n0:n0 + 4 * chunk].double()
+            gW = gW + y.t() @ x
+            gS = gS + y.abs().t() @ x.abs()
+            gb = gb + y.sum(0)
+            bS = bS + y.abs().sum(0)
+    else:
+        H, W, C = oc.in_height, oc.in_width, oc.in_channel
+        kh, kw, G = oc.kernel_height, oc.kernel_width, oc.group
+        oh, ow = oc.out_height, oc.out_width
+        gW = gS = gb = bS = 0
+        for n0 in range(0, N, chunk):
+            xs = a[n0:n0 + chunk].double()
+            n = xs.shape[0]
+            # row col = h + w*H + c*H*W  ->  [n, C, H, W]
+            xt = xs.reshape(n, C, W, H).transpose(2, 3)
+            u = F.unfold(xt, (kh, kw), padding=(oc.in_pad_height, oc.in_pad_width))
+            # output col = g*P + px*oh + py  ->  [n, G, oh*ow] in unfold's order
+            y = d[n0:n0 + chunk].double().reshape(n, G, ow, oh).transpose(2, 3).reshape(
+                n, G, oh * ow)
+            gW = gW + torch.einsum("nkl,ngl->kg", u, y)
+            gS = gS + torch.einsum("nkl,ngl->kg", u.abs(), y.abs())
+            gb = gb + y.sum((0, 2))
+            bS = bS + y.abs().sum((0, 2))
+        # unfold's k = c*kh*kw + ky*kw + kx  ->  the kernel matrix's c*kh*kw + kx*kh + ky
+        def kmat(t):
+            return t.reshape(C, kh, kw, G).permute(0, 2, 1, 3).reshape(C * kw * kh, G)
+        gW, gS = kmat(gW), kmat(gS)
+    out = [t.cpu().numpy() for t in (gW, gb, gS, bS)]
+    return (out[0].astype(np.float32), out[1].astype(np.float32)), (out[2], out[3])
+
+
 def _rows(t, rows):
     if rows is None:
         return host(t)
@@ -75,25 +123,32 @@ def _rows(t, rows):
     return host(t.index_select(0, idx))
 
 
-def run_step(kc, config, net, x, dy, rows=None):
+def run_step(kc, config, net, x, dy, rows=None, keep=False):
     """The training step on the GPU; returns the oracle layers (parameters
     before the step), the layers' outputs and input derivatives (sampled
-    rows) and the parameters after."""
+    rows), the parameters after and, with `keep`, device copies of every
+    layer's whole output and input derivative."""
     n = net.NumComponents()
     before = oracle_layers(config, net, kc)
     net.Propagate(x)
     # outputs first: a fused conv's output is recomputed on request, which is
     # possible until its backprop runs
+    full_o = [net.Output(i).clone() for i in range(n)] if keep else None
     outs = [_rows(net.Output(i), rows) for i in range(n)]
     net.Backprop(dy)
+    full_d = [net.InputDeriv(i).clone() for i in range(n)] if keep else None
     derivs = [_rows(net.InputDeriv(i), rows) for i in range(n)]
     after = [[host(c.GetParam(w)) for w in (kc.PARAM_LINEAR, kc.PARAM_BIAS, kc.PARAM_PREV_GRAD)]
              if c.NumGradientParams() > 0 else None for c in net.components]
-    return before, outs, derivs, after
+    return before, outs, derivs, after, (full_o, full_d)
 
 
-def check_step(kc, config, net, x, dy, rows=None, what=""):
-    layers, outs, derivs, after = run_step(kc, config, net, x, dy, rows)
+def check_step(kc, config, net, x, dy, rows=None, what="", update=True):
+    """One step checked layer by layer; with `rows`, the row-local checks on
+    those rows and (update=True) the updates against device_gradient."""
+    keep = rows is not None and update
+    layers, outs, derivs, after, (full_o, full_d) = run_step(kc, config, net, x, dy, rows,
+                                                            keep=keep)
     xin = _rows(x, rows)
     dout = _rows(dy, rows)
     ins = [xin] + outs[:-1]
@@ -110,11 +165,16 @@ def check_step(kc, config, net, x, dy, rows=None, what=""):
         assert_bound(y, y_t, y_s, what=f"{tag} Propagate")
         dx_t, dx_s = truth(lambda: oc.backprop(a, d_next[i], update=False))
         assert_bound(derivs[i], dx_t, dx_s, what=f"{tag} dX")
-        if rows is not None:
+        if rows is not None and not update:
             continue
         # the update: W' = W + m*prev - lr*wd*W + lr*gW (bias: b + lr*gb), lr
         # divided by the rows of the step (B10)
-        (gW_t, gb_t), (gW_s, gb_s) = truth(lambda: oc.gradient(a, d_next[i]))
+        if rows is None:
+            (gW_t, gb_t), (gW_s, gb_s) = truth(lambda: oc.gradient(a, d_next[i]))
+        else:
+            a_full = x if i == 0 else full_o[i - 1]
+            d_full = dy if i == len(layers) - 1 else full_d[i + 1]
+            (gW_t, gb_t), (gW_s, gb_s) = device_gradient(oc, a_full, d_full)
         W0, b0, p0 = oc.W.copy(), oc.b.copy(), oc.prev.copy()
         with O.accum(1):
             oc.apply(gW_t, gb_t, N)

@@ -279,14 +279,17 @@ C2_FC = [("fc_fwd", 4096, 1024, 11616, False, True),
 @pytest.mark.parametrize("name,m,n,k,ta,tb", C2_FC, ids=[c[0] for c in C2_FC])
 @pytest.mark.parametrize("side", ["row", "col"])
 @pytest.mark.parametrize("spread", [24, 28, 32])
-def test_gemm_f16x3_intra_group_range(kc, name, m, n, k, ta, tb, side, spread):
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_gemm_f16x3_intra_group_range(kc, name, m, n, k, ta, tb, side, spread, beta):
     """The f16x3 scale is one power of two per row of op(A) / column of
     op(B), set by the group's largest element; elements far below it lose
     their low part (an f16 subnormal).  Here one row of op(A) (side "row") or
     one column of op(B) ("col") is N(0,1) * 2^-spread except one element of
     size 1 whose partner in the other operand is 0 for every output: the
     small elements carry all of S, and the elementwise 1e-5 * S bar must
-    hold.  c2's FC shapes, all three transposes."""
+    hold.  c2's FC shapes, all three transposes; beta 1
+    as in the nnet2 AffineComponent update (the staged epilogue
+    of a one-split tile once applied beta twice to a rejected element)."""
     import torch
     a, b, c0 = _mats(torch, m, n, k, ta, tb, seed=31)
     A = a.t() if ta else a
@@ -311,8 +314,9 @@ def test_gemm_f16x3_intra_group_range(kc, name, m, n, k, ta, tb, side, spread):
     else:
         A[2, :] = 0.0
     c = c0.clone()
-    _gemm_mode(kc, 2, lambda: kc.gemm(a, b, c, ta, tb, 1.0, 0.0))
+    _gemm_mode(kc, 2, lambda: kc.gemm(a, b, c, ta, tb, 1.0, beta))
     torch.cuda.synchronize()
-    _bound(torch, a, b, c0, c, ta, tb, 1.0, 0.0)
+    _bound(torch, a, b, c0, c, ta, tb, 1.0, beta)
     zero = c[:, 1] if side == "row" else c[2, :]
-    assert bool((zero == 0).all()), zero
+    want = (c0[:, 1] if side == "row" else c0[2, :]) * beta
+    assert torch.equal(zero, want), zero

@@ -2471,8 +2471,28 @@ static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
       const size_t need = kcnn_conv_bwd_frame_ws(g);
       if (need == 0 || ws == nullptr || ws_bytes < need) return -1;
     }
-    int rc = kcnn_conv_bwd_x6(g, X, xs, dY, dys, K, ks, dX, dxs, gW ? part : nullptr, S,
-                              dx_acc, st, pmask, pms, pc, ph, bdbg);
+    // The gradient's bf16-MFMA accumulation chains are kept to 16 frames per
+    // workgroup: a longer chain grows its error linearly with the frames
+    // (c2 stack, prev' normwise against fp64: 2.6e-6 at 4096 frames, 9.2e-6
+    // at 16384, 3.8e-5 at 65536; an fp32 contraction 1.5e-6 at each;
+    // experiments/diag_wgrad_acc.py).  Larger batches run as launches over
+    // frame ranges of at most BWD_X6_FRAMES, each workgroup adding its range's
+    // partial to its slot in fp32 (fixed order: deterministic).
+    constexpr int BWD_X6_FRAMES = 4096;
+    const int nch = gW != nullptr ? (g.R + BWD_X6_FRAMES - 1) / BWD_X6_FRAMES : 1;
+    int rc = 0;
+    for (int c = 0; c < nch && !rc; ++c) {
+      const int r0 = (int)((int64_t)g.R * c / nch), r1 = (int)((int64_t)g.R * (c + 1) / nch);
+      ConvGeom gc = g;
+      gc.R = r1 - r0;
+      gc.M = (int64_t)gc.R * g.P;
+      // every range holds at least 2048 frames (nch > 1), so the same S slots
+      rc = kcnn_conv_bwd_x6(gc, X ? X + (int64_t)r0 * xs : X, xs, dY + (int64_t)r0 * dys, dys,
+                            K, ks, dX ? dX + (int64_t)r0 * dxs : dX, dxs, gW ? part : nullptr,
+                            nch > 1 ? (int)frame_grid(gc, 1) : S, dx_acc, st,
+                            pmask ? pmask + (int64_t)r0 * pms : pmask, pms, pc, ph,
+                            bdbg | (c > 0 ? 1 << 30 : 0));
+    }
     if (rc || gW == nullptr) return rc;
     hipLaunchKernelGGL(reduce_splits_kernel, dim3((E + 63) / 64), dim3(256), 0, st, part, S,
                        E, g.Kdim * g.G, g.G, 0, gW, gws, gb);

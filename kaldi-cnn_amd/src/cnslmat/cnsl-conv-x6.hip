@@ -543,7 +543,8 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6_kernel(
         float sum = 0.0f;
 #pragma unroll
         for (int w = 0; w < 4; w++) sum += red[w * 1024 + e];
-        dst[i * g.G + ch * 32 + j] = sum;
+        // (dbg bit 30: add to the partial an earlier frame range left there)
+        dst[i * g.G + ch * 32 + j] = (dbg & (1 << 30)) ? dst[i * g.G + ch * 32 + j] + sum : sum;
       }
     }
   };
@@ -1060,7 +1061,8 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6p_kernel(
         float sum = 0.0f;
 #pragma unroll
         for (int w = 0; w < 4; w++) sum += red[w * 1024 + e];
-        dst[i * g.G + ch * 32 + j] = sum;
+        // (dbg bit 30: add to the partial an earlier frame range left there)
+        dst[i * g.G + ch * 32 + j] = (dbg & (1 << 30)) ? dst[i * g.G + ch * 32 + j] + sum : sum;
       }
     }
   };
@@ -1670,7 +1672,8 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6q_kernel(
         float sum = 0.0f;
 #pragma unroll
         for (int w = 0; w < 4; w++) sum += red[w * 1024 + e];
-        dst[i * g.G + ch * 32 + j] = sum;
+        // (dbg bit 30: add to the partial an earlier frame range left there)
+        dst[i * g.G + ch * 32 + j] = (dbg & (1 << 30)) ? dst[i * g.G + ch * 32 + j] + sum : sum;
       }
     }
   };

@@ -101,6 +101,28 @@ struct GemmF16Args {
   float alpha, beta;
 };
 
+// Logical workgroup id -> (split, tile row, tile column).  The splits of a
+// tile are consecutive; the tiles go in groups of GM tile rows, column-major
+// inside a group, so the 32 workgroups an XCD runs at once (consecutive ids,
+// XCD-aware order in the kernels) cover about GM x 32 / (GM ksplit) tiles
+// sharing GM row panels of op(A) and a few column panels of op(B) in that
+// XCD's L2, instead of one row panel and 32 column panels (c2's data
+// gradient: an XCD wave then reads 8 MB of operand panels instead of 17)
+#ifndef KCNN_GEMM_GM
+#define KCNN_GEMM_GM 4
+#endif
+__device__ __forceinline__ void tile_of(const GemmF16Args &p, int lid, int &split, int &tm,
+                                        int &tn) {
+  split = lid % p.ksplit;
+  const int t = lid / p.ksplit;
+  const int gsz = KCNN_GEMM_GM * p.tiles_n;
+  const int g = t / gsz, r = t - g * gsz;
+  const int m0 = g * KCNN_GEMM_GM;
+  const int gm = min(p.tiles_m - m0, KCNN_GEMM_GM);
+  tm = m0 + r % gm;
+  tn = r / gm;
+}
+
 __device__ __forceinline__ int swz(int r, int c) {
   return r * ROWB + ((c ^ ((r >> 2) & 3)) << 4);
 }
@@ -653,9 +675,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
   const int nb = gridDim.x, b = blockIdx.x;
   const int xcd = b & 7, q = nb >> 3, rr = nb & 7;
   const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
-  const int split = lid % p.ksplit;
-  const int rest = lid / p.ksplit;
-  const int tn = rest % p.tiles_n, tm = rest / p.tiles_n;
+  int split, tm, tn;
+  tile_of(p, lid, split, tm, tn);
   const int row0 = tm * BM, col0 = tn * BN;
   const int kbeg = split * p.kps;
   const int kend = min(p.K, kbeg + p.kps);
@@ -799,9 +820,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
   const int nb = gridDim.x, b = blockIdx.x;
   const int xcd = b & 7, q = nb >> 3, rr = nb & 7;
   const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
-  const int split = lid % p.ksplit;
-  const int rest = lid / p.ksplit;
-  const int tn = rest % p.tiles_n, tm = rest / p.tiles_n;
+  int split, tm, tn;
+  tile_of(p, lid, split, tm, tn);
   const int row0 = tm * BM, col0 = tn * BN;
   const int kbeg = split * p.kps;
   const int kend = min(p.K, kbeg + p.kps);
@@ -852,6 +872,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
     acc[i][j] = mfma(fa[i][PA[pr]], fb[j][PB[pr]], acc[i][j]);
   };
 
+  // waves 4-7 (each SIMD's second wave) at priority 1 for the whole kernel
+  // (MI355X_MICROARCH.md, two waves per SIMD, item 4: the younger half loses
+  // every VALU arbitration otherwise)
+#ifndef KCNN_GEMM_PRIO
+#define KCNN_GEMM_PRIO 1
+#endif
+  if (KCNN_GEMM_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
   // the first two K tiles' loads go out before the tile's scales are read
   // (the split needs both; the scales' loads and barriers then pass under
   // the tiles' latency: c2's data gradient 400 -> 381 us at K 1024 without
@@ -1133,24 +1160,42 @@ __device__ __forceinline__ void stats_cols(const StatOp &o, int blk) {
     }
 }
 
-__global__ __launch_bounds__(256) void stats_kernel(StatOp a, StatOp b) {
+// Up to three statistics passes in one launch (their blocks in order): a
+// GEMM's two operands, or the FC backward's output derivative (rows and
+// columns) and weight columns (kl_gemm_stats3)
+struct StatOps {
+  StatOp o[3];
+};
+// the op of block `blk` among the ops' `count(o)` blocks, and its block index there
+template <typename Count>
+__device__ __forceinline__ int pick_op(const StatOps &s, int blk, Count count, int &local) {
+  const int n0 = count(s.o[0]), n1 = count(s.o[1]);
+  if (blk < n0) { local = blk; return 0; }
+  if (blk < n0 + n1) { local = blk - n0; return 1; }
+  local = blk - n0 - n1;
+  return 2;
+}
+__host__ __device__ inline int ncount_blocks(const StatOp &o);
+__host__ __device__ inline int nfinal_blocks(const StatOp &o) {
+  return o.mode == 1 && o.blocks ? o.fblocks : 0;
+}
+
+__global__ __launch_bounds__(256) void stats_kernel(StatOps s) {
   __shared__ uint32_t red[12];
-  if (a.clear && blockIdx.x == 0 && threadIdx.x < 2) a.clear[threadIdx.x] = 0u;
-  const bool isa = (int)blockIdx.x < a.blocks;  // uniform
-  const StatOp &o = isa ? a : b;
-  const int blk = isa ? blockIdx.x : blockIdx.x - a.blocks;
+  if (s.o[0].clear && blockIdx.x == 0 && threadIdx.x < 2) s.o[0].clear[threadIdx.x] = 0u;
+  int blk;
+  const int w = pick_op(s, blockIdx.x, [](const StatOp &o) { return o.blocks; }, blk);
+  const StatOp &o = s.o[w];  // (uniform)
   if (o.mode == 0) stats_rows(o, blk, red);
   else stats_cols(o, blk);
 }
 
 // The column maxima / minima over the partials (64 columns per block, 4
 // groups of partials through LDS); the counts zeroed for stats_count_kernel.
-__global__ __launch_bounds__(256) void stats_finalize_kernel(StatOp a, StatOp b) {
+__global__ __launch_bounds__(256) void stats_finalize_kernel(StatOps s) {
   __shared__ uint32_t red[2][4][64];
-  const int fa = a.mode == 1 ? a.fblocks : 0;
-  const bool isa = (int)blockIdx.x < fa;
-  const StatOp &o = isa ? a : b;
-  const int blk = isa ? blockIdx.x : blockIdx.x - fa;
+  int blk;
+  const StatOp &o = s.o[pick_op(s, blockIdx.x, [](const StatOp &q) { return nfinal_blocks(q); }, blk)];
   const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blk * 64 + lane;
   uint32_t m = 0, n = 0xffffffffu;
@@ -1194,12 +1239,12 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(StatOp a, StatOp b)
 // spread column's count of small elements by an integer atomic (exact and
 // order-independent).
 constexpr int CNT_ROWS = 64;
-__global__ __launch_bounds__(256) void stats_count_kernel(StatOp a, StatOp b) {
-  const int na = a.mode == 1 && a.blocks ? ((a.cols + 63) / 64) * ((a.rows + CNT_ROWS - 1) / CNT_ROWS)
-                                         : 0;
-  const bool isa = (int)blockIdx.x < na;
-  const StatOp &o = isa ? a : b;
-  const int blk = isa ? blockIdx.x : blockIdx.x - na;
+__host__ __device__ inline int ncount_blocks(const StatOp &o) {
+  return o.mode == 1 && o.blocks ? ((o.cols + 63) / 64) * ((o.rows + CNT_ROWS - 1) / CNT_ROWS) : 0;
+}
+__global__ __launch_bounds__(256) void stats_count_kernel(StatOps s) {
+  int blk;
+  const StatOp &o = s.o[pick_op(s, blockIdx.x, [](const StatOp &q) { return ncount_blocks(q); }, blk)];
   const int ncb = (o.cols + 63) / 64;
   const int cb = blk % ncb, rc = blk / ncb;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1255,32 +1300,35 @@ size_t stat_part_words(int rows, int cols, int mode) {
   const StatOp o = stat_op(nullptr, rows, cols, cols, 1, nullptr, nullptr);
   return 2 * (size_t)o.rbk * cols;
 }
-int stats_launch(const StatOp &a, const StatOp &b, hipStream_t st) {
+int stats_launch3(const StatOps &ops, hipStream_t st) {
   // empty operands: maxima 0 (no scale), minima 0 (no nonzero element)
-  for (const StatOp *o : {&a, &b})
-    if (o->blocks == 0 && o->out) {
-      const size_t n = o->mode == 0 ? (size_t)std::max(o->rows, 0) : (size_t)std::max(o->cols, 0);
-      if (n && hipMemsetAsync(o->out, 0, 3 * n * 4, st) != hipSuccess) return (int)hipGetLastError();
+  for (const StatOp &o : ops.o)
+    if (o.blocks == 0 && o.out) {
+      const size_t n = o.mode == 0 ? (size_t)std::max(o.rows, 0) : (size_t)std::max(o.cols, 0);
+      if (n && hipMemsetAsync(o.out, 0, 3 * n * 4, st) != hipSuccess) return (int)hipGetLastError();
     }
-  const int nb = a.blocks + b.blocks;
+  int nb = 0, nf = 0, nc = 0;
+  for (const StatOp &o : ops.o) {
+    nb += o.blocks;
+    nf += nfinal_blocks(o);
+    nc += ncount_blocks(o);
+  }
   if (nb == 0) return 0;
-  hipLaunchKernelGGL(stats_kernel, dim3(nb), dim3(256), 0, st, a, b);
+  hipLaunchKernelGGL(stats_kernel, dim3(nb), dim3(256), 0, st, ops);
   int rc = kcnn::launch_status();
-  if (rc) return rc;
-  const int nf = (a.mode == 1 && a.blocks ? a.fblocks : 0) + (b.mode == 1 && b.blocks ? b.fblocks : 0);
-  if (nf == 0) return 0;
-  StatOp a2 = a, b2 = b;
-  if (a2.blocks == 0) a2.mode = 0;  // nothing to finalize
-  if (b2.blocks == 0) b2.mode = 0;
-  hipLaunchKernelGGL(stats_finalize_kernel, dim3(nf), dim3(256), 0, st, a2, b2);
+  if (rc || nf == 0) return rc;
+  hipLaunchKernelGGL(stats_finalize_kernel, dim3(nf), dim3(256), 0, st, ops);
   rc = kcnn::launch_status();
   if (rc) return rc;
-  auto ncnt = [](const StatOp &o) {
-    return o.mode == 1 && o.blocks ? ((o.cols + 63) / 64) * ((o.rows + CNT_ROWS - 1) / CNT_ROWS)
-                                   : 0;
-  };
-  hipLaunchKernelGGL(stats_count_kernel, dim3(ncnt(a2) + ncnt(b2)), dim3(256), 0, st, a2, b2);
+  hipLaunchKernelGGL(stats_count_kernel, dim3(nc), dim3(256), 0, st, ops);
   return kcnn::launch_status();
+}
+int stats_launch(const StatOp &a, const StatOp &b, hipStream_t st) {
+  StatOps ops;
+  ops.o[0] = a;
+  ops.o[1] = b;
+  ops.o[2] = StatOp{};
+  return stats_launch3(ops, st);
 }
 
 // C = alpha * sum_s part[s] + beta * C, the splits added in increasing s
@@ -1650,6 +1698,33 @@ extern "C" int kl_absmax_rows_cols(const float *R, int rows, int cols, int ld, u
     if (e != hipSuccess) return (int)e;
   }
   return stats_launch(q, r, kcnn::as_stream(stream));
+}
+
+// Up to three statistics passes in one set of launches (stats, finalize,
+// count): op i over X_i (rows_i x cols_i, pitch ld_i), per row (mode_i 0)
+// or per column (1, part_i: kl_absmax_cols_words of scratch) into the block
+// out_i; X_i NULL skips op i.  The FC backward's output derivative (rows for
+// the data gradient, columns for the weight gradient) and weight columns in
+// one pass set instead of two (AffineComponent::Backprop).
+extern "C" int kl_gemm_stats3(const float *X0, int rows0, int cols0, int ld0, int mode0,
+                              uint32_t *out0, uint32_t *part0, const float *X1, int rows1,
+                              int cols1, int ld1, int mode1, uint32_t *out1, uint32_t *part1,
+                              const float *X2, int rows2, int cols2, int ld2, int mode2,
+                              uint32_t *out2, uint32_t *part2, kcnn_stream_t stream) {
+  StatOps ops;
+  const float *X[3] = {X0, X1, X2};
+  const int rows[3] = {rows0, rows1, rows2}, cols[3] = {cols0, cols1, cols2};
+  const int ld[3] = {ld0, ld1, ld2}, mode[3] = {mode0, mode1, mode2};
+  uint32_t *out[3] = {out0, out1, out2}, *part[3] = {part0, part1, part2};
+  for (int i = 0; i < 3; ++i) {
+    ops.o[i] = StatOp{};
+    if (!X[i]) continue;
+    if (rows[i] < 0 || cols[i] < 0 || ld[i] < cols[i] || !out[i] || (mode[i] != 0 && mode[i] != 1) ||
+        (mode[i] == 1 && rows[i] > 0 && cols[i] > 0 && !part[i]))
+      return (int)hipErrorInvalidValue;
+    ops.o[i] = stat_op(X[i], rows[i], cols[i], ld[i], mode[i], out[i], mode[i] ? part[i] : nullptr);
+  }
+  return stats_launch3(ops, kcnn::as_stream(stream));
 }
 
 // C[M x N] = alpha * op(A) op(B) + beta * C with the operands' max |x| given:

@@ -272,6 +272,32 @@ const CuGemmStatsHint *CuGemmStatsHint::Find(const float *data, MatrixIndexT row
   return nullptr;
 }
 
+CuGemmBackpropStats::CuGemmBackpropStats(const CuMatrixBase<float> &dy,
+                                         const CuMatrixBase<float> &W, bool cols) {
+  CuDevice &dev = CuDevice::Instantiate();
+  const int N = dy.NumRows(), O = dy.NumCols(), I = W.NumCols();
+  if (dev.GemmMode() != 2 || N == 0 || O == 0 || I == 0 || W.NumRows() != O) return;
+  // blocks [max, min, cnt]: dy rows (N), dy columns (O), W columns (I), then
+  // the column partials
+  const size_t pd = cols ? kl_absmax_cols_words(N, O) : 0, pw = kl_absmax_cols_words(O, I);
+  const size_t words = 3 * ((size_t)N + O + I) + pd + pw;
+  ws_ = dev.Malloc(words * 4);
+  uint32_t *rows_d = static_cast<uint32_t *>(ws_), *cols_d = rows_d + 3 * (size_t)N,
+           *cols_w = cols_d + 3 * (size_t)O, *part_d = cols_w + 3 * (size_t)I,
+           *part_w = part_d + pd;
+  CNSL_SAFE_CALL(kl_gemm_stats3(dy.Data(), N, O, dy.Stride(), 0, rows_d, nullptr,
+                                cols ? dy.Data() : nullptr, N, O, dy.Stride(), 1, cols_d, part_d,
+                                W.Data(), O, I, W.Stride(), 1, cols_w, part_w,
+                                reinterpret_cast<kcnn_stream_t>(dev.Stream())));
+  hint_d_ = new CuGemmStatsHint(dy.Data(), N, O, dy.Stride(), rows_d, cols ? cols_d : nullptr);
+  hint_w_ = new CuGemmStatsHint(W.Data(), O, I, W.Stride(), nullptr, cols_w);
+}
+CuGemmBackpropStats::~CuGemmBackpropStats() {
+  delete hint_w_;
+  delete hint_d_;
+  if (ws_) CuDevice::Instantiate().Free(ws_);
+}
+
 // The f16x3 product (mode 2) of aligned operands Ap, Bp (A, B themselves, or
 // their padded copies; A and B name the operands for the statistics hints),
 // plus bias[j] on every row when bias != NULL.  False when the kernel

@@ -336,6 +336,28 @@ class CuGemmStatsHint {
   const CuGemmStatsHint *prev_;
 };
 
+/// The statistics of an affine layer's backward GEMMs in one launch set
+/// (kl_gemm_stats3) -- out_deriv's rows (the data gradient's op(A)),
+/// linear_params' columns (its op(B)) and, with `cols`, out_deriv's columns
+/// (the weight gradient's op(A) = out_deriv^T) -- offered to those AddMatMat
+/// calls as CuGemmStatsHint while in scope; without it each GEMM takes its
+/// own statistics pass, two for the pair (three kernels each).  Does nothing
+/// unless AddMatMat runs the f16x3 engine on these operands.  The caller
+/// keeps out_deriv and linear_params unmodified while it is in scope (the
+/// weight update itself is fine: the weight-gradient GEMM reads neither).
+class CuGemmBackpropStats {
+ public:
+  CuGemmBackpropStats(const CuMatrixBase<float> &out_deriv, const CuMatrixBase<float> &linear,
+                      bool cols);
+  ~CuGemmBackpropStats();
+  CuGemmBackpropStats(const CuGemmBackpropStats &) = delete;
+  CuGemmBackpropStats &operator=(const CuGemmBackpropStats &) = delete;
+
+ private:
+  void *ws_ = nullptr;
+  CuGemmStatsHint *hint_d_ = nullptr, *hint_w_ = nullptr;  // destroyed in reverse order
+};
+
 /// Host N(0,1) generator shared by SetRandn (splitmix64 -> Box-Muller).
 void RandnFill(float *dst, size_t n);
 void SetRandnSeed(uint64_t seed);

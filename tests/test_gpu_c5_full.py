@@ -38,7 +38,8 @@ B = 4096
 
 def _sample_rows(extra=()):
     r = np.linspace(0, B - 1, 56).astype(np.int64)
-    return np.unique(np.concatenate([r, [0, 1, B - 3, B - 2, B - 1], list(extra)]))
+    return np.unique(np.concatenate([r, np.array([0, 1, B - 3, B - 2, B - 1] + list(extra),
+                                                  dtype=np.int64)]))
 
 
 def test_c5_sampled_rows(kc):
@@ -55,6 +56,8 @@ def test_c5_sampled_rows(kc):
     try:
         check_step(kc, cfg, net, x, dy, rows=_sample_rows(), what="c5@4096")
         calls, tiles, elems = kc.conv_fix_counts()
+        print(f"\nc5@4096: {calls} f16x3 calls, {tiles} tiles and {elems} elements "
+              "recomputed in fp32")
         # C2, C3 forward, C3 data gradient, C2's 1x1 data gradient (plus the
         # outputs recomputed on request for the check)
         assert calls >= 4, (calls, tiles, elems)
@@ -111,6 +114,8 @@ def test_c3_pool_adversarial(kc):
     try:
         check_step(kc, cfg, net, x, dp, rows=rows, what="C3->P2 adversarial")
         calls, tiles, elems = kc.conv_fix_counts()
+        print(f"\nC3->P2 adversarial: {calls} f16x3 calls, {tiles} tiles and {elems} "
+              "elements recomputed in fp32")
         assert calls >= 2, (calls, tiles, elems)      # forward and data gradient
         assert tiles > 0, (calls, tiles, elems)       # conv_igemm_fixup_kernel
         assert elems > 0, (calls, tiles, elems)       # conv_igemm_efix_kernel

@@ -1483,7 +1483,7 @@ __global__ __launch_bounds__(256) void gemm_f16x3_reduce_kernel(GemmF16Args p, i
 constexpr int FIX_DEPTH = 16;
 // the fixup's grid: a flagged call's groups take the workgroups in turn
 // (c2's weight-gradient shape with 32 spread rows, 1452 groups: +925 us at
-// 128 workgroups, experiments/fixup_storm.py); an unflagged call exits at the
+// 128 workgroups, measured r05 by a one-off driver); an unflagged call exits at the
 // first load, and the launch costs the same 4.4 us at 128 or 1024
 constexpr int FIX_GRID = 1024;
 __global__ __launch_bounds__(256) void gemm_f16x3_fixup_kernel(GemmF16Args p, int a_kc,

@@ -64,10 +64,18 @@ struct kcnn_nnet {
   std::vector<uint32_t *> fstat;
   std::vector<size_t> fstat_words;
   std::vector<char> fstat_valid;
+  // fwd[i]'s column statistics left pending by the fused forward (the next
+  // component's FC backward runs them, pool-stats.h PoolColDeferred) and the
+  // forward's per-workgroup column partials they read, kept until then
+  std::vector<PoolColDeferred> fdefer;
+  std::vector<void *> fpart;
+  std::vector<size_t> fpart_bytes;
   ~kcnn_nnet() {
     for (auto *m : mask)
       if (m) CuDevice::Instantiate().Free(m);
     for (auto *f : fstat)
+      if (f) CuDevice::Instantiate().Free(f);
+    for (auto *f : fpart)
       if (f) CuDevice::Instantiate().Free(f);
     for (auto *c : comps) delete c;
   }
@@ -658,6 +666,9 @@ kcnn_nnet *kcnn_nnet_new(const char *config) {
     n->fstat.assign(n->comps.size() + 1, nullptr);
     n->fstat_words.assign(n->comps.size() + 1, 0);
     n->fstat_valid.assign(n->comps.size() + 1, 0);
+    n->fdefer.assign(n->comps.size() + 1, PoolColDeferred{});
+    n->fpart.assign(n->comps.size() + 1, nullptr);
+    n->fpart_bytes.assign(n->comps.size() + 1, 0);
     n->deriv_deferred.assign(n->comps.size(), 0);
   });
   return rc ? nullptr : n.release();
@@ -687,9 +698,11 @@ static void size_output(CuMatrix<BaseFloat> *m, int rows, int cols) {
 static std::unique_ptr<CuGemmStatsHint> input_stats(const kcnn_nnet *n, size_t i) {
   if (i >= n->fstat_valid.size() || !n->fstat_valid[i]) return nullptr;
   const CuMatrix<BaseFloat> &x = n->fwd[i];
-  return std::unique_ptr<CuGemmStatsHint>(new CuGemmStatsHint(
+  std::unique_ptr<CuGemmStatsHint> h(new CuGemmStatsHint(
       x.Data(), x.NumRows(), x.NumCols(), x.Stride(), n->fstat[i],
       n->fstat[i] + 3 * (size_t)x.NumRows()));
+  if (n->fdefer[i].pending) h->pending = const_cast<PoolColDeferred *>(&n->fdefer[i]);
+  return h;
 }
 
 // Component i (Conv) and i+1 (channel-only Maxpool) in one fused pass;
@@ -723,7 +736,12 @@ static bool propagate_pair(kcnn_nnet *n, size_t i) {
                               conv->Kernel_height(), conv->Kernel_width(), conv->Group(),
                               pool->FusableChannelPool())
                         : 0;
-  CuScratch part(pw * 4);
+  if (pw && n->fpart_bytes[i + 2] < pw * 4) {  // kept: the column work may run in the backward
+    if (n->fpart[i + 2]) CuDevice::Instantiate().Free(n->fpart[i + 2]);
+    n->fpart[i + 2] = CuDevice::Instantiate().Malloc(pw * 4);
+    n->fpart_bytes[i + 2] = pw * 4;
+  }
+  n->fdefer[i + 2].pending = 0;
   if (pw) {
     const size_t need = 3 * ((size_t)rows + pool->OutputDim());
     if (n->fstat_words[i + 2] < need) {
@@ -733,12 +751,15 @@ static bool propagate_pair(kcnn_nnet *n, size_t i) {
     }
     ps.rowmax = n->fstat[i + 2];
     ps.colmax = n->fstat[i + 2] + 3 * (size_t)rows;
-    ps.partials = static_cast<uint32_t *>(part.p);
+    ps.partials = static_cast<uint32_t *>(n->fpart[i + 2]);
     ps.partial_words = pw;
   }
-  if (!conv->PropagateMaxpool(n->fwd[i], &n->fwd[i + 1], *pool, &n->fwd[i + 2],
-                              n->mask[i + 1], pool->OutputDim(), store, pw ? &ps : nullptr))
-    return false;
+  {
+    PoolColDeferScope defer(pw ? &n->fdefer[i + 2] : nullptr);
+    if (!conv->PropagateMaxpool(n->fwd[i], &n->fwd[i + 1], *pool, &n->fwd[i + 2],
+                                n->mask[i + 1], pool->OutputDim(), store, pw ? &ps : nullptr))
+      return false;
+  }
   n->fstat_valid[i + 2] = ps.produced;
   n->mask_valid[i + 1] = 1;
   n->out_stale[i + 1] = !store;
@@ -774,6 +795,7 @@ int kcnn_nnet_propagate(kcnn_nnet *n, const float *in, MatrixDim in_dim) {
     std::fill(n->out_stale.begin(), n->out_stale.end(), 0);
     std::fill(n->deriv_deferred.begin(), n->deriv_deferred.end(), 0);
     std::fill(n->fstat_valid.begin(), n->fstat_valid.end(), 0);
+    for (auto &d : n->fdefer) d.pending = 0;
     for (size_t i = 0; i < n->comps.size(); i++) {
       if (propagate_pair(n, i) || propagate_relu_pair(n, i)) { i++; continue; }
       ChunkInfo ii = nnet_in_info(n, i), oi = nnet_out_info(n, i);

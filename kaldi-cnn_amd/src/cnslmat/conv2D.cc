@@ -8,8 +8,18 @@
 #include <algorithm>
 
 #include "cnsl-hip-kernels.h"
+#include "pool-stats.h"
 #include "../kaldi-lite/cu-device.h"
 #include "../kaldi-lite/cu-matrix.h"
+
+// kcnn_pool_defer_request's request of this thread (pool-stats.h)
+static thread_local PoolColDeferred *t_pool_defer = nullptr;
+PoolColDeferred *kcnn_pool_defer_request(PoolColDeferred *d) {
+  PoolColDeferred *prev = t_pool_defer;
+  t_pool_defer = d;
+  return prev;
+}
+PoolColDeferred *kcnn_pool_defer_current() { return t_pool_defer; }
 
 namespace kaldi {
 

@@ -46,4 +46,33 @@ size_t kcnn_conv2d_maxpool_stats_words(int rows, int in_height, int in_width,
                                        int group, int pool_channel_dim);
 }
 
+// The pooled output's column statistics (the maxima from the forward's
+// exponent bytes, then the small elements' minima and counts: two small
+// kernels) left to their consumer instead of launched by the forward.  The
+// only reader of the column block is the FC weight-gradient GEMM, which runs
+// in the backward; the FC backward's statistics launches take this work
+// over (kl_gemm_stats3), and any other f16x3 GEMM that reads the column
+// block first completes it (kcnn_pool_cols_complete).  The exponent bytes
+// must live until then (the runtime keeps them per layer).
+struct PoolColDeferred {
+  const uint8_t *pcol = nullptr;  // exponent bytes [nblk][npool]
+  int nblk = 0, npool = 0;
+  const float *P = nullptr;       // the pooled output (suspect frames' rows)
+  int ps = 0, R = 0, vec = 0;
+  uint32_t *rowblk = nullptr, *colblk = nullptr;  // the statistics blocks
+  int pending = 0;
+};
+// While a request is set on this thread, the fused forward that writes the
+// statistics (kcnn_conv2d_maxpool_stats) fills it and sets pending instead
+// of launching the column kernels.  Returns the previous request.
+PoolColDeferred *kcnn_pool_defer_request(PoolColDeferred *d);
+PoolColDeferred *kcnn_pool_defer_current();
+// The column kernels of a pending request (pending -> 0); 0 or a HIP error.
+int kcnn_pool_cols_complete(PoolColDeferred *d, kcnn_stream_t stream);
+struct PoolColDeferScope {
+  explicit PoolColDeferScope(PoolColDeferred *d) : prev(kcnn_pool_defer_request(d)) {}
+  ~PoolColDeferScope() { kcnn_pool_defer_request(prev); }
+  PoolColDeferred *prev;
+};
+
 #endif  // KCNN_CNSLMAT_POOL_STATS_H_

@@ -59,10 +59,16 @@
 #include "cnslmat/f16-split.h"
 #include "cnslmat/hip-util.h"
 #include "cnslmat/momentum-step.h"
+#include "cnslmat/pool-stats-dev.h"
+#include "cnslmat/pool-stats.h"
 #include "kaldi-lite/cu-kernels-lite.h"
 
 namespace {
 
+using kcnn::COLMAX_ROWS;
+using kcnn::PoolCountSmem;
+using kcnn::pool_colmax_block;
+using kcnn::pool_count_block;
 using kcnn::f16x3::f16x8;
 using kcnn::f16x3::f32x16;
 using kcnn::f16x3::NONFINITE;
@@ -1165,6 +1171,11 @@ __device__ __forceinline__ void stats_cols(const StatOp &o, int blk) {
 // columns) and weight columns (kl_gemm_stats3)
 struct StatOps {
   StatOp o[3];
+  // a fused pool's pending column statistics (pool-stats-dev.h): pcx x pcy
+  // colmax blocks after the ops' blocks in stats_kernel, pcn count blocks
+  // after the finalize blocks in stats_finalize_kernel (0: none)
+  PoolColDeferred pc;
+  int pcx, pcy, pcn;
 };
 // the op of block `blk` among the ops' `count(o)` blocks, and its block index there
 template <typename Count>
@@ -1183,6 +1194,12 @@ __host__ __device__ inline int nfinal_blocks(const StatOp &o) {
 __global__ __launch_bounds__(256) void stats_kernel(StatOps s) {
   __shared__ uint32_t red[12];
   if (s.o[0].clear && blockIdx.x == 0 && threadIdx.x < 2) s.o[0].clear[threadIdx.x] = 0u;
+  const int nb3 = s.o[0].blocks + s.o[1].blocks + s.o[2].blocks;
+  if ((int)blockIdx.x >= nb3) {  // (uniform) a pool's column maxima
+    const int k = blockIdx.x - nb3;
+    pool_colmax_block(s.pc.pcol, s.pc.nblk, s.pc.npool, s.pc.colblk, k % s.pcx, k / s.pcx);
+    return;
+  }
   int blk;
   const int w = pick_op(s, blockIdx.x, [](const StatOp &o) { return o.blocks; }, blk);
   const StatOp &o = s.o[w];  // (uniform)
@@ -1194,6 +1211,13 @@ __global__ __launch_bounds__(256) void stats_kernel(StatOps s) {
 // groups of partials through LDS); the counts zeroed for stats_count_kernel.
 __global__ __launch_bounds__(256) void stats_finalize_kernel(StatOps s) {
   __shared__ uint32_t red[2][4][64];
+  __shared__ PoolCountSmem psm;
+  const int nf3 = nfinal_blocks(s.o[0]) + nfinal_blocks(s.o[1]) + nfinal_blocks(s.o[2]);
+  if ((int)blockIdx.x >= nf3) {  // (uniform) a pool's small elements, after its maxima
+    pool_count_block(s.pc.P, s.pc.ps, s.pc.R, s.pc.npool, s.pc.vec, s.pc.rowblk, s.pc.colblk,
+                     blockIdx.x - nf3, s.pcn, psm);
+    return;
+  }
   int blk;
   const StatOp &o = s.o[pick_op(s, blockIdx.x, [](const StatOp &q) { return nfinal_blocks(q); }, blk)];
   const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
@@ -1313,18 +1337,20 @@ int stats_launch3(const StatOps &ops, hipStream_t st) {
     nf += nfinal_blocks(o);
     nc += ncount_blocks(o);
   }
+  nb += ops.pcx * ops.pcy;
+  nf += ops.pcn;
   if (nb == 0) return 0;
   hipLaunchKernelGGL(stats_kernel, dim3(nb), dim3(256), 0, st, ops);
   int rc = kcnn::launch_status();
   if (rc || nf == 0) return rc;
   hipLaunchKernelGGL(stats_finalize_kernel, dim3(nf), dim3(256), 0, st, ops);
   rc = kcnn::launch_status();
-  if (rc) return rc;
+  if (rc || nc == 0) return rc;
   hipLaunchKernelGGL(stats_count_kernel, dim3(nc), dim3(256), 0, st, ops);
   return kcnn::launch_status();
 }
 int stats_launch(const StatOp &a, const StatOp &b, hipStream_t st) {
-  StatOps ops;
+  StatOps ops{};
   ops.o[0] = a;
   ops.o[1] = b;
   ops.o[2] = StatOp{};
@@ -1710,8 +1736,16 @@ extern "C" int kl_gemm_stats3(const float *X0, int rows0, int cols0, int ld0, in
                               uint32_t *out0, uint32_t *part0, const float *X1, int rows1,
                               int cols1, int ld1, int mode1, uint32_t *out1, uint32_t *part1,
                               const float *X2, int rows2, int cols2, int ld2, int mode2,
-                              uint32_t *out2, uint32_t *part2, kcnn_stream_t stream) {
-  StatOps ops;
+                              uint32_t *out2, uint32_t *part2, void *pool_cols,
+                              kcnn_stream_t stream) {
+  StatOps ops{};
+  if (pool_cols) {  // the pool's column kernels' grids (cnsl-conv-frame.hip kcnn_pool_cols_complete)
+    ops.pc = *static_cast<const PoolColDeferred *>(pool_cols);
+    const int ncq = ops.pc.npool % 4 == 0 ? ops.pc.npool / 4 : ops.pc.npool;
+    ops.pcx = (ncq + 255) / 256;
+    ops.pcy = (ops.pc.nblk + COLMAX_ROWS - 1) / COLMAX_ROWS;
+    ops.pcn = std::min(ops.pc.R, 256);
+  }
   const float *X[3] = {X0, X1, X2};
   const int rows[3] = {rows0, rows1, rows2}, cols[3] = {cols0, cols1, cols2};
   const int ld[3] = {ld0, ld1, ld2}, mode[3] = {mode0, mode1, mode2};

@@ -49,11 +49,14 @@ int kl_absmax_rows_cols(const float *R, int rows, int cols, int ld, uint32_t *rm
                         const float *Q, int qrows, int qcols, int ldq, uint32_t *cmax,
                         uint32_t *part, uint32_t *clear, kcnn_stream_t stream);
 /* Up to three statistics passes (rows: mode 0; columns: mode 1 with
-   kl_absmax_cols_words of part) in one launch set; X_i NULL skips op i. */
+   kl_absmax_cols_words of part) in one launch set; X_i NULL skips op i;
+   pool_cols (nullable): a PoolColDeferred (cnslmat/pool-stats.h) whose
+   column kernels run inside the same launches. */
 int kl_gemm_stats3(const float *X0, int rows0, int cols0, int ld0, int mode0, uint32_t *out0,
                    uint32_t *part0, const float *X1, int rows1, int cols1, int ld1, int mode1,
                    uint32_t *out1, uint32_t *part1, const float *X2, int rows2, int cols2,
-                   int ld2, int mode2, uint32_t *out2, uint32_t *part2, kcnn_stream_t stream);
+                   int ld2, int mode2, uint32_t *out2, uint32_t *part2, void *pool_cols,
+                   kcnn_stream_t stream);
 size_t kl_gemm_f16x3_workspace_bytes(int M, int N, int K);
 int kl_gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alpha,
                      const float *A, int lda, const float *B, int ldb, float beta, float *C,

@@ -12,6 +12,7 @@
 
 #include "cu-device.h"
 #include "cu-kernels-lite.h"
+#include "../cnslmat/pool-stats.h"
 #include "kaldi-io.h"
 
 namespace kaldi {
@@ -272,8 +273,15 @@ const CuGemmStatsHint *CuGemmStatsHint::Find(const float *data, MatrixIndexT row
   return nullptr;
 }
 
+// a hint's column block for a GEMM, its pending work run first
+static const uint32_t *hint_cols(const CuGemmStatsHint *h, kcnn_stream_t st) {
+  if (h->pending) CNSL_SAFE_CALL(kcnn_pool_cols_complete(h->pending, st));
+  return h->colmax;
+}
+
 CuGemmBackpropStats::CuGemmBackpropStats(const CuMatrixBase<float> &dy,
-                                         const CuMatrixBase<float> &W, bool cols) {
+                                         const CuMatrixBase<float> &W, bool cols,
+                                         const CuMatrixBase<float> *in) {
   CuDevice &dev = CuDevice::Instantiate();
   const int N = dy.NumRows(), O = dy.NumCols(), I = W.NumCols();
   if (dev.GemmMode() != 2 || N == 0 || O == 0 || I == 0 || W.NumRows() != O) return;
@@ -285,10 +293,19 @@ CuGemmBackpropStats::CuGemmBackpropStats(const CuMatrixBase<float> &dy,
   uint32_t *rows_d = static_cast<uint32_t *>(ws_), *cols_d = rows_d + 3 * (size_t)N,
            *cols_w = cols_d + 3 * (size_t)O, *part_d = cols_w + 3 * (size_t)I,
            *part_w = part_d + pd;
+  // the layer input's pending column statistics (the fused pool's) join these
+  // launches: the weight-gradient GEMM below reads them
+  PoolColDeferred *pc = nullptr;
+  if (cols && in) {
+    const CuGemmStatsHint *h =
+        CuGemmStatsHint::Find(in->Data(), in->NumRows(), in->NumCols(), in->Stride());
+    if (h && h->pending && h->pending->pending) pc = h->pending;
+  }
   CNSL_SAFE_CALL(kl_gemm_stats3(dy.Data(), N, O, dy.Stride(), 0, rows_d, nullptr,
                                 cols ? dy.Data() : nullptr, N, O, dy.Stride(), 1, cols_d, part_d,
-                                W.Data(), O, I, W.Stride(), 1, cols_w, part_w,
+                                W.Data(), O, I, W.Stride(), 1, cols_w, part_w, pc,
                                 reinterpret_cast<kcnn_stream_t>(dev.Stream())));
+  if (pc) pc->pending = 0;
   hint_d_ = new CuGemmStatsHint(dy.Data(), N, O, dy.Stride(), rows_d, cols ? cols_d : nullptr);
   hint_w_ = new CuGemmStatsHint(W.Data(), O, I, W.Stride(), nullptr, cols_w);
 }
@@ -317,8 +334,8 @@ bool CuMatrixBase<Real>::GemmF16x3(Real alpha, const CuMatrixBase<Real> &A,
                                                     A.Stride());
   const CuGemmStatsHint *hb = CuGemmStatsHint::Find(B.Data(), B.NumRows(), B.NumCols(),
                                                     B.Stride());
-  const uint32_t *ag = ha ? (transA == kNoTrans ? ha->rowmax : ha->colmax) : nullptr;
-  const uint32_t *bg = hb ? (transB == kNoTrans ? hb->colmax : hb->rowmax) : nullptr;
+  const uint32_t *ag = ha ? (transA == kNoTrans ? ha->rowmax : hint_cols(ha, S())) : nullptr;
+  const uint32_t *bg = hb ? (transB == kNoTrans ? hint_cols(hb, S()) : hb->rowmax) : nullptr;
   const size_t wsf = kl_gemm_f16x3_full_workspace_bytes(m, n, k);
   void *wf = dev0.Malloc(wsf);
   const int rc = kl_gemm_f16x3_bias(transA == kTrans, transB == kTrans, m, n, k, alpha,
@@ -354,8 +371,8 @@ bool CuMatrixBase<Real>::AddMatMatMomentum(const CuMatrixBase<Real> &A,
                                                     A.Stride());
   const CuGemmStatsHint *hb = CuGemmStatsHint::Find(B.Data(), B.NumRows(), B.NumCols(),
                                                     B.Stride());
-  const uint32_t *ag = ha ? (transA == kNoTrans ? ha->rowmax : ha->colmax) : nullptr;
-  const uint32_t *bg = hb ? (transB == kNoTrans ? hb->colmax : hb->rowmax) : nullptr;
+  const uint32_t *ag = ha ? (transA == kNoTrans ? ha->rowmax : hint_cols(ha, S())) : nullptr;
+  const uint32_t *bg = hb ? (transB == kNoTrans ? hint_cols(hb, S()) : hb->rowmax) : nullptr;
   const size_t wsf = kl_gemm_f16x3_full_workspace_bytes(m, n, k);
   void *wf = dev0.Malloc(wsf);
   const int rc = kl_gemm_f16x3_momentum(transA == kTrans, transB == kTrans, m, n, k, A.Data(),

@@ -318,6 +318,9 @@ Real VecVec(const CuVectorBase<Real> &a, const CuVectorBase<Real> &b);
 /// f16x3 engine scales each operand row / column by them
 /// (kaldi-lite/cu-gemm-f16x3.hip) and would otherwise read the operand once
 /// more to compute them.  The owner keeps the matrix unmodified in scope.
+}  // namespace kaldi
+struct PoolColDeferred;  // cnslmat/pool-stats.h
+namespace kaldi {
 class CuGemmStatsHint {
  public:
   CuGemmStatsHint(const float *data, MatrixIndexT rows, MatrixIndexT cols, MatrixIndexT stride,
@@ -329,6 +332,10 @@ class CuGemmStatsHint {
   static const CuGemmStatsHint *Find(const float *data, MatrixIndexT rows, MatrixIndexT cols,
                                      MatrixIndexT stride);
   const uint32_t *rowmax, *colmax;
+  /// colmax's work left pending by its producer (nullable): run by the
+  /// reader (CuGemmBackpropStats merges it into its launches; AddMatMat
+  /// runs it first) before colmax is read
+  PoolColDeferred *pending = nullptr;
 
  private:
   const float *data_;
@@ -347,8 +354,10 @@ class CuGemmStatsHint {
 /// weight update itself is fine: the weight-gradient GEMM reads neither).
 class CuGemmBackpropStats {
  public:
+  /// in_value (nullable): the layer's input, whose pending column
+  /// statistics (a fused pool's, CuGemmStatsHint::pending) join the launches
   CuGemmBackpropStats(const CuMatrixBase<float> &out_deriv, const CuMatrixBase<float> &linear,
-                      bool cols);
+                      bool cols, const CuMatrixBase<float> *in_value = NULL);
   ~CuGemmBackpropStats();
   CuGemmBackpropStats(const CuGemmBackpropStats &) = delete;
   CuGemmBackpropStats &operator=(const CuGemmBackpropStats &) = delete;

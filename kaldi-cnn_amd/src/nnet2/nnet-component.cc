@@ -288,9 +288,10 @@ void AffineComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
   AffineComponent *to_update = dynamic_cast<AffineComponent *>(to_update_in);
   in_deriv->Resize(out_deriv.NumRows(), InputDim(), kUndefined);
   // f16x3 engine: the two GEMMs' operand statistics (out_deriv's rows and
-  // W's columns for the data gradient, out_deriv's columns for the update)
-  // in one launch set instead of one per GEMM
-  CuGemmBackpropStats stats(out_deriv, linear_params_, to_update != NULL);
+  // W's columns for the data gradient, out_deriv's columns for the update,
+  // and in_value's columns when a fused pool left them pending) in one
+  // launch set instead of one per GEMM
+  CuGemmBackpropStats stats(out_deriv, linear_params_, to_update != NULL, &in_value);
   in_deriv->AddMatMat(1.0, out_deriv, kNoTrans, linear_params_, kNoTrans, 0.0);
   if (to_update != NULL) {
     if (to_update->is_gradient_)

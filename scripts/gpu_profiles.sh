@@ -21,6 +21,9 @@ timeout -k 10 300 python bench.py --config nnet --json-out $O/bench_nnet.json > 
 # c3 (65536 frames on one GPU) and one rank's c4 shard (16384 frames)
 timeout -k 10 300 python bench.py --no-cpu-baseline --frames-per-gpu 65536 --json-out $O/bench_c3.json > $O/bench_c3.log 2>&1 || exit 5
 timeout -k 10 300 python bench.py --no-cpu-baseline --frames-per-gpu 16384 --json-out $O/bench_c4shard.json > $O/bench_c4shard.log 2>&1 || exit 5
+# the same c4 shard as a data-parallel rank at world size 1 (RCCL; the DP
+# step's own cost beside the single-GPU line)
+HSA_ENABLE_IPC_MODE_LEGACY=0 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr=127.0.0.1 --master-port=29513 bench.py --gpus 1 --no-cpu-baseline --frames-per-gpu 16384 --json-out $O/bench_c4shard_dp1.json > $O/bench_c4shard_dp1.log 2>&1 || exit 5
 fi
 if [ "$PART" = 1 ]; then echo done; exit 0; fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c2/prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/c2.prof.log 2>&1 || exit 6

@@ -1148,7 +1148,12 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6q_kernel(
   char *Yp = smem;                                            // [3][32][384] bf16
   char *Wimg = Yp + 3 * YPL;                                  // [3][32][128] bf16
   float *Zt = reinterpret_cast<float *>(Wimg + 3 * WPL);      // [Kdim][PZ]
-  float *Xs = Zt + g.Kdim * PZ;                               // padded map + {1}
+  // the padded map + {1}, split once per frame: element e is (m << 16 | h, l)
+  // of its three bf16 parts (bf16-split.h), so the wgrad waves' im2col
+  // gather packs fragments from them (3 v_perm per pair) instead of splitting
+  // every gathered copy of a value (11 VALU per pair; each value is gathered
+  // kh * kw times)
+  uint2 *Xs = reinterpret_cast<uint2 *>(Zt + g.Kdim * PZ);
   int *qtab = reinterpret_cast<int *>(Xs + round4(CHWp + 1));  // [384]
   // col2im taps of each dX element (kw == 1, kh <= 8): Z offset | ylo << 16 |
   // ny << 20, the same every frame
@@ -1176,20 +1181,22 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6q_kernel(
     *reinterpret_cast<uint32_t *>(Wimg + WPL + o) = m;
     *reinterpret_cast<uint32_t *>(Wimg + 2 * WPL + o) = lo;
   }
-  int abase = CHWp * 4, qmul = 0;
+  // byte offsets into Xs (8 B per element)
+  uint32_t abase = (uint32_t)CHWp * 8, qmul = 0;
   if (l < g.Kdim) {
     uint32_t c, r, qx, qy;
     g.div_khkw.divmod((uint32_t)l, c, r);
     g.div_kh.divmod(r, qx, qy);
-    abase = ((int)c * Hp * Wp + (int)qx * Hp + (int)qy) * 4;
+    abase = ((uint32_t)c * Hp * Wp + qx * Hp + qy) * 8;
     qmul = 1;
   }
-  for (int e = tid; e < CHWp; e += NT) Xs[e] = 0.0f;
-  if (tid == 0) Xs[CHWp] = 1.0f;
+  for (int e = tid; e < CHWp; e += NT) Xs[e] = make_uint2(0u, 0u);
+  if (tid == 0) Xs[CHWp] = make_uint2(0x3f80u, 0u);  // 1.0f = h alone
   for (int p = tid; p < PP; p += NT) {
     uint32_t px, py;
     g.div_oh.divmod((uint32_t)p, px, py);
-    qtab[p] = p < P ? ((int)px * Hp + (int)py) * 4 : 0x3fffffff;
+    // past P: past every lane's range (the clamp below reads the 1.0 entry)
+    qtab[p] = p < P ? ((int)px * Hp + (int)py) * 8 : 0x00ffffff;
   }
   const int khkw0 = g.kh * g.kw;
   const bool c2fast = g.kw == 1 && g.kh <= 8;
@@ -1203,7 +1210,7 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6q_kernel(
       ctab[e] = ((int)c * khkw0 * PZ + tx * g.oh + ty) | (ylo << 16) | (ny << 20);
     }
   }
-  const uint32_t amax = (uint32_t)CHWp * 4;
+  const uint32_t amax = (uint32_t)CHWp * 8;
   const char *Xb = reinterpret_cast<const char *>(Xs);
 
   // ---- split units: (pooled row j, position quad p0), the same in every slab
@@ -1333,7 +1340,9 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6q_kernel(
           g.div_H.divmod(q, wi, hi);
           slot = (int)c * Hp * Wp + ((int)wi + g.pad_w) * Hp + (int)hi + g.pad_h;
         }
-        Xs[slot] = xv[i];
+        uint32_t h, m, lo;  // bf16-split.h's parts of the one value (its split2 bits)
+        split2(xv[i], xv[i], h, m, lo);
+        Xs[slot] = make_uint2((m << 16) | (h & 0xffffu), lo & 0xffffu);
       }
     }
   };
@@ -1432,19 +1441,34 @@ __global__ __launch_bounds__(NT, 1) void conv_bwd_x6q_kernel(
       qv[s][0] = *reinterpret_cast<const int4 *>(qtab + pbase);
       qv[s][1] = *reinterpret_cast<const int4 *>(qtab + pbase + 4);
     }
-    float v[NS][8];
+    uint2 v[NS][8];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const int q[8] = {qv[s][0].x, qv[s][0].y, qv[s][0].z, qv[s][0].w,
                         qv[s][1].x, qv[s][1].y, qv[s][1].z, qv[s][1].w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const uint32_t off = min((uint32_t)(abase + qmul * q[e]), amax);
-        v[s][e] = *reinterpret_cast<const float *>(Xb + off);
+        // (24-bit multiply: one full-rate mad; qmul is 0 or 1)
+        const uint32_t off = min(__umul24(qmul, (uint32_t)q[e]) + abase, amax);
+        v[s][e] = *reinterpret_cast<const uint2 *>(Xb + off);
       }
     }
+    // the three planes' fragments from the pre-split parts: the same bits
+    // split8 gives for the values
 #pragma unroll
-    for (int s = 0; s < NS; ++s) split8(v[s], a[S0 + s][0], a[S0 + s][1], a[S0 + s][2]);
+    for (int s = 0; s < NS; ++s) {
+      uint32_t hh[4], mm[4], ll[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint2 w0 = v[s][2 * i], w1 = v[s][2 * i + 1];
+        hh[i] = __builtin_amdgcn_perm(w1.x, w0.x, 0x05040100u);
+        mm[i] = __builtin_amdgcn_perm(w1.x, w0.x, 0x07060302u);
+        ll[i] = __builtin_amdgcn_perm(w1.y, w0.y, 0x05040100u);
+      }
+      a[S0 + s][0] = __builtin_bit_cast(bf16x8, make_uint4(hh[0], hh[1], hh[2], hh[3]));
+      a[S0 + s][1] = __builtin_bit_cast(bf16x8, make_uint4(mm[0], mm[1], mm[2], mm[3]));
+      a[S0 + s][2] = __builtin_bit_cast(bf16x8, make_uint4(ll[0], ll[1], ll[2], ll[3]));
+    }
   };
   using C0 = std::integral_constant<int, 0>;
   using CA = std::integral_constant<int, SA>;
@@ -1691,7 +1715,11 @@ size_t x6p_lds(const ConvGeom &g) {
 }
 
 // conv_bwd_x6q_kernel: x6p's plan and the col2im tap table
-size_t x6q_lds(const ConvGeom &g) { return x6p_lds(g) + (size_t)round4(g.C * g.HW) * 4; }
+// (and the map's split parts, 8 B per element instead of x6p's 4)
+size_t x6q_lds(const ConvGeom &g) {
+  const int CHWp = g.C * (g.H + 2 * g.pad_h) * (g.W + 2 * g.pad_w);
+  return x6p_lds(g) + (size_t)round4(g.C * g.HW) * 4 + (size_t)round4(CHWp + 1) * 4;
+}
 
 size_t x6_lds(const ConvGeom &g, bool dx, int pc, int ph) {
   const int CHWp = g.C * (g.H + 2 * g.pad_h) * (g.W + 2 * g.pad_w);

@@ -156,7 +156,30 @@ struct F16Aux {
   const uint32_t *xst;   // [max R][min R][cnt R] of X's rows (frames)
   unsigned *list;        // [tile count, element count, tile ids (one per tile)]
   unsigned *elist;       // element entries (8 waves x REJ_MAX per tile)
+  const uint32_t *wsplit;  // W split once per call: [Kdim][ks] of (lo << 16 | hi)
 };
+
+// W's f16x3 parts, once per call (conv_w_presplit_kernel): element (k, g)
+// under its filter's scale (the tile kernel's exponent of row g of A = W^T),
+// hi in the low half and lo in the high half of a word, the bits split8h
+// gives; the tiles then only repack them (two v_perm per element pair)
+// instead of splitting every tile's copy of W (each tile re-reads all of W)
+__global__ __launch_bounds__(256) void conv_w_presplit_kernel(const float *__restrict__ Kw,
+                                                              int ks, int Kdim, int G,
+                                                              const uint32_t *__restrict__ wst,
+                                                              uint32_t *__restrict__ out) {
+  const float m1 = f16x3::opaque_m1();
+  const int64_t n = (int64_t)Kdim * G;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int k = (int)(i / G), gg = (int)(i - (int64_t)k * G);
+    const int e0 = f16x3::scale_exp(wst[gg]);
+    const int e = e0 == f16x3::SKIP ? 0 : e0;
+    const float x = Kw[(int64_t)k * ks + gg];
+    uint32_t h, l;
+    f16x3::split2h(x, x, e, e, h, l, m1);
+    out[(int64_t)k * ks + gg] = (l << 16) | (h & 0xffffu);
+  }
+}
 constexpr int kAuxBytes = 384 * 8;  // F16: scale exponents and weights of a tile's groups
 
 template <int BG, bool PADDED, bool STG, bool TAB, int POOL, bool F16>
@@ -188,8 +211,9 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
   // A = W^T: thread row g0 + a_row, k = kt*32 + a_kc*APT + j (a_kc uniform)
   const int a_row = tid % BG;
   const int a_kc = __builtin_amdgcn_readfirstlane(tid / BG);
+  // (F16: W's parts, split once per call; the same range)
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)Kw, (short)0, g.Kdim * ks * 4, 0x00020000);
+      F16 ? (void *)fx.wsplit : (void *)Kw, (short)0, g.Kdim * ks * 4, 0x00020000);
   const unsigned a_voff = (unsigned)(g0 + a_row) * 4u;
   // B = im2col(X): thread column m0 + b_row, k = kt*32 + b_kc*BPT + e
   const int b_row = tid % BN;
@@ -346,9 +370,22 @@ __global__ __launch_bounds__(NT, 1) void conv_igemm_x6_kernel(
   const float m1 = F16 ? f16x3::opaque_m1() : -1.0f;
   auto store = [&](char *buf) {
     if constexpr (F16) {
+      // A: the pre-split words repacked, hi halves to plane 0, lo to plane 1
 #pragma unroll
-      for (int cc = 0; cc < APT / 8; cc++)
-        put8h(buf, PLA, swzi(a_row, a_kc * (APT / 8) + cc), &av[8 * cc], ea, m1);
+      for (int cc = 0; cc < APT / 8; cc++) {
+        uint32_t hh[4], ll[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const uint32_t w0 = __float_as_uint(av[8 * cc + 2 * i]);
+          const uint32_t w1 = __float_as_uint(av[8 * cc + 2 * i + 1]);
+          hh[i] = __builtin_amdgcn_perm(w1, w0, 0x05040100u);
+          ll[i] = __builtin_amdgcn_perm(w1, w0, 0x07060302u);
+        }
+        const int off = swzi(a_row, a_kc * (APT / 8) + cc);
+        *reinterpret_cast<uint4 *>(buf + off) = make_uint4(hh[0], hh[1], hh[2], hh[3]);
+        *reinterpret_cast<uint4 *>(buf + PLA + off) = make_uint4(ll[0], ll[1], ll[2], ll[3]);
+      }
+      (void)ea;
 #pragma unroll
       for (int cc = 0; cc < BPT / 8; cc++)
         put8h(buf + 2 * PLA, PLB, swzi(b_row, b_kc * (BPT / 8) + cc), &bv[8 * cc], eb, m1);
@@ -1430,22 +1467,30 @@ struct F16Setup {
   int rc = 0;
   F16Setup(bool on, const ConvGeom &g, const float *X, int xs, const float *K, int ks,
            unsigned blocks, hipStream_t st)
-      : ws(on ? words(g, blocks) * 4 : 0) {
+      : ws(on ? words(g, blocks, ks) * 4 : 0) {
     if (!on) return;
     uint32_t *w = static_cast<uint32_t *>(ws.p);
     uint32_t *wst = w, *xst = wst + 3 * (size_t)g.G, *list = xst + 3 * (size_t)g.R,
              *elist = list + 2 + blocks, *part = elist + elist_words(blocks);
     rc = kl_absmax_rows_cols(X, g.R, g.HW * g.C, xs, xst, K, g.Kdim, g.G, ks, wst, part, list,
                              reinterpret_cast<kcnn_stream_t>(st));
+    if (rc) return;
+    uint32_t *wsplit = part + kl_absmax_cols_words(g.Kdim, g.G);
+    const int64_t nw = (int64_t)g.Kdim * g.G;
+    hipLaunchKernelGGL(conv_w_presplit_kernel,
+                       dim3((unsigned)std::min<int64_t>((nw + 255) / 256, 1024)), dim3(256), 0,
+                       st, K, ks, g.Kdim, g.G, (const uint32_t *)wst, wsplit);
+    rc = (int)hipGetLastError();
     fx.wst = wst;
     fx.xst = xst;
     fx.list = list;
     fx.elist = elist;
+    fx.wsplit = wsplit;
   }
   static size_t elist_words(unsigned blocks) { return (size_t)blocks * 8 * REJ_MAX * EW; }
-  static size_t words(const ConvGeom &g, unsigned blocks) {
+  static size_t words(const ConvGeom &g, unsigned blocks, int ks) {
     return 3 * (size_t)g.G + 3 * (size_t)g.R + 2 + blocks + elist_words(blocks) +
-           kl_absmax_cols_words(g.Kdim, g.G);
+           kl_absmax_cols_words(g.Kdim, g.G) + (size_t)g.Kdim * ks;
   }
 };
 // f16x3 for the large convolutions (2 M G Kdim >= 2^34 flop: c5's C2 / C3

@@ -299,7 +299,12 @@ struct Loader {
         asm volatile("");  // a branch: not per-element selects in every K step
         if (kq * KPT + j >= kv) x0 = x1 = 0.0f;
       }
+#ifdef KCNN_GEMM_XNOSPLIT
+      ph[hf] = __float_as_uint(x0);
+      pl[hf] = __float_as_uint(x1);
+#else
       split2h(x0, x1, e[2 * hf], e[2 * hf + 1], ph[hf], pl[hf], m1);
+#endif
       if (hf == 1) {
         const int o = tswz<R>(kq * KPT + j, 4 * rq);
         *reinterpret_cast<uint2 *>(lds + o) = make_uint2(ph[0], ph[1]);
@@ -325,7 +330,12 @@ struct Loader {
         if (kb + 2 * q >= kv) x0 = 0.0f;
         if (kb + 2 * q + 1 >= kv) x1 = 0.0f;
       }
+#ifdef KCNN_GEMM_XNOSPLIT  // experiment build: timing without the split
+      ph[q & 3] = __float_as_uint(x0);
+      pl[q & 3] = __float_as_uint(x1);
+#else
       split2h(x0, x1, e[u], e[u], ph[q & 3], pl[q & 3], m1);
+#endif
       if ((q & 3) == 3) {
         const int off = swz(r, c0 + (q >> 2));
         *reinterpret_cast<uint4 *>(lds + off) = make_uint4(ph[0], ph[1], ph[2], ph[3]);
@@ -875,7 +885,11 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
   auto mfma_n = [&](int n, const f16x8 (&fa)[2][2], const f16x8 (&fb)[2][2]) {
     const int i = n / 6, j = (n / 3) & 1, pr = n % 3;
     constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};
+#ifdef KCNN_GEMM_XNOMFMA  // experiment build: timing without the products
+    asm volatile("" ::"v"(fa[i][PA[pr]]), "v"(fb[j][PB[pr]]));
+#else
     acc[i][j] = mfma(fa[i][PA[pr]], fb[j][PB[pr]], acc[i][j]);
+#endif
   };
 
   // waves 4-7 (each SIMD's second wave) at priority 1 for the whole kernel
@@ -940,8 +954,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
 #pragma unroll
       for (int n = 0; n < 12; ++n) {
         mfma_n(n, fa1, fb1);
+#ifndef KCNN_GEMM_XNOLOAD  // experiment build: timing without the main loop's loads
         if (n == 1) lan.load(rsA, p.lda, vra, kk(t + 3, A_KC), tid);
         if (n == 3) lbn.load(rsB, p.ldb, vrb, kk(t + 3, B_KC), tid);
+#endif
         if (more && n >= 2 && n < 10) read_frag(nbuf, 0, n - 2, fa0, fb0);
         __builtin_amdgcn_sched_barrier(0);
       }

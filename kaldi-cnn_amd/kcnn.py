@@ -631,6 +631,11 @@ class Nnet:
                                                  ptr(grad), int(skip_first_dx)))
 
     def Backprop(self, out_deriv, skip_first_dx=False):
+        """The whole backward in one kcnn_nnet_backprop call; with
+        skip_first_dx, one kcnn_nnet_backprop_component call per layer."""
+        if not skip_first_dx:
+            check(lib().kcnn_nnet_backprop(self._h, ptr(out_deriv), dim(out_deriv)))
+            return
         for i in reversed(range(self.NumComponents())):
             self.BackpropComponent(i, out_deriv, 0, None, skip_first_dx)
 

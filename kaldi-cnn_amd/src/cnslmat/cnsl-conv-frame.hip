@@ -28,7 +28,9 @@
 #include <stdlib.h>
 
 #include "conv-geom.h"
+#include "conv-update.h"
 #include "f16-split.h"
+#include "momentum-step.h"
 #include "pool-stats-dev.h"
 #include "x6-util.h"
 
@@ -1900,9 +1902,11 @@ __global__ __launch_bounds__(256) void reduce_pass1(const float *__restrict__ in
 // output mapping: e < nw -> gW[row][col] with (row, col) = gk_layout ?
 // (e % inner, e / inner) : (e / inner, e % inner); e >= nw -> gb[e - nw].
 // (Two passes of 32-row groups spent ~14 us of latency at c2, for 3.3 MB.)
+// u.W != NULL (conv-update.h): the sums step W / prev (momentum_step) and b
+// instead of being stored in gW / gb (gk_layout 0 only).
 __global__ __launch_bounds__(256) void reduce_splits_kernel(
     const float *__restrict__ in, int S, int E, int nw, int inner, int gk_layout,
-    float *__restrict__ gW, int gws, float *__restrict__ gb) {
+    float *__restrict__ gW, int gws, float *__restrict__ gb, ConvUpdateEpi u) {
   __shared__ float red[4][64];
   const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + c;
@@ -1925,7 +1929,17 @@ __global__ __launch_bounds__(256) void reduce_splits_kernel(
   if (e < nw) {
     const int a = e / inner, b = e - a * inner;
     const int row = gk_layout ? b : a, col = gk_layout ? a : b;
-    gW[(int64_t)row * gws + col] = sum;
+    if (u.W) {  // ApplyGradient's MomentumUpdate on this element
+      float *pw = u.W + (int64_t)row * u.ldw + col, *pp = u.prev + (int64_t)row * u.ldp + col;
+      float p = *pp, w = *pw;
+      kcnn::momentum_step(sum, p, w, u.momentum, u.a_wd, u.a_g);
+      *pp = p;
+      *pw = w;
+    } else {
+      gW[(int64_t)row * gws + col] = sum;
+    }
+  } else if (u.W) {  // its BiasUpdate
+    u.b[e - nw] = __builtin_fmaf(u.a_g, sum, u.b[e - nw]);
   } else if (gb) {
     gb[e - nw] = sum;
   }
@@ -2253,7 +2267,7 @@ int kcnn_conv_wgrad_frame(const ConvGeom &g, const float *X, int xs,
   if (rc) return rc;
   (void)tmp;
   hipLaunchKernelGGL(reduce_splits_kernel, dim3((E + 63) / 64), dim3(256), 0, st, part, S,
-                     E, g.Kdim * g.G, g.G, 0, gW, gws, gb);
+                     E, g.Kdim * g.G, g.G, 0, gW, gws, gb, ConvUpdateEpi{});
   return (int)hipGetLastError();
 }
 
@@ -2294,8 +2308,8 @@ static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
                            const float *dY, int dys, const float *K, int ks,
                            float *dX, int dxs, float *gW, int gws, float *gb,
                            void *ws, size_t ws_bytes, int dx_acc, hipStream_t st,
-                           const unsigned char *pmask = nullptr, int pms = 0, int pc = 0,
-                           int ph = 1) {
+                           const unsigned char *pmask, int pms, int pc, int ph,
+                           const ConvUpdateEpi *ue) {
   static const int enabled = KCNN_KNOB("KCNN_FUSED_BWD", 1);
   static const int variant = KCNN_KNOB("KCNN_BWD_VARIANT", 3);  // 1: register-staged
   static const int bdbg = KCNN_KNOB("KCNN_BWD_DEBUG", 0);
@@ -2335,7 +2349,7 @@ static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
     }
     if (rc || gW == nullptr) return rc;
     hipLaunchKernelGGL(reduce_splits_kernel, dim3((E + 63) / 64), dim3(256), 0, st, part, S,
-                       E, g.Kdim * g.G, g.G, 0, gW, gws, gb);
+                       E, g.Kdim * g.G, g.G, 0, gW, gws, gb, ue ? *ue : ConvUpdateEpi{});
     return (int)hipGetLastError();
   }
   if (ph != 1) return -1;  // 3-D windows: the bf16x6 kernel only
@@ -2433,7 +2447,7 @@ static int bwd_frame_chunk(const ConvGeom &g, const float *X, int xs,
   float *tmp = part + (size_t)S * E;
   (void)tmp;
   hipLaunchKernelGGL(reduce_splits_kernel, dim3((E + 63) / 64), dim3(256), 0, st, part, S,
-                     E, g.Kdim * g.G, g.G, 0, gW, gws, gb);
+                     E, g.Kdim * g.G, g.G, 0, gW, gws, gb, ue ? *ue : ConvUpdateEpi{});
   return (int)hipGetLastError();
 }
 
@@ -2447,9 +2461,15 @@ int kcnn_conv_bwd_frame(const ConvGeom &g, const float *X, int xs,
                         float *dX, int dxs, float *gW, int gws, float *gb,
                         void *ws, size_t ws_bytes, hipStream_t st,
                         const unsigned char *pmask, int pms, int pc, int ph) {
-  if (g.G <= 128)
-    return bwd_frame_chunk(g, X, xs, dY, dys, K, ks, dX, dxs, gW, gws, gb, ws,
-                           ws_bytes, 0, st, pmask, pms, pc, ph);
+  // the caller's update request (conv-update.h), for this layer's W
+  ConvUpdateEpi *u = kcnn_conv_update_current();
+  if (u && !(gW && gb && u->Kdim == g.Kdim && u->G == g.G)) u = nullptr;
+  if (g.G <= 128) {
+    const int rc = bwd_frame_chunk(g, X, xs, dY, dys, K, ks, dX, dxs, gW, gws, gb, ws,
+                                   ws_bytes, 0, st, pmask, pms, pc, ph, u);
+    if (rc == 0 && u) u->applied = 1;
+    return rc;
+  }
   if (g.G % 32 != 0 || (int64_t)g.G * g.P * 4 % 16 != 0) return -1;
   static const int variant = KCNN_KNOB("KCNN_BWD_VARIANT", 3);
   if (variant != 3 && dX != nullptr) return -1;  // chunking needs dX accumulation
@@ -2459,16 +2479,25 @@ int kcnn_conv_bwd_frame(const ConvGeom &g, const float *X, int xs,
     // pooled rows of P / ph values when pc, masks of 1 (ph == 1) or 2 bytes
     const int64_t dofs = pc ? (int64_t)(g0 / pc) * (g.P / ph) : (int64_t)g0 * g.P;
     const int64_t mofs = dofs * (ph > 1 ? 2 : 1);
+    ConvUpdateEpi uc{};
+    if (u) {  // the chunk's filter columns of W, prev and b
+      uc = *u;
+      uc.W += g0;
+      uc.prev += g0;
+      uc.b += g0;
+      uc.G = gc.G;
+    }
     const int rc = bwd_frame_chunk(
         gc, X, xs, dY + dofs, dys, K + g0, ks, dX, dxs, gW ? gW + g0 : nullptr, gws,
         gb ? gb + g0 : nullptr, ws, ws_bytes, g0 > 0, st, pmask ? pmask + mofs : nullptr,
-        pms, pc, ph);
+        pms, pc, ph, u ? &uc : nullptr);
     if (rc) {
       // only the first chunk may decline (nothing written yet); a later
       // failure is a launch error
       return g0 == 0 ? rc : (rc < 0 ? (int)hipErrorLaunchFailure : rc);
     }
   }
+  if (u) u->applied = 1;
   return 0;
 }
 
@@ -2483,7 +2512,7 @@ int kcnn_reduce_splits_wgrad(const float *in, int S, int E, float *tmp, int nw,
                              hipStream_t st) {
   (void)tmp;
   hipLaunchKernelGGL(reduce_splits_kernel, dim3((E + 63) / 64), dim3(256), 0, st, in, S, E,
-                     nw, inner, 1, gW, gws, gb);
+                     nw, inner, 1, gW, gws, gb, ConvUpdateEpi{});
   return (int)hipGetLastError();
 }
 
@@ -2499,6 +2528,6 @@ int kcnn_reduce_splits(const float *in, int S, int E, float *tmp, float *out,
                        hipStream_t st) {
   (void)tmp;
   hipLaunchKernelGGL(reduce_splits_kernel, dim3((E + 63) / 64), dim3(256), 0, st, in, S, E,
-                     E, E, 0, out, 0, nullptr);
+                     E, E, 0, out, 0, nullptr, ConvUpdateEpi{});
   return (int)hipGetLastError();
 }

@@ -8,6 +8,7 @@
 #include <algorithm>
 
 #include "cnsl-hip-kernels.h"
+#include "conv-update.h"
 #include "pool-stats.h"
 #include "../kaldi-lite/cu-device.h"
 #include "../kaldi-lite/cu-matrix.h"
@@ -20,6 +21,13 @@ PoolColDeferred *kcnn_pool_defer_request(PoolColDeferred *d) {
   return prev;
 }
 PoolColDeferred *kcnn_pool_defer_current() { return t_pool_defer; }
+static thread_local ConvUpdateEpi *t_conv_update = nullptr;
+ConvUpdateEpi *kcnn_conv_update_request(ConvUpdateEpi *u) {
+  ConvUpdateEpi *prev = t_conv_update;
+  t_conv_update = u;
+  return prev;
+}
+ConvUpdateEpi *kcnn_conv_update_current() { return t_conv_update; }
 
 namespace kaldi {
 

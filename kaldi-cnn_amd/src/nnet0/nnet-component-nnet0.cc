@@ -11,6 +11,7 @@
 #include "../kaldi-lite/kaldi-io.h"
 #include "../nnet2/parse-from-string.h"
 #include "cnsl-hip-kernels.h"
+#include "cnslmat/conv-update.h"
 
 namespace cnsl {
 namespace nnet0 {
@@ -334,9 +335,16 @@ void ConvolutionComponent::Backprop(const ChunkInfo &, const ChunkInfo &,
     // dX (with the pre-update kernel, as the reference orders it) and the
     // gradient from one pass over out_deriv, then the update step (:541).
     Scratch grad(sizeof(BaseFloat) * (size_t)NumGradientParams());
-    BackpropGradient(ChunkInfo(), ChunkInfo(), in_value, in_value, out_deriv,
-                     in_deriv, grad.f());
-    to_update->ApplyGradient(grad.f(), in_value.NumRows());
+    // the step in the gradient's reduction where the frame kernels run it
+    // (conv-update.h), else ApplyGradient on the gradient
+    ConvUpdateEpi ue{};
+    to_update->UpdateRequest(in_value.NumRows(), &ue);
+    {
+      ConvUpdateScope scope(&ue);
+      BackpropGradient(ChunkInfo(), ChunkInfo(), in_value, in_value, out_deriv,
+                       in_deriv, grad.f());
+    }
+    if (!ue.applied) to_update->ApplyGradient(grad.f(), in_value.NumRows());
     return;
   }
   if (in_deriv != NULL) {
@@ -700,7 +708,10 @@ bool ConvolutionComponent::BackpropPooled(const CuMatrixBase<BaseFloat> &in_valu
   void *ws = ws_s.p;
   MatrixDim idd = in_value.Dim();
   int rc;
+  ConvUpdateEpi ue{};
+  if (to_update != NULL) to_update->UpdateRequest(num_chunks, &ue);
   {
+    ConvUpdateScope scope(to_update != NULL ? &ue : nullptr);
     CuProfileScope prof("ConvolutionComponent::BackpropPooled");
     rc = ph == 1
         ? hipF_conv2d_backward_pooled(
@@ -722,8 +733,24 @@ bool ConvolutionComponent::BackpropPooled(const CuMatrixBase<BaseFloat> &in_valu
   }
   if (rc < 0) return false;
   CNSL_SAFE_CALL(rc);
-  if (to_update != NULL) to_update->ApplyGradient(g, num_chunks);
+  if (to_update != NULL && !ue.applied) to_update->ApplyGradient(g, num_chunks);
   return true;
+}
+
+void ConvolutionComponent::UpdateRequest(int32 num_sample, ConvUpdateEpi *u) {
+  KALDI_ASSERT(num_sample > 0);
+  const double learning_rate = learning_rate_ / (double)num_sample;  // :767
+  u->W = linear_params_.Data();
+  u->ldw = linear_params_.Stride();
+  u->prev = prev_grad_.Data();
+  u->ldp = prev_grad_.Stride();
+  u->b = bias_params_.Data();
+  u->Kdim = KernelDim();
+  u->G = group_;
+  u->momentum = momentum_;
+  u->a_wd = (BaseFloat)(-1 * learning_rate * weight_decay_);
+  u->a_g = (BaseFloat)learning_rate;
+  u->applied = 0;
 }
 
 // Apply half of Update (:767-775), one pass over W / prev_grad_ / grad.

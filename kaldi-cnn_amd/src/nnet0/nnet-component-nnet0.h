@@ -26,6 +26,8 @@
 using namespace kaldi;
 using namespace kaldi::nnet2;
 
+struct ConvUpdateEpi;  // cnslmat/conv-update.h
+
 namespace cnsl {
 namespace nnet0 {
 
@@ -116,6 +118,9 @@ class ConvolutionComponent : public nnet2::UpdatableComponent {
                                const CuMatrixBase<BaseFloat> &out_deriv,
                                BaseFloat *grad) const;
   virtual void ApplyGradient(const BaseFloat *grad, int32 num_sample);
+  // ApplyGradient's step as a request for the fused backward's reduction
+  // (cnslmat/conv-update.h)
+  void UpdateRequest(int32 num_sample, ::ConvUpdateEpi *u);
   // dX and the gradient from one pass over out_deriv (hipF_conv2d_backward).
   virtual void BackpropGradient(const ChunkInfo &in_info, const ChunkInfo &out_info,
                                 const CuMatrixBase<BaseFloat> &in_value,

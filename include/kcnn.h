@@ -281,6 +281,14 @@ int kcnn_nnet_backprop_component(kcnn_nnet *n, int i, const float *out_deriv,
                                  MatrixDim od_dim, int mode, float *grad,
                                  int skip_first_dx);
 /* Full backward pass, last component to first, mode 0 (reference). */
+/* An affine layer (FullyConnected / Affine) in data-parallel training: its
+ * parameter gradient into grad (mode 3), then between(ctx) -- where the caller
+ * starts the gradient's all-reduce -- then its input derivative (mode 2),
+ * unless i == 0 and skip_first_dx.  The same results as the mode 3 and mode 2
+ * calls; both GEMMs' operand statistics come from one launch set. */
+int kcnn_nnet_backprop_split(kcnn_nnet *n, int i, const float *out_deriv, MatrixDim od_dim,
+                             float *grad, int skip_first_dx, void (*between)(void *),
+                             void *ctx);
 int kcnn_nnet_backprop(kcnn_nnet *n, const float *out_deriv, MatrixDim od_dim);
 
 #ifdef __cplusplus

@@ -630,6 +630,26 @@ class Nnet:
         check(lib().kcnn_nnet_backprop_component(self._h, i, ptr(od), odim, mode,
                                                  ptr(grad), int(skip_first_dx)))
 
+    def BackpropSplit(self, i, out_deriv, grad, skip_first_dx, between):
+        """kcnn_nnet_backprop_split: affine layer i's gradient into grad,
+        then between() (e.g. the gradient's all-reduce is started there),
+        then its input derivative; one statistics pass for both GEMMs."""
+        err = []
+
+        def cb(_ctx):
+            try:
+                between()
+            except BaseException as e:  # noqa: BLE001 -- re-raised below
+                err.append(e)
+        fn = ctypes.CFUNCTYPE(None, ctypes.c_void_p)(cb)
+        od = out_deriv
+        odim = dim(od) if od is not None else MatrixDim(0, 0, 0)
+        rc = lib().kcnn_nnet_backprop_split(self._h, i, ptr(od), odim, ptr(grad),
+                                            int(skip_first_dx), fn, None)
+        if err:
+            raise err[0]
+        check(rc)
+
     def Backprop(self, out_deriv, skip_first_dx=False):
         """The whole backward in one kcnn_nnet_backprop call; with
         skip_first_dx, one kcnn_nnet_backprop_component call per layer."""

@@ -24,9 +24,10 @@ reproduces the single-GPU math at the same global batch (the reference
 itself divides by its local row count, :767).
 
 `net` is duck-typed: anything with NumComponents(), components[i]
-(NumGradientParams, ApplyGradient), Propagate(x) and
-BackpropComponent(i, out_deriv, mode, grad) -- kcnn.Nnet on the GPU; the
-tests drive the same function with a CPU stand-in over gloo.
+(NumGradientParams, ApplyGradient), Propagate(x),
+BackpropComponent(i, out_deriv, mode, grad) and BackpropSplit(i, out_deriv,
+grad, skip_first_dx, between) -- kcnn.Nnet on the GPU; the tests drive the
+same function with a CPU stand-in over gloo.
 """
 from __future__ import annotations
 
@@ -92,9 +93,11 @@ def dp_train_step(net, x, out_deriv, grads, dist, frames_global, mark=None):
     pending = []
     for i in reversed(range(net.NumComponents())):
         if i in grads.large and getattr(net.components[i], "SplitGradient", lambda: True)():
-            net.BackpropComponent(i, out_deriv, mode=3, grad=grads[i], skip_first_dx=False)
-            pending.append(([i], dist.all_reduce(grads[i], async_op=True)))
-            net.BackpropComponent(i, out_deriv, mode=2, skip_first_dx=False)
+            # the gradient, its all-reduce started, then the data gradient
+            # (one library call: both GEMMs' statistics from one pass)
+            def start(i=i):
+                pending.append(([i], dist.all_reduce(grads[i], async_op=True)))
+            net.BackpropSplit(i, out_deriv, grads[i], False, start)
         elif i in grads.large:
             net.BackpropComponent(i, out_deriv, mode=1, grad=grads[i], skip_first_dx=False)
             pending.append(([i], dist.all_reduce(grads[i], async_op=True)))
@@ -106,7 +109,13 @@ def dp_train_step(net, x, out_deriv, grads, dist, frames_global, mark=None):
         pending.append((grads.small, dist.all_reduce(grads.bucket, async_op=True)))
     if mark:
         mark("wait_begin")
-    for _, work in pending:
+    # NCCL (RCCL) runs a process group's collectives in order on one stream,
+    # so the compute stream waits for the last one alone: each stream wait
+    # (and the event behind it) cost the c2 step 20-50 us of GPU idle at
+    # world size 1 (rocprofv3 trace); other backends wait for each
+    backend = getattr(dist, "get_backend", lambda: None)()
+    waits = pending[-1:] if backend == "nccl" else pending
+    for _, work in waits:
         work.wait()
     if mark:
         mark("wait_end")

@@ -910,6 +910,35 @@ int kcnn_nnet_backprop_component(kcnn_nnet *n, int i, const float *out_deriv,
   });
 }
 
+// An affine layer's parameter gradient, then between(ctx) (the caller starts
+// its all-reduce there), then the layer's data gradient: mode 3 and mode 2 in
+// one call, so both GEMMs' operand statistics come from one launch set that
+// lives across the callback (the pair of calls computed them twice).
+int kcnn_nnet_backprop_split(kcnn_nnet *n, int i, const float *out_deriv, MatrixDim od_dim,
+                             float *grad, int skip_first_dx, void (*between)(void *),
+                             void *ctx) {
+  return guard([&] {
+    const int nc = (int)n->comps.size();
+    KALDI_ASSERT(i >= 0 && i < nc && grad != NULL);
+    Component *c = n->comps[i];
+    auto *af = dynamic_cast<kaldi::nnet2::AffineComponent *>(c);
+    if (af == NULL) KALDI_ERR << "kcnn_nnet_backprop_split: component " << i << " is not affine";
+    KALDI_ASSERT(!(i + 1 < nc && n->deriv_deferred[i + 1]) && !n->mask_valid[i]);
+    auto hint = input_stats(n, i);
+    if (n->out_stale[i + 1]) n->out_stale[i + 1] = 2;
+    CuSubMatrix<BaseFloat> od = (i == nc - 1)
+        ? view(out_deriv, od_dim)
+        : CuSubMatrix<BaseFloat>(n->deriv[i + 1].Data(), n->deriv[i + 1].NumRows(),
+                                 n->deriv[i + 1].NumCols(), n->deriv[i + 1].Stride());
+    CuMatrix<BaseFloat> *dx = (i == 0 && skip_first_dx) ? nullptr : &n->deriv[i];
+    ChunkInfo ii = nnet_in_info(n, i), oi = nnet_out_info(n, i);
+    CuGemmBackpropStats stats(od, af->LinearParams(), true, &n->fwd[i]);
+    af->BackpropGradient(ii, oi, n->fwd[i], n->fwd[i + 1], od, nullptr, grad);
+    if (between) between(ctx);
+    if (dx) c->Backprop(ii, oi, n->fwd[i], n->fwd[i + 1], od, nullptr, dx);
+  });
+}
+
 int kcnn_nnet_backprop(kcnn_nnet *n, const float *out_deriv, MatrixDim od_dim) {
   for (int i = (int)n->comps.size() - 1; i >= 0; i--) {
     int rc = kcnn_nnet_backprop_component(n, i, out_deriv, od_dim, 0, nullptr, 0);

@@ -285,6 +285,14 @@ CuGemmBackpropStats::CuGemmBackpropStats(const CuMatrixBase<float> &dy,
   CuDevice &dev = CuDevice::Instantiate();
   const int N = dy.NumRows(), O = dy.NumCols(), I = W.NumCols();
   if (dev.GemmMode() != 2 || N == 0 || O == 0 || I == 0 || W.NumRows() != O) return;
+  // an enclosing launch set already covers them (kcnn_nnet_backprop_split:
+  // the gradient and the data gradient of one layer around the caller's
+  // all-reduce, one statistics pass for both)
+  {
+    const CuGemmStatsHint *hd = CuGemmStatsHint::Find(dy.Data(), N, O, dy.Stride());
+    const CuGemmStatsHint *hw = CuGemmStatsHint::Find(W.Data(), O, I, W.Stride());
+    if (hd && hd->rowmax && (!cols || hd->colmax) && hw && hw->colmax && !hw->pending) return;
+  }
   // blocks [max, min, cnt]: dy rows (N), dy columns (O), W columns (I), then
   // the column partials
   const size_t pd = cols ? kl_absmax_cols_words(N, O) : 0, pw = kl_absmax_cols_words(O, I);

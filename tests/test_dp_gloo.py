@@ -78,6 +78,13 @@ class OracleNet:
                 grad.copy_(torch.from_numpy(np.concatenate([gW.ravel(), gb])))
 
 
+    def BackpropSplit(self, i, out_deriv, grad, skip_first_dx, between):
+        """kcnn_nnet_backprop_split: mode 3, between(), mode 2."""
+        self.BackpropComponent(i, out_deriv, 3, grad, skip_first_dx)
+        between()
+        self.BackpropComponent(i, out_deriv, 2, None, skip_first_dx)
+
+
 def _data():
     H, W, C = CONV[:3]
     r = np.random.default_rng(77)

@@ -72,3 +72,55 @@ def test_bench_gpus_n_launches_n_ranks():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["dp"]["ranks_seen"] == 2
     assert res["config"]["parallelism"] == "dp2" and res["config"]["global_batch"] == 512
+
+
+@pytest.mark.parametrize("name,N", [("c2", 4096), ("c2", 37), ("long_2x1x4_pad", 64)])
+def test_backprop_split_equals_mode3_then_mode2(kc, name, N):
+    """kcnn_nnet_backprop_split (the FC layer's gradient, the caller's
+    callback, its data gradient; one statistics pass) gives the bits of the
+    mode-3 and mode-2 calls, and calls back once, between the two."""
+    import torch
+    from _util import dev, host, randn, rng
+    from test_gpu_nnet import STACKS, build
+
+    def run(split):
+        net = build(kc, STACKS[name], seed=11)
+        r = rng(3)
+        x = dev(randn(r, (N, net.components[0].InputDim())))
+        dy = dev(randn(r, (N, net.components[2].OutputDim()), 0.1))
+        fc = net.components[2]
+        grad = torch.zeros(fc.NumGradientParams(), device="cuda")
+        net.Propagate(x)
+        calls = []
+        if split:
+            net.BackpropSplit(2, dy, grad, False,
+                              lambda: calls.append(host(grad[None, :]).copy()))
+        else:
+            net.BackpropComponent(2, dy, mode=3, grad=grad, skip_first_dx=False)
+            calls.append(host(grad[None, :]).copy())
+            net.BackpropComponent(2, dy, mode=2, skip_first_dx=False)
+        return calls, host(grad[None, :]), host(net.InputDeriv(2))
+
+    a, b = run(True), run(False)
+    assert len(a[0]) == 1
+    for u, v, what in ((a[0][0], b[0][0], "grad at the callback"), (a[1], b[1], "grad"),
+                       (a[2], b[2], "input derivative")):
+        np.testing.assert_array_equal(u, v, err_msg=f"{name} N={N}: {what}")
+
+
+def test_backprop_split_callback_error(kc):
+    """An exception in the callback reaches the caller."""
+    import torch
+    from _util import dev, randn, rng
+    from test_gpu_nnet import STACKS, build
+    net = build(kc, STACKS["c2"], seed=11)
+    r = rng(3)
+    x = dev(randn(r, (8, net.components[0].InputDim())))
+    dy = dev(randn(r, (8, net.components[2].OutputDim()), 0.1))
+    grad = torch.zeros(net.components[2].NumGradientParams(), device="cuda")
+    net.Propagate(x)
+
+    def boom():
+        raise RuntimeError("callback failed")
+    with pytest.raises(RuntimeError, match="callback failed"):
+        net.BackpropSplit(2, dy, grad, False, boom)

@@ -3,6 +3,7 @@
 // CopyRowsFromVec, AddRowSumMat, TraceMatMat/VecVec).  Reductions are
 // two-pass with a fixed order, so results are bitwise reproducible.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 
 #include "../cnslmat/hip-util.h"
 #include "cu-kernels-lite.h"
@@ -83,20 +84,32 @@ __global__ __launch_bounds__(256) void kl_colsum_partial(
   }
   part[(int64_t)blockIdx.y * md.cols + j] = s;
 }
-// pass 2 -- v = beta*v + alpha*sum_slabs (slab order fixed).
+// pass 2 -- v = beta*v + alpha*sum_slabs: block = 64 columns x 4 slab
+// groups (group g sums slabs g, g + 4, ... in increasing order, lanes along
+// the columns: 256-B coalesced reads), then (g0 + g1) + (g2 + g3) -- a fixed
+// order, so the bits are deterministic.
 __global__ __launch_bounds__(256) void kl_colsum_final(
     const float *__restrict__ part, int slabs, int cols, float alpha,
     float beta, float *__restrict__ v) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= cols) return;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
   float s = 0.0f;
-  for (int b = 0; b < slabs; b += 8) {
-    float t[8];
+  if (j < cols) {
+    int b = grp;
+    for (; b + 28 < slabs; b += 32) {  // 8 partials' loads in flight
+      float t[8];
 #pragma unroll
-    for (int u = 0; u < 8; u++) t[u] = b + u < slabs ? part[(int64_t)(b + u) * cols + j] : 0.0f;
+      for (int u = 0; u < 8; u++) t[u] = part[(int64_t)(b + 4 * u) * cols + j];
 #pragma unroll
-    for (int u = 0; u < 8; u++) s += t[u];
+      for (int u = 0; u < 8; u++) s += t[u];
+    }
+    for (; b < slabs; b += 4) s += part[(int64_t)b * cols + j];
   }
+  red[grp][lane] = s;
+  __syncthreads();
+  if (grp != 0 || j >= cols) return;
+  s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
   // beta 1: one rounding, the bits of BiasUpdate's fma(a_g, gb, b)
   // (cnsl-hip-kernels.hip), so a bias row updated here equals one updated
   // from a stored column sum
@@ -175,15 +188,24 @@ int kl_sum_partials(const float *parts, int S, int m, int n, float beta,
                    SumPartialsF{parts, (int64_t)m * n, n, C, cd.stride, beta, S},
                    kcnn::as_stream(st));
 }
+// rows per slab of kl_colsum_partial: a multiple of 8, at least 16, and at
+// most 256 slabs (c2's 4096-row FC derivative: 16 rows, 256 slabs, 1024
+// blocks of the 1024 columns -- 64-row slabs gave 256 blocks, one wave per
+// SIMD, 2.2 TB/s)
+static int colsum_rows_per_slab(int rows) {
+  const int r = (rows + 255) / 256;
+  return std::max(16, (r + 7) / 8 * 8);
+}
 size_t kl_col_sum_workspace_bytes(MatrixDim md) {
-  const int slabs = (md.rows + 63) / 64;
+  const int rps = colsum_rows_per_slab(md.rows);
+  const int slabs = (md.rows + rps - 1) / rps;
   return (size_t)(slabs > 0 ? slabs : 1) * (size_t)md.cols * sizeof(float);
 }
 int kl_col_sum(const float *M, MatrixDim md, float alpha, float beta, float *v,
                void *ws, kcnn_stream_t st) {
   hipStream_t s = kcnn::as_stream(st);
   if (md.cols <= 0) return 0;
-  const int rps = 64;
+  const int rps = colsum_rows_per_slab(md.rows);
   int slabs = (md.rows + rps - 1) / rps;
   float *part = static_cast<float *>(ws);
   if (slabs == 0) {
@@ -194,7 +216,7 @@ int kl_col_sum(const float *M, MatrixDim md, float alpha, float beta, float *v,
     hipLaunchKernelGGL(kl_colsum_partial, dim3((md.cols + 255) / 256, slabs),
                        dim3(256), 0, s, M, md, rps, part);
   }
-  hipLaunchKernelGGL(kl_colsum_final, dim3((md.cols + 255) / 256), dim3(256), 0,
+  hipLaunchKernelGGL(kl_colsum_final, dim3((md.cols + 63) / 64), dim3(256), 0,
                      s, part, slabs, md.cols, alpha, beta, v);
   return kcnn::launch_status();
 }

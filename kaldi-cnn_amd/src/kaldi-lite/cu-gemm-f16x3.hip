@@ -544,8 +544,9 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
   // before the half is stored, so alpha, beta * C and the bias are applied
   // to it once, by the same 16-B store as its neighbours (a
   // second store_value after the staged store read back the new C).
-  const bool staged = row0 + BM <= p.M && col0 + BN <= p.N && !skip && !p.mom.W &&
-                      (partial || ((ldo & 3) | ((uintptr_t)slab & 15)) == 0)
+  // (the momentum update's W and prev have 16-B aligned rows: host check)
+  const bool staged = row0 + BM <= p.M && col0 + BN <= p.N && !skip &&
+                      (partial || p.mom.W || ((ldo & 3) | ((uintptr_t)slab & 15)) == 0)
 #ifdef KCNN_EXPERIMENTS  // KCNN_GEMM_DEBUG & 8: the per-register stores only
                       && !(p.dbg & 128)
 #endif
@@ -598,6 +599,19 @@ __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *s
         const int f = lane + 64 * k, rr = f >> 4, c4 = f & 15;
         const float4 v = *reinterpret_cast<const float4 *>(st + rr * SR + 4 * c4);
         const int row = row0 + wm * 64 + i * 32 + rr, col = col0 + wn * 64 + 4 * c4;
+        if (!partial && p.mom.W) {  // emit's momentum step, four elements per access
+          float4 *wq = reinterpret_cast<float4 *>(p.mom.W + (int64_t)row * p.mom.ldw + col);
+          float4 *pq = reinterpret_cast<float4 *>(p.mom.prev + (int64_t)row * p.mom.ldp + col);
+          float4 w4 = *wq, q4 = *pq;
+          const MomentumEpi &m = p.mom;
+          kcnn::momentum_step(p.alpha * v.x, q4.x, w4.x, m.momentum, m.a_wd, m.a_g);
+          kcnn::momentum_step(p.alpha * v.y, q4.y, w4.y, m.momentum, m.a_wd, m.a_g);
+          kcnn::momentum_step(p.alpha * v.z, q4.z, w4.z, m.momentum, m.a_wd, m.a_g);
+          kcnn::momentum_step(p.alpha * v.w, q4.w, w4.w, m.momentum, m.a_wd, m.a_g);
+          *pq = q4;
+          *wq = w4;
+          continue;
+        }
         float4 *o = reinterpret_cast<float4 *>(slab + (int64_t)row * ldo + col);
         if (partial) {
           *o = v;
@@ -1626,15 +1640,21 @@ __global__ __launch_bounds__(256) void gemm_f16x3_fixup_kernel(GemmF16Args p, in
   }
 }
 
-int choose_ksplit(int64_t tiles, int K) {
+// The split-K count of least modelled time: ceil(tiles s / 256) rounds of
+// one workgroup per CU, each K / s steps at 0.0458 us per k plus 11.1 us of
+// tile prologue and epilogue (fitted to c2's three FC GEMMs on MI355X), and
+// for s > 1 the reduce's (s + 1) M N fp32 reads and writes at 4 TB/s.  (The
+// reduce was unpriced before r06: nnet.config's 4096 x 3454 x 4096 layers
+// took 4 splits and a 86-92 us reduce; one split is 2.4 % faster per step.)
+int choose_ksplit(int64_t tiles, int M, int N, int K) {
   int best = 1;
-  double best_score = -1.0;
+  double best_t = 0.0;
   for (int s = 1; s <= 4; ++s) {
     if (s > 1 && K / s < 1024) break;
-    const int64_t nb = tiles * s;
-    const int64_t waves = (nb + 255) / 256;
-    const double score = (double)nb / (double)(waves * 256) - 0.02 * (s - 1);
-    if (score > best_score + 1e-9) { best_score = score; best = s; }
+    const int64_t rounds = (tiles * s + 255) / 256;
+    double t = (double)rounds * (0.0458 * ((K + s - 1) / s) + 11.1);
+    if (s > 1) t += (double)(s + 1) * M * N * 4.0 / 4.0e6;
+    if (s == 1 || t < best_t) { best_t = t; best = s; }
   }
   return best;
 }
@@ -1696,7 +1716,7 @@ size_t flag_bytes(int M, int N) {
 }
 size_t partial_bytes(int M, int N, int K) {
   const int64_t tiles = (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  const int s = choose_ksplit(tiles, K);
+  const int s = choose_ksplit(tiles, M, N, K);
   return s > 1 ? slab_bytes(s, M, N) + flag_bytes(M, N) : 0;
 }
 
@@ -1814,7 +1834,11 @@ static int gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alph
   a.tiles_m = (M + BM - 1) / BM;
   a.tiles_n = (N + BN - 1) / BN;
   const int64_t tiles = (int64_t)a.tiles_m * a.tiles_n;
-  int s = choose_ksplit(tiles, K);
+  int s = choose_ksplit(tiles, M, N, K);
+#ifdef KCNN_EXPERIMENTS  // A/B: KCNN_F16X3_KSPLIT forces the split count (0: chosen)
+  static const int ks_force = KCNN_KNOB("KCNN_F16X3_KSPLIT", 0);
+  if (ks_force > 0) s = std::min(ks_force, 4);
+#endif
   const size_t need = s > 1 ? slab_bytes(s, M, N) + flag_bytes(M, N) : 0;
   if (need > ws_bytes || !ws) s = 1;
   if (s > 1) {

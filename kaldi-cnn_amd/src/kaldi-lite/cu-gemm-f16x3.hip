@@ -104,29 +104,55 @@ struct GemmF16Args {
   MomentumEpi mom;               // mom.W: C is a weight gradient applied in the store (emit)
   int dbg;                       // KCNN_EXPERIMENTS builds: A/B switches
   int kps, ksplit, tiles_m, tiles_n;
+  int nwhole;                    // ksplit > 1: the first nwhole tiles (a multiple of 256) whole
   float alpha, beta;
 };
 
-// Logical workgroup id -> (split, tile row, tile column).  The splits of a
-// tile are consecutive; the tiles go in groups of GM tile rows, column-major
-// inside a group, so the 32 workgroups an XCD runs at once (consecutive ids,
-// XCD-aware order in the kernels) cover about GM x 32 / (GM ksplit) tiles
-// sharing GM row panels of op(A) and a few column panels of op(B) in that
-// XCD's L2, instead of one row panel and 32 column panels (c2's data
-// gradient: an XCD wave then reads 8 MB of operand panels instead of 17)
+// Tile t of the order -> (tile row, tile column).  The tiles go in groups of
+// GM tile rows, column-major inside a group, so the 32 workgroups an XCD runs
+// at once (consecutive logical ids, block_tile) cover about 32 / GM tile
+// columns of GM tile rows, sharing GM row panels of op(A) and a few column
+// panels of op(B) in that XCD's L2, instead of one row panel and 32 column
+// panels (c2's data gradient: an XCD wave then reads 8 MB of operand panels
+// instead of 17)
 #ifndef KCNN_GEMM_GM
 #define KCNN_GEMM_GM 4
 #endif
-__device__ __forceinline__ void tile_of(const GemmF16Args &p, int lid, int &split, int &tm,
-                                        int &tn) {
-  split = lid % p.ksplit;
-  const int t = lid / p.ksplit;
+__device__ __forceinline__ void tile_rc(const GemmF16Args &p, int t, int &tm, int &tn) {
   const int gsz = KCNN_GEMM_GM * p.tiles_n;
   const int g = t / gsz, r = t - g * gsz;
   const int m0 = g * KCNN_GEMM_GM;
   const int gm = min(p.tiles_m - m0, KCNN_GEMM_GM);
   tm = m0 + r % gm;
   tn = r / gm;
+}
+// ... and back: the order's index of tile (tm, tn)
+__device__ __forceinline__ int tile_index(const GemmF16Args &p, int tm, int tn) {
+  const int g = tm / KCNN_GEMM_GM, m0 = g * KCNN_GEMM_GM;
+  const int gm = min(p.tiles_m - m0, KCNN_GEMM_GM);
+  return g * KCNN_GEMM_GM * p.tiles_n + tn * gm + (tm - m0);
+}
+// This workgroup's (split, tile row, tile column); true for a whole tile.
+// Blocks [0, nwhole) take tiles [0, nwhole) over all of K, the others the
+// ksplit splits of the remaining tiles (consecutive logical ids: the splits
+// of one tile).  Each part in the XCD-aware order (gemm_x6_kernel): block b
+// runs on XCD b & 7, and consecutive logical ids go to one XCD (nwhole is a
+// multiple of 256, so both parts keep that phase and every XCD gets an
+// eighth of each).  nwhole 0: the plain split grid.
+__device__ __forceinline__ bool block_tile(const GemmF16Args &p, int &split, int &tm, int &tn) {
+  const bool whole = (int)blockIdx.x < p.nwhole;
+  const int b = whole ? (int)blockIdx.x : (int)blockIdx.x - p.nwhole;
+  const int nb = whole ? p.nwhole : (int)gridDim.x - p.nwhole;
+  const int ks = whole ? 1 : p.ksplit;
+  const int xcd = b & 7, q = nb >> 3, rr = nb & 7;
+  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
+  split = lid % ks;
+  tile_rc(p, (whole ? 0 : p.nwhole) + lid / ks, tm, tn);
+  return whole;
+}
+// C element (r, c) is a split tile's (its value from the partial slabs)
+__device__ __forceinline__ bool in_split_tile(const GemmF16Args &p, int r, int c) {
+  return p.nwhole == 0 || tile_index(p, r / BM, c / BN) >= p.nwhole;
 }
 
 __device__ __forceinline__ int swz(int r, int c) {
@@ -500,7 +526,8 @@ __device__ __forceinline__ void fix_rejected(const GemmF16Args &p, bool a_kc, bo
 // The tile's results.  C/D map of 32x32x16: register g of lane l holds row
 // (g & 3) + 8 (g >> 2) + 4 (l >> 5), column l & 31.  Each value is unscaled
 // by 2^-(s_row + s_col) (exact).
-//  - One split: C = alpha * v + beta * C.
+//  - One split (or a whole tile of a split grid, block_tile): C = alpha * v
+//    + beta * C.
 //  - ksplit > 1: the split's values go to its partial slab, which
 //    gemm_f16x3_reduce_kernel adds in increasing split order.  (Adding them
 //    in the tile's last-arriving workgroup instead needs a device-scope
@@ -513,11 +540,11 @@ __device__ __forceinline__ void fix_rejected(const GemmF16Args &p, bool a_kc, bo
 template <bool A_KC, bool B_KC>
 __device__ __forceinline__ void tile_epilogue(const GemmF16Args &p, const int *sexp,
                                               const float *sw, const f32x16 (&acc)[2][2],
-                                              int split, int row0, int col0, int flags, int tid,
-                                              char *lds) {
+                                              int split, bool whole, int row0, int col0,
+                                              int flags, int tid, char *lds) {
   const int lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
   const int half2 = lane >> 5;
-  const bool partial = p.ksplit > 1;
+  const bool partial = p.ksplit > 1 && !whole;
   const bool skip = flags & 1;
   // the spread check (f16-split.h): with a spread row or column in the tile
   // and one split, an element whose |acc| is below its threshold is
@@ -701,15 +728,11 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
   const float m1 = kcnn::f16x3::opaque_m1();
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  // XCD-aware order (gemm_x6_kernel): consecutive logical ids on one XCD
-  const int nb = gridDim.x, b = blockIdx.x;
-  const int xcd = b & 7, q = nb >> 3, rr = nb & 7;
-  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
   int split, tm, tn;
-  tile_of(p, lid, split, tm, tn);
+  const bool whole = block_tile(p, split, tm, tn);
   const int row0 = tm * BM, col0 = tn * BN;
-  const int kbeg = split * p.kps;
-  const int kend = min(p.K, kbeg + p.kps);
+  const int kbeg = whole ? 0 : split * p.kps;
+  const int kend = whole ? p.K : min(p.K, kbeg + p.kps);
   const int T = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   const int klast = kend - kbeg - (T - 1) * BK;  // valid k of the last tile
 
@@ -816,7 +839,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_kernel(GemmF16Args p) {
     }
   }
 
-  tile_epilogue<A_KC, B_KC>(p, sexp, sw, acc, split, row0, col0, flags, tid, lds);
+  tile_epilogue<A_KC, B_KC>(p, sexp, sw, acc, split, whole, row0, col0, flags, tid, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -847,14 +870,11 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
   const float m1 = kcnn::f16x3::opaque_m1();
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int nb = gridDim.x, b = blockIdx.x;
-  const int xcd = b & 7, q = nb >> 3, rr = nb & 7;
-  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
   int split, tm, tn;
-  tile_of(p, lid, split, tm, tn);
+  const bool whole = block_tile(p, split, tm, tn);
   const int row0 = tm * BM, col0 = tn * BN;
-  const int kbeg = split * p.kps;
-  const int kend = min(p.K, kbeg + p.kps);
+  const int kbeg = whole ? 0 : split * p.kps;
+  const int kend = whole ? p.K : min(p.K, kbeg + p.kps);
   const int T = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   const int klast = kend - kbeg - (T - 1) * BK;
 
@@ -990,7 +1010,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_f16x3_fast_kernel(GemmF16Args p) {
     }
   }
 
-  tile_epilogue<A_KC, B_KC>(p, sexp, sw, acc, split, row0, col0, flags, tid, lds);
+  tile_epilogue<A_KC, B_KC>(p, sexp, sw, acc, split, whole, row0, col0, flags, tid, lds);
 }
 
 // Max |x| and min nonzero |x| per row or per column of a pitched fp32 matrix,
@@ -1507,8 +1527,9 @@ __global__ __launch_bounds__(256) void gemm_f16x3_reduce_kernel(GemmF16Args p, i
   // active in every pass, and every group of 64 quads gets its flag written
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
-    int r, c;
-    const uint32_t rej = reduce_quad(p, e, nq, np4, plane, r, c, true);
+    // (a whole tile's quads were stored by its workgroup: no slabs, no rejections)
+    int r = (int)(e / nq), c = (int)(e - (int64_t)r * nq) * 4;
+    const uint32_t rej = in_split_tile(p, r, c) ? reduce_quad(p, e, nq, np4, plane, r, c, true) : 0u;
     // the wave's rejections (ballots: only the active lanes)
     const int n = __builtin_popcountll(__ballot(rej & 1)) + __builtin_popcountll(__ballot(rej & 2)) +
                   __builtin_popcountll(__ballot(rej & 4)) + __builtin_popcountll(__ballot(rej & 8));
@@ -1565,8 +1586,10 @@ __global__ __launch_bounds__(256) void gemm_f16x3_fixup_kernel(GemmF16Args p, in
     for (int j = 0; j < n; ++j) {
       const int64_t e0 = (base + (int64_t)list[j] * gridDim.x + blockIdx.x) << 6;
       const int64_t e = e0 + lane;
-      const bool valid = e < total;
-      int r = 0, c = 0;
+      // (past C: row and column 0, whose loads below stay in bounds)
+      int r = e < total ? (int)(e / nq) : 0;
+      int c = e < total ? (int)(e - (int64_t)r * nq) * 4 : 0;
+      const bool valid = e < total && in_split_tile(p, r, c);
       const uint32_t rej = valid ? reduce_quad(p, e, nq, np4, plane, r, c, false) : 0u;
       if (!rows) {
         const uint64_t mine = (lane & 3) == wave ? rej : 0u;
@@ -1640,22 +1663,30 @@ __global__ __launch_bounds__(256) void gemm_f16x3_fixup_kernel(GemmF16Args p, in
   }
 }
 
-// The split-K count of least modelled time: ceil(tiles s / 256) rounds of
-// one workgroup per CU, each K / s steps at 0.0458 us per k plus 11.1 us of
-// tile prologue and epilogue (fitted to c2's three FC GEMMs on MI355X), and
-// for s > 1 the reduce's (s + 1) M N fp32 reads and writes at 4 TB/s.  (The
-// reduce was unpriced before r06: nnet.config's 4096 x 3454 x 4096 layers
-// took 4 splits and a 86-92 us reduce; one split is 2.4 % faster per step.)
-int choose_ksplit(int64_t tiles, int M, int N, int K) {
-  int best = 1;
-  double best_t = 0.0;
-  for (int s = 1; s <= 4; ++s) {
-    if (s > 1 && K / s < 1024) break;
-    const int64_t rounds = (tiles * s + 255) / 256;
-    double t = (double)rounds * (0.0458 * ((K + s - 1) / s) + 11.1);
-    if (s > 1) t += (double)(s + 1) * M * N * 4.0 / 4.0e6;
-    if (s == 1 || t < best_t) { best_t = t; best = s; }
+// The split-K count (and the whole tiles in front of the split ones,
+// block_tile) of least modelled time: the whole tiles in nwhole / 256 rounds
+// of one workgroup per CU, the split ones in ceil((tiles - nwhole) s / 256)
+// rounds, a round of k steps 0.0458 k + 11.1 us (the tile prologue and
+// epilogue; fitted to c2's three FC GEMMs on MI355X), and for s > 1 the
+// reduce's (s + 1) fp32 reads and writes of the split tiles' share of M N
+// at 4 TB/s.  (The reduce was unpriced before r06: nnet.config's 4096 x 3454
+// x 4096 layers took 4 splits and an 86-92 us reduce, one split being 2.4 %
+// faster per step; c2's 364-tile weight gradient split all its tiles in 2.84
+// rounds, where 256 whole tiles and 108 split ones take 1 + 0.84.)
+int choose_ksplit(int64_t tiles, int M, int N, int K, int *nwhole = nullptr) {
+  auto round = [](int k) { return 0.0458 * k + 11.1; };
+  int best = 1, best_w = 0;
+  double best_t = (double)((tiles + 255) / 256) * round(K);
+  for (int s = 2; s <= 4 && K / s >= 1024; ++s) {
+    const int ks = (K + s - 1) / s;
+    for (int64_t w = 0; w < tiles; w += 256) {
+      const int64_t rest = tiles - w;
+      const double t = (double)(w / 256) * round(K) + (double)((rest * s + 255) / 256) * round(ks) +
+                       (double)(s + 1) * M * N * 4.0 / 4.0e6 * (double)rest / (double)tiles;
+      if (t < best_t) { best_t = t; best = s; best_w = (int)w; }
+    }
   }
+  if (nwhole) *nwhole = best > 1 ? best_w : 0;
   return best;
 }
 
@@ -1834,10 +1865,14 @@ static int gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alph
   a.tiles_m = (M + BM - 1) / BM;
   a.tiles_n = (N + BN - 1) / BN;
   const int64_t tiles = (int64_t)a.tiles_m * a.tiles_n;
-  int s = choose_ksplit(tiles, M, N, K);
-#ifdef KCNN_EXPERIMENTS  // A/B: KCNN_F16X3_KSPLIT forces the split count (0: chosen)
+  int nwhole = 0;
+  int s = choose_ksplit(tiles, M, N, K, &nwhole);
+#ifdef KCNN_EXPERIMENTS  // A/B: KCNN_F16X3_KSPLIT forces the split count (0: chosen), no whole tiles;
+                         // KCNN_F16X3_NOWHOLE keeps the chosen count without whole tiles
   static const int ks_force = KCNN_KNOB("KCNN_F16X3_KSPLIT", 0);
+  static const int no_whole = KCNN_KNOB("KCNN_F16X3_NOWHOLE", 0);
   if (ks_force > 0) s = std::min(ks_force, 4);
+  if (ks_force > 0 || no_whole) nwhole = 0;
 #endif
   const size_t need = s > 1 ? slab_bytes(s, M, N) + flag_bytes(M, N) : 0;
   if (need > ws_bytes || !ws) s = 1;
@@ -1850,14 +1885,17 @@ static int gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alph
   }
   a.ksplit = s;
   a.kps = ((K + s - 1) / s + BK - 1) / BK * BK;
-  const int64_t nb = tiles * s;
-  if (nb >= ((int64_t)1 << 31)) return (int)hipErrorNotSupported;
-  // every offset a workgroup forms (rows of its tile, k up to K + 2 BK) < 2^31
-  auto fits = [&](bool kc, int ld, int R) {
+  // every offset a workgroup forms (rows of its tile, k up to its K span +
+  // 2 BK) < 2^31
+  auto fits = [&](bool kc, int ld, int R, int span) {
     if (kc) return (int64_t)R * ld * 4 + (int64_t)(K + 2 * BK) * 4 < ((int64_t)1 << 31);
-    return (int64_t)(a.kps + 2 * BK) * ld * 4 + (int64_t)R * 4 < ((int64_t)1 << 31);
+    return (int64_t)(span + 2 * BK) * ld * 4 + (int64_t)R * 4 < ((int64_t)1 << 31);
   };
-  if (!fits(a_kc, lda, BM) || !fits(b_kc, ldb, BN)) return (int)hipErrorNotSupported;
+  if (!fits(a_kc, lda, BM, a.kps) || !fits(b_kc, ldb, BN, a.kps)) return (int)hipErrorNotSupported;
+  if (s == 1 || !fits(a_kc, lda, BM, K) || !fits(b_kc, ldb, BN, K)) nwhole = 0;
+  a.nwhole = nwhole;
+  const int64_t nb = nwhole + (tiles - nwhole) * s;
+  if (nb >= ((int64_t)1 << 31)) return (int)hipErrorNotSupported;
   // a row-contiguous operand takes 16-B loads along its rows when they are
   // aligned (pitch % 4 == 0: a quad that starts inside the row count M or N
   // ends inside the pitch; its values past the count feed only C rows or

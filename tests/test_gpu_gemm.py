@@ -139,12 +139,15 @@ def test_gemm_f16x3_row_scales(kc, case, ta, tb, shape):
 
 @pytest.mark.parametrize("mode", [2, 0])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
-@pytest.mark.parametrize("shape", [(260, 140, 300), (300, 260, 4500)])
+@pytest.mark.parametrize("shape", [(260, 140, 300), (300, 260, 4500), (1024, 11616, 2048)])
 def test_gemm_nonfinite_pattern(kc, mode, ta, tb, shape):
     """Inf and NaN operands give sgemm's IEEE pattern (+Inf, -Inf, NaN, and
     the finite elements elsewhere within the bound): f16x3 computes the rows
     and columns they touch as fp32 dot products; rocBLAS for comparison.
-    The second shape splits K over workgroups (in-kernel reduction)."""
+    The second shape splits K over workgroups (in-kernel reduction); the
+    third runs 256 of its 364 tiles whole and splits the other 108 (the
+    split-K cost model's mixed grid, block_tile), with Inf / NaN rows in
+    both parts."""
     import torch
     m, n, k = shape
     a, b, c0 = _mats(torch, m, n, k, ta, tb, seed=5)

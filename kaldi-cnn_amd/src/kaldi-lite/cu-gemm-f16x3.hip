@@ -1443,6 +1443,29 @@ __device__ __forceinline__ uint32_t reduce_quad(const GemmF16Args &p, int64_t e,
       cc[i] = c + i < N ? p.bcnt[c + i] : 0u;
     }
   }
+  // the bias quad too, and the momentum update's W and prev quads (the 16-B
+  // paths' operands, loaded here, not after the tests: one memory round trip
+  // per quad instead of two; host: the update's rows 16-B aligned)
+  float4 w4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), q4 = w4;
+  float4 *wp = nullptr, *qp = nullptr;
+  if (p.mom.W && store) {
+    wp = reinterpret_cast<float4 *>(p.mom.W + (int64_t)r * p.mom.ldw + c);
+    qp = reinterpret_cast<float4 *>(p.mom.prev + (int64_t)r * p.mom.ldp + c);
+    if (c + 4 <= N) {
+      w4 = *wp;
+      q4 = *qp;
+    }
+  }
+  float bv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (p.bias && store) {
+    if (c + 4 <= N && ((uintptr_t)p.bias & 15) == 0) {
+      const float4 b4 = *reinterpret_cast<const float4 *>(p.bias + c);
+      bv[0] = b4.x; bv[1] = b4.y; bv[2] = b4.z; bv[3] = b4.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bv[i] = c + i < N ? p.bias[c + i] : 0.0f;
+    }
+  }
   if (p.ksplit > 1) {
     v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
     for (int k = 2; k < p.ksplit; ++k) {
@@ -1463,9 +1486,6 @@ __device__ __forceinline__ uint32_t reduce_quad(const GemmF16Args &p, int64_t e,
   const bool fin = max(max(bm[0], bm[1]), max(bm[2], bm[3])) < NONFINITE;
   if (p.mom.W && !any && fin) {  // the fused momentum update, 16-B (host: aligned)
     if (store) {
-      float4 *wp = reinterpret_cast<float4 *>(p.mom.W + (int64_t)r * p.mom.ldw + c);
-      float4 *qp = reinterpret_cast<float4 *>(p.mom.prev + (int64_t)r * p.mom.ldp + c);
-      float4 w4 = *wp, q4 = *qp;
       const MomentumEpi &m = p.mom;
       kcnn::momentum_step(p.alpha * sv[0], q4.x, w4.x, m.momentum, m.a_wd, m.a_g);
       kcnn::momentum_step(p.alpha * sv[1], q4.y, w4.y, m.momentum, m.a_wd, m.a_g);
@@ -1485,7 +1505,7 @@ __device__ __forceinline__ uint32_t reduce_quad(const GemmF16Args &p, int64_t e,
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         wv[i] = p.beta == 0.0f ? p.alpha * sv[i] : p.alpha * sv[i] + p.beta * oi[i];
-        if (p.bias) wv[i] += p.bias[c + i];
+        if (p.bias) wv[i] += bv[i];
       }
       *reinterpret_cast<float4 *>(o) = make_float4(wv[0], wv[1], wv[2], wv[3]);
     }

@@ -54,6 +54,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <mutex>
 #include <type_traits>
 
 #include "cnslmat/f16-split.h"
@@ -105,6 +106,8 @@ struct GemmF16Args {
   int dbg;                       // KCNN_EXPERIMENTS builds: A/B switches
   int kps, ksplit, tiles_m, tiles_n;
   int nwhole;                    // ksplit > 1: the first nwhole tiles (a multiple of 256) whole
+  int fix_local;                 // ksplit > 1: no fix-up launch; the reduce recomputes every rejection
+  uint32_t *fix_report;          // nullable (host memory): set to 1 when a group would be deferred
   float alpha, beta;
 };
 
@@ -1553,10 +1556,11 @@ __global__ __launch_bounds__(256) void gemm_f16x3_reduce_kernel(GemmF16Args p, i
     // the wave's rejections (ballots: only the active lanes)
     const int n = __builtin_popcountll(__ballot(rej & 1)) + __builtin_popcountll(__ballot(rej & 2)) +
                   __builtin_popcountll(__ballot(rej & 4)) + __builtin_popcountll(__ballot(rej & 8));
-    const bool defer = n > REJ_LOCAL;
+    const bool defer = n > REJ_LOCAL && !p.fix_local;
     if (lane == 0) {
       p.rflag[e >> 6] = defer ? 1u : 0u;
       if (defer) p.rflag[(total + 63) >> 6] = p.gen;
+      if (n > REJ_LOCAL && p.fix_report) *p.fix_report = 1u;
     }
     if (n == 0 || defer) continue;
     fix_rejected(p, a_kc != 0, b_kc != 0, rej, lane, [&](int l, int bit, int &row, int &col) {
@@ -1857,6 +1861,53 @@ extern "C" int kl_gemm_stats3(const float *X0, int rows0, int cols0, int ld0, in
 extern "C" size_t kl_gemm_f16x3_workspace_bytes(int M, int N, int K) {
   return partial_bytes(M, N, K);
 }
+// The fix-up launch of a split-K call (an exit-at-once kernel of 4.4 us in
+// all but the rare calls with a spread group, FIX_GRID) is skipped for a call
+// site (shape, transposes, momentum or not) whose previous call deferred no
+// group: the site's word in host memory, cleared by the host at each launch
+// and set by the reduce when a group would have been deferred, is read at
+// the next launch.  A skipped call's reduce recomputes every rejection itself
+// (fix_local), so a stale or wrong guess costs time, never a result.  Up to
+// FIX_SITES sites; the others always launch the fix-up.
+constexpr int FIX_SITES = 256;
+struct FixSites {
+  std::mutex mu;
+  uint32_t *flags = nullptr;  // pinned host words (1: the fix-up was needed or is unknown)
+  uint32_t *dflags = nullptr; // the same words' device address
+  int64_t key[FIX_SITES][6];
+  int n = 0;
+  bool failed = false;
+};
+// the word of this site, nullptr when there is none (table full, no host memory)
+static uint32_t *fix_site(int M, int N, int K, int ta, int tb, int mom, uint32_t **dev) {
+  static FixSites fs;
+  std::lock_guard<std::mutex> lk(fs.mu);
+  if (!fs.flags && !fs.failed) {
+    void *h = nullptr, *d = nullptr;
+    if (hipHostMalloc(&h, FIX_SITES * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) ==
+            hipSuccess &&
+        hipHostGetDevicePointer(&d, h, 0) == hipSuccess) {
+      fs.flags = static_cast<uint32_t *>(h);
+      fs.dflags = static_cast<uint32_t *>(d);
+    } else {
+      (void)hipGetLastError();
+      fs.failed = true;
+    }
+  }
+  if (!fs.flags) return nullptr;
+  const int64_t k[6] = {M, N, K, ta, tb, mom};
+  int i = 0;
+  for (; i < fs.n; ++i)
+    if (std::equal(k, k + 6, fs.key[i])) break;
+  if (i == fs.n) {
+    if (fs.n == FIX_SITES) return nullptr;
+    std::copy(k, k + 6, fs.key[fs.n++]);
+    __atomic_store_n(fs.flags + i, 1u, __ATOMIC_RELAXED);
+  }
+  *dev = fs.dflags + i;
+  return fs.flags + i;
+}
+
 static int gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alpha,
                          const float *A, int lda, const float *B, int ldb, float beta, float *C,
                          int ldc, const uint32_t *amax, const uint32_t *bmax, const float *bias,
@@ -1926,13 +1977,24 @@ static int gemm_f16x3_st(int transA, int transB, int M, int N, int K, float alph
     static const int tr = KCNN_KNOB("KCNN_F16X3_TR", 1);
     return tr && ld % 4 == 0 && (uintptr_t)ptr % 16 == 0 ? (int)LT : (int)LR;
   };
+  bool fix_launch = true;
+  if (s > 1) {
+    uint32_t *dev = nullptr;
+    uint32_t *site = fix_site(M, N, K, transA != 0, transB != 0, a.mom.W != nullptr, &dev);
+    if (site) {
+      fix_launch = __atomic_load_n(site, __ATOMIC_RELAXED) != 0;
+      __atomic_store_n(site, 0u, __ATOMIC_RELAXED);
+      a.fix_report = dev;
+      a.fix_local = fix_launch ? 0 : 1;
+    }
+  }
   launch(mode(a_kc, A, lda), mode(b_kc, B, ldb), a, (unsigned)nb, st);
   int rc = kcnn::launch_status();
   if (rc || s == 1) return rc;
   hipLaunchKernelGGL(gemm_f16x3_reduce_kernel, dim3(kcnn::grid_for((int64_t)M * ((N + 3) / 4))),
                      dim3(256), 0, st, a, a_kc ? 1 : 0, b_kc ? 1 : 0);
   rc = kcnn::launch_status();
-  if (rc) return rc;
+  if (rc || !fix_launch) return rc;
   // op(B) row-contiguous: the fixup's 16-B loads along its rows
   const int rows = !b_kc && ldb % 4 == 0 && (uintptr_t)B % 16 == 0 && N % 4 == 0;
   const int64_t slots = ((int64_t)M * ((N + 3) / 4) + 63) / 64;

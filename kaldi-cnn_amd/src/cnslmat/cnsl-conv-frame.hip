@@ -1903,7 +1903,7 @@ __global__ __launch_bounds__(256) void reduce_pass1(const float *__restrict__ in
 // (e % inner, e / inner) : (e / inner, e % inner); e >= nw -> gb[e - nw].
 // (Two passes of 32-row groups spent ~14 us of latency at c2, for 3.3 MB.)
 // u.W != NULL (conv-update.h): the sums step W / prev (momentum_step) and b
-// instead of being stored in gW / gb (gk_layout 0 only).
+// instead of being stored in gW / gb (W and prev with gW's (row, col)).
 __global__ __launch_bounds__(256) void reduce_splits_kernel(
     const float *__restrict__ in, int S, int E, int nw, int inner, int gk_layout,
     float *__restrict__ gW, int gws, float *__restrict__ gb, ConvUpdateEpi u) {
@@ -2506,14 +2506,24 @@ size_t kcnn_reduce_splits_ws(int S, int E) {
 }
 
 // Generic: in [S][E] -> out (with the gW/gb mapping of the implicit-GEMM
-// wgrad: e = g*Kdim + k for e < G*Kdim); tmp is unused (one pass).
+// wgrad: e = g*Kdim + k for e < G*Kdim); tmp is unused (one pass).  The
+// caller's update request for this layer's W (conv-update.h: Kdim = inner,
+// G = nw / inner) is applied here instead of storing gW / gb, as the frame
+// kernels' reduction does (the long-kernel weight gradients run after the
+// data gradient, so W is stepped after its last read).
 int kcnn_reduce_splits_wgrad(const float *in, int S, int E, float *tmp, int nw,
                              int inner, float *gW, int gws, float *gb,
                              hipStream_t st) {
   (void)tmp;
+  ConvUpdateEpi *u = kcnn_conv_update_current();
+  if (u && !(gW && gb && inner > 0 && u->Kdim == inner && (int64_t)u->G * inner == nw &&
+             E == nw + u->G))
+    u = nullptr;
   hipLaunchKernelGGL(reduce_splits_kernel, dim3((E + 63) / 64), dim3(256), 0, st, in, S, E,
-                     nw, inner, 1, gW, gws, gb, ConvUpdateEpi{});
-  return (int)hipGetLastError();
+                     nw, inner, 1, gW, gws, gb, u ? *u : ConvUpdateEpi{});
+  const int rc = (int)hipGetLastError();
+  if (rc == 0 && u) u->applied = 1;
+  return rc;
 }
 
 int kcnn_reduce_splits_pass1(const float *in, int S, int E, float *tmp,

@@ -347,6 +347,37 @@ def test_fc_update_equals_gradient_then_apply(kc, I, Od, N, spread):
         assert_same(out[0][k], out[1][k], f"FC param {k}")
 
 
+@pytest.mark.parametrize("name,N", [("c2", 600), ("nnet_cfg_l1", 2048), ("nnet_cfg_l2", 2048),
+                                    ("c5_C3_pad", 1024), ("c5_C4", 1024)])
+def test_conv_update_equals_gradient_then_apply(kc, name, N):
+    """ConvolutionComponent's update inside Backprop (:738-777) gives the
+    bits of BackpropGradient + ApplyGradient (the DP step's split), and the
+    same data gradient (taken with the pre-update kernel).  The frame kernels
+    and the long-kernel weight gradients (nnet.config's and c5's layers:
+    kcnn_reduce_splits_wgrad) apply the momentum step in their gradient
+    reduction (conv-update.h); the other paths run ApplyGradient."""
+    H, W, C, kh, kw, G, ph, pw = CONVS[name]
+    line = conv_line(H, W, C, kh, kw, G, ph, pw) + " weight-decay=0.0005 momentum=0.9"
+    oh, ow = H + 2 * ph - kh + 1, W + 2 * pw - kw + 1
+    r = rng(21)
+    params = [randn(r, (kh * kw * C, G), 0.05), randn(r, (G,), 0.5),
+              randn(r, (kh * kw * C, G), 0.01)]
+    x, dy = dev(randn(r, (N, H * W * C))), dev(randn(r, (N, oh * ow * G), 0.1))
+    out = []
+    for fused in (True, False):
+        comp = kc.Component.NewFromString(line)
+        for which, v in enumerate(params):
+            comp.SetParam(which, dev(v))
+        if fused:
+            dx = comp.Backprop(x, None, dy, update=True)
+        else:
+            dx, g = comp.BackpropGradient(x, dy)
+            comp.ApplyGradient(g, N)
+        out.append([host(dx)] + [host(comp.GetParam(w)) for w in range(3)])
+    for k, what in enumerate(["dX", "W", "b", "prev_grad"]):
+        assert_same(out[0][k], out[1][k], f"conv {name} {what}")
+
+
 @pytest.mark.parametrize("binary", [True, False])
 def test_read_write_roundtrip(kc, tmp_path, binary):
     comps = [
